@@ -1,0 +1,258 @@
+/*
+ * zp.h -- C ABI of libzp.so, the MI355X (gfx950) implementation of ZebraPose's
+ * data-parallel hot path.
+ *
+ * Plain C: pointers, sizes and POD structs only; no torch types.  Every pointer
+ * argument named x / y / w / res / ... is a DEVICE pointer (caller-owned memory,
+ * e.g. the PyTorch caching allocator); `stream` is a hipStream_t (NULL = legacy
+ * default stream).  All calls are stream-ordered and never synchronise the host.
+ * Return value: 0 (ZP_OK) or an error code; zp_last_error() describes the last
+ * failure of the calling thread.
+ *
+ * Layouts.  Activations are NHWC ("channels last") with a row stride `ld*`
+ * (elements per pixel) and a channel offset `c*0`, so a producer can write
+ * straight into a channel slice of a concat buffer (the reference's torch.cat,
+ * aspp.py:101-112).  Packed conv weights are [rows_pad][k_pad] with
+ * k = tap * Cin + cin ("tap-major implicit GEMM").
+ *
+ * Reference interfaces replaced (file:line in lyltc1/ZebraPose):
+ *   zp_conv2d          nn.Conv2d / nn.ConvTranspose2d + BatchNorm2d + ReLU (+ residual add)
+ *                      as called at model/resnet.py:41-51, torchvision resnet children
+ *                      (resnet.py:191-199), model/aspp.py:60-80, 89-112
+ *   zp_conv2d_wgrad    their weight gradients (autograd of the same modules, train_v6.py:337)
+ *   zp_bn_*            BatchNorm2d train/eval semantics (resnet.py:29, aspp.py:12..)
+ *   zp_maxpool3s2      torchvision maxpool (resnet.py:197), and its backward
+ *   zp_global_avgpool  aspp.py:94  AdaptiveAvgPool2d(1)   (+ zp_broadcast_hw = aspp.py:96 bilinear 1x1->HxW)
+ *   zp_code_loss       BinaryCodeLoss / HammingLoss / BinaryLossWeighted (model/BinaryCodeNet.py:8-81,
+ *                      96-109) as driven at train_v6.py:325-327;  zp_mask_loss  MaskLoss (:84-93)
+ *   zp_threshold       common_ops.py:5-19 (sigmoid > 0.5 -> {0,1})
+ *   zp_decode          binary_code_helper/CNN_output_to_pose.py:34-64, 100-130 and
+ *                      class_id_encoder_decoder.py:17-28 (bits -> id -> LUT -> 2D/3D)
+ *   zp_lut_coarsen     binary_code_helper/generate_new_dict.py:4-33 (ignore_bit LUT)
+ *   zp_adam            torch.optim.Adam step used by train_v6.py:268-269, 338
+ */
+#ifndef ZP_H_
+#define ZP_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ZP_ABI_VERSION 1
+
+#define ZP_OK 0
+#define ZP_ERR_ARG 1
+#define ZP_ERR_HIP 2
+
+/* element types of activations / packed weights */
+#define ZP_F32 0
+#define ZP_BF16 1
+
+/* zp_conv_args.out_mode */
+#define ZP_OUT_NHWC 0       /* y[n, oy, ox, cy0 + c] (ldy elements per pixel), dtype of the call */
+#define ZP_OUT_HEAD_NCHW 1  /* c == 0 -> y (f32 [N,1,OH,OW]); c >= 1 -> y2 (f32 [N,Cout-1,OH,OW]) */
+#define ZP_OUT_NHWC_F32 2   /* y f32 NHWC regardless of dtype (raw conv output for train-mode BN) */
+
+#define ZP_MAX_TAPS 64
+#define ZP_MAX_SUB 4
+
+/* One implicit-GEMM sub-problem.  Grid point (n, gy, gx), tap t reads input pixel
+ * (gy*sy + ty[t], gx*sx + tx[t]) (zero outside) and writes output pixel
+ * (gy*oys + oyo, gx*oxs + oxo).  This covers strided/dilated convs, the four
+ * sub-pixel phases of ConvTranspose2d(3, s2, p1, op1), and the data-gradient
+ * convs of both. */
+typedef struct zp_conv_sub {
+  const void* w;        /* packed weights [rows_pad][k_pad], dtype of the call */
+  const float* scale;   /* per-output-channel multiplier (folded BN) or NULL (=1) */
+  const float* shift;   /* per-output-channel addend (folded BN + bias) or NULL (=0) */
+  void* y;              /* output (see out_mode) */
+  void* y2;             /* second output (ZP_OUT_HEAD_NCHW) */
+  int ldy, cy0, OH, OW;
+  int oys, oyo, oxs, oxo;
+  int ntaps;            /* taps in ty/tx (general path) */
+  int kw, dil, pad;     /* arithmetic taps for the small-Cin path: t -> ((t/kw)*dil-pad, (t%kw)*dil-pad) */
+  signed char ty[ZP_MAX_TAPS];
+  signed char tx[ZP_MAX_TAPS];
+} zp_conv_sub;
+
+typedef struct zp_conv_args {
+  int dtype;            /* ZP_F32 (exact-f32 MFMA path) or ZP_BF16 (bf16 MFMA, fp32 accumulate) */
+  const void* x;        /* input NHWC */
+  int ldx, cx0, IH, IW, Cin;   /* Cin: multiple of 64 (bf16) / 32 (f32), or 8 (small-Cin path) */
+  int N, GH, GW, sy, sx;       /* GEMM grid (pixels) and input stride */
+  int Cout, k_pad;             /* k_pad: weight row length (elements) */
+  int w_rows;                  /* packed weight rows (>= Cout, multiple of the cout tile: use
+                                  zp_conv_rows_pad(Cout)) */
+  const void* res;             /* residual NHWC (same pixel as y) or NULL */
+  int ldr, cr0;
+  int relu, out_mode;
+  float* stats;                /* if non-NULL (raw output only: no scale/shift/res/relu): per-channel
+                                  partial statistics of the stored value, [3][parts][Cout] =
+                                  (count, mean, centred M2), parts = zp_conv2d_stat_parts() */
+  int nsub;
+  zp_conv_sub sub[ZP_MAX_SUB];
+} zp_conv_args;
+
+int zp_abi_version(void);
+const char* zp_last_error(void);
+
+/* ---- convolution (forward and data-gradient) ---------------------------------------- */
+int zp_conv2d(const zp_conv_args* a, void* stream);
+/* packed weight row count zp_conv2d expects for Cout output channels */
+int zp_conv_rows_pad(int Cout);
+/* number of pixel tiles (grid_x) a zp_conv2d launch with these args uses */
+int zp_conv2d_grid(const zp_conv_args* a);
+/* number of partial-sum slots `stats` needs: 2 * grid_x * nsub */
+int zp_conv2d_stat_parts(const zp_conv_args* a);
+
+/* Pack an f32 weight tensor src[d0][d1][kh][kw] into dst[rows_pad][k_pad] (dtype), taps
+ * (ky[t], kx[t]), t < ntaps:
+ *   transposed == 0: dst[r][t*cstride + c] = src[r][c][ky[t]][kx[t]]   (conv forward: OIHW)
+ *   transposed == 1: dst[r][t*cstride + c] = src[c][r][ky[t]][kx[t]]   (ConvT forward, conv dgrad)
+ * ky/kx are HOST arrays (<= ZP_MAX_TAPS).  Padding rows / columns / channels are zeroed. */
+int zp_pack_weight(const float* src, int d0, int d1, int kh, int kw, int transposed, int ntaps,
+                   const int* ky, const int* kx, int cstride, int dtype, void* dst, int rows_pad,
+                   int k_pad, void* stream);
+
+/* ---- weight gradient ------------------------------------------------------------------
+ * dw[co][ci][ky][kx] (f32, layout of the conv's own weight; transposed_w=1 for ConvT's
+ * [ci][co][kh][kw]) = sum over grid points and taps of dy[out pixel][co] * x[in pixel][ci],
+ * with the same sub/tap geometry as the forward zp_conv_args (sub[].y = dy, dtype = act dtype).
+ * `ws` is a device workspace of zp_conv2d_wgrad_ws_bytes() bytes. accumulate != 0 adds to dw. */
+typedef struct zp_wgrad_args {
+  int dtype;
+  const void* x; int ldx, cx0, IH, IW, Cin;
+  int N, GH, GW, sy, sx;
+  int Cout;
+  int Cw;                      /* input channels of the weight tensor (<= Cin; Cin may be padded) */
+  int kh, kw, transposed_w;
+  int nsub;
+  struct {
+    const void* dy; int lddy, cdy0, OH, OW, oys, oyo, oxs, oxo;
+    int ntaps;
+    signed char ky[ZP_MAX_TAPS], kx[ZP_MAX_TAPS];   /* weight tap of each geometric tap */
+    signed char ty[ZP_MAX_TAPS], tx[ZP_MAX_TAPS];
+  } sub[ZP_MAX_SUB];
+  float* dw;
+  int accumulate;
+} zp_wgrad_args;
+long long zp_conv2d_wgrad_ws_bytes(const zp_wgrad_args* a);
+int zp_conv2d_wgrad(const zp_wgrad_args* a, void* ws, void* stream);
+
+/* ---- batch norm ---------------------------------------------------------------------- */
+/* eval: scale = gamma / sqrt(var + eps); shift = beta + (bias - mean) * scale (bias may be NULL) */
+int zp_bn_fold(const float* gamma, const float* beta, const float* mean, const float* var,
+               const float* conv_bias, float eps, int C, float* scale, float* shift, void* stream);
+/* train: merge the [3][parts][C] partial statistics of zp_conv2d(stats) (count = P, checked),
+ * update running stats (momentum, unbiased var; the conv bias, if any, is added to the mean)
+ * and emit scale/shift for the apply pass, plus save[2][C] = (mean, invstd) of the raw values. */
+int zp_bn_train_finalize(const float* partials, int parts, int C, long long count, float eps,
+                         float momentum, const float* gamma, const float* beta, const float* conv_bias,
+                         float* running_mean, float* running_var, int64_t* num_batches_tracked,
+                         float* scale, float* shift, float* save, void* stream);
+/* y[p, cy0+c] = act(x[p, c]*scale[c] + shift[c] (+ res[p, cr0+c])), x: raw conv output [P][C] */
+int zp_bn_apply(const void* x, int P, int C, const float* scale, const float* shift,
+                const void* res, int ldr, int cr0, int relu, int dtype, void* y, int ldy, int cy0,
+                void* stream);
+/* number of partial slots zp_bn_bwd_reduce uses for P pixels (partials needs [2][parts+1][C]) */
+int zp_bn_bwd_parts(int P, int C);
+/* backward of y = act(bn(x) (+res)):  g = dy * (y > 0 if relu);  xhat = (x - mean) * invstd;
+ * partials[0][k][c] = sum g, partials[1][k][c] = sum g*xhat over pixel block k (x == NULL: only sum g);
+ * then totals into partials[.][parts][c] and (optional) dgamma = sum g*xhat, dbeta = sum g
+ * (written, or added if accumulate). */
+int zp_bn_bwd_reduce(const void* dy, int lddy, int cdy0, const void* y, int ldy, int cy0,
+                     const void* x, int P, int C, const float* save, int relu, int dtype,
+                     float* partials, float* dgamma, float* dbeta, int accumulate, void* stream);
+/* dx[p][c] = gamma*invstd*(g - sum_g/P - xhat*sum_gx/P)  (dx dtype, [P][C]);
+ * dres (optional) [p, cdres0+c] = g, or += g if res_accumulate */
+int zp_bn_bwd_apply(const void* dy, int lddy, int cdy0, const void* y, int ldy, int cy0,
+                    const void* x, int P, int C, const float* save, const float* partials,
+                    const float* gamma, int relu, int dtype, void* dx, void* dres, int lddres,
+                    int cdres0, int res_accumulate, void* stream);
+
+/* ---- layout / pooling ---------------------------------------------------------------- */
+/* x f32 NCHW [B][C][H][W] -> y NHWC [B][H][W][cpad] (dtype), channels C..cpad-1 zero */
+int zp_nchw_to_nhwc(const float* x, int B, int C, int H, int W, int cpad, int dtype, void* y,
+                    void* stream);
+/* 3x3 / stride 2 / pad 1 max pool, NHWC slices; C multiple of 8 */
+int zp_maxpool3s2(const void* x, int B, int IH, int IW, int ldx, int cx0, int C, int dtype,
+                  void* y, int OH, int OW, int ldy, int cy0, void* stream);
+int zp_maxpool3s2_bwd(const void* x, int ldx, int cx0, const void* dy, int lddy, int cdy0,
+                      int B, int IH, int IW, int C, int OH, int OW, int dtype,
+                      void* dx, int lddx, int cdx0, int accumulate, void* stream);
+/* y[b][c] = mean over H*W of x (f32 accumulate), y dtype */
+int zp_global_avgpool(const void* x, int B, int H, int W, int ldx, int cx0, int C, int dtype,
+                      void* y, void* stream);
+/* y[b, :, :, cy0 + c] = src[b][c] */
+int zp_broadcast_hw(const void* src, int B, int C, int dtype, void* y, int H, int W, int ldy, int cy0,
+                    void* stream);
+/* backward of zp_broadcast_hw: out[b][c] (dtype) = sum over H*W of dy[b, h, w, cdy0 + c] */
+int zp_sum_hw(const void* dy, int B, int H, int W, int lddy, int cdy0, int C, int dtype, void* out,
+              void* stream);
+/* backward of zp_global_avgpool: y[b, h, w, cy0 + c] (+)= src[b][c] * mul  (src dtype) */
+int zp_add_broadcast_hw(const void* src, float mul, int B, int C, int dtype, void* y, int H, int W,
+                        int ldy, int cy0, int accumulate, void* stream);
+/* generic NHWC slice copy / add / cast: y[p, cy0+c] (+)= x[p, cx0+c]  */
+int zp_copy_slice(const void* x, int ldx, int cx0, int xdtype, void* y, int ldy, int cy0, int ydtype,
+                  int P, int C, int accumulate, void* stream);
+/* head gradient f32 NCHW (dmask [B][1][H][W], dcode [B][L][H][W]) -> y NHWC [B][H][W][ldy]
+ * (dtype), channel 0 = mask, 1..L = code, channels L+1..ldy-1 zeroed */
+int zp_head_grad_to_nhwc(const float* dmask, const float* dcode, int B, int L, int H, int W, int ldy,
+                         int dtype, void* y, void* stream);
+
+/* ---- loss ---------------------------------------------------------------------------- */
+/* loss_b of BinaryCodeLoss('BCE', mask_binary_code_loss=mask_code, 2, use_hist)
+ * (model/BinaryCodeNet.py:34-81 with HammingLoss :100-109), f64 like the reference:
+ *   code_logits f32 [B][L][H][W];
+ *   mask: mask01 (f64 [B][1][H][W], rounded and clamped to {0,1} as HammingLoss does) or, if
+ *         mask01 == NULL, mask_logits (f32 [B][1][H][W]) thresholded like train_v6.py:325-326;
+ *   gt [B][L][H][W]: f64 if gt_f64 else u8 (0/1);
+ *   hist_state f64[L+1]: [0..L) the histogram EMA (module state), [L] = 0 before the first call;
+ *   out f64[2] = (loss_b, mean hamming loss); coef f64[L] = w_i / sum(w) / (B*H*W), kept for the
+ *   backward.  ws: zp_code_loss_ws_bytes(B, L, H, W) bytes. */
+long long zp_code_loss_ws_bytes(int B, int L, int H, int W);
+int zp_code_loss(const float* code_logits, const double* mask01, const float* mask_logits, const void* gt,
+                 int gt_f64, int B, int L, int H, int W, int use_hist, int mask_code, double* hist_state,
+                 double* out, double* coef, void* ws, void* stream);
+/* dcode[b][i][p] = gscale * coef[i] * (sigmoid(z) - t) * (mask_code ? m : 1), z = (mask_code ? m : 1) * code;
+ * gscale = *grad_scale (f64 device scalar) or 1 if NULL */
+int zp_code_loss_bwd(const float* code_logits, const double* mask01, const float* mask_logits, const void* gt,
+                     int gt_f64, int B, int L, int H, int W, int mask_code, const double* coef,
+                     const double* grad_scale, float* dcode, void* stream);
+/* MaskLoss (BinaryCodeNet.py:89-93): out f32[1] = mean |sigmoid(x) - g| over n elements
+ * (x = mask logits [B][1][H][W] viewed as [B][H][W]); ws: zp_mask_loss_ws_bytes(n) bytes */
+long long zp_mask_loss_ws_bytes(long long n);
+int zp_mask_loss(const float* mask_logits, const float* gt_mask, long long n, float* out, void* ws, void* stream);
+/* dmask = gscale * sign(sigmoid(x) - g) * sigmoid(x) * (1 - sigmoid(x)) / n  (gscale f32 device scalar or NULL) */
+int zp_mask_loss_bwd(const float* mask_logits, const float* gt_mask, long long n, const float* grad_scale,
+                     float* dmask, void* stream);
+
+/* ---- decode -------------------------------------------------------------------------- */
+/* bits (u8, or f64 if out_f64) = logits > 8.940696716308594e-08f  (CPU fp32 sigmoid(x) > 0.5) */
+int zp_threshold(const float* logits, long long n, int out_f64, void* bits, void* stream);
+/* Per crop b (lut_index[b] selects the LUT when several objects are batched, NULL = 0):
+ *   mask = threshold(mask_logits), id = sum_i bit_i << (L-1-i) over code channels 0..L-1,
+ *   in row-major order of the mask pixels: xy = (int)(bbox[2]/bbox_size * x + bbox[0]),
+ *   (int)(bbox[3]/bbox_size * y + bbox[1]) (truncation toward zero), xyz = lut[id] or 0 if any
+ *   component is NaN; counts[b] = number of mask pixels.  ids (optional) = id image [B][H][W].
+ *   mask_logits f32 [B][1][H][W], code_logits f32 [B][Lfull][H][W], lut f32 [n_lut][2^L][3],
+ *   bbox int32 [B][4], xy int32 [B][H*W][2], xyz f32 [B][H*W][3].
+ *   ws: zp_decode_ws_bytes(B, H, W) bytes. */
+long long zp_decode_ws_bytes(int B, int H, int W);
+int zp_decode(const float* mask_logits, const float* code_logits, int B, int H, int W, int Lfull,
+              int L, const float* lut, const int* lut_index, const int* bbox, int bbox_size,
+              int* ids, int* counts, int* xy, float* xyz, void* ws, void* stream);
+/* out[n][3] (f32) = mean over the 2^(old-new) children of lut64 (f64, summed in order) */
+int zp_lut_coarsen(const double* lut64, int old_bits, int new_bits, float* out, void* stream);
+
+/* ---- optimizer ----------------------------------------------------------------------- */
+/* torch.optim.Adam (no weight decay, amsgrad off) over one flat f32 buffer; step >= 1 */
+int zp_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long long n,
+            double lr, double beta1, double beta2, double eps, long long step, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ZP_H_ */

@@ -1,0 +1,148 @@
+"""Unit-level parity of the libzp conv / BN / pooling kernels against a plain PyTorch fp32 CPU
+reference of the same op (conv or transposed conv + train-mode BatchNorm + residual + ReLU,
+forward and backward), for every geometry the network uses."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+GEOMS = [
+    # kind, cin, cout, k, s, p, d, bias, H
+    ("conv", 64, 64, 3, 1, 1, 1, False, 16),
+    ("conv", 64, 128, 3, 2, 1, 1, False, 16),
+    ("conv", 64, 128, 1, 2, 0, 1, False, 16),
+    ("conv", 128, 256, 3, 1, 2, 2, False, 12),
+    ("conv", 256, 256, 3, 1, 4, 4, False, 12),
+    ("conv", 512, 256, 3, 1, 6, 6, True, 8),
+    ("conv", 512, 256, 3, 1, 18, 18, True, 8),
+    ("conv", 1280, 256, 1, 1, 0, 1, True, 8),
+    ("convT", 256, 256, 3, 2, 1, 1, False, 8),
+    ("convT", 320, 256, 3, 2, 1, 1, False, 8),
+]
+
+
+def _mk(kind, cin, cout, k, s, p, d, bias):
+    from zebrapose_amd.model import layers as LY
+    if kind == "conv":
+        conv = LY.Conv2d(cin, cout, k, s, p, d, bias=bias)
+    else:
+        conv = LY.ConvTranspose2d(cin, cout, k, s, p, output_padding=1, bias=False)
+    bn = LY.BatchNorm2d(cout)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.normal_(0, 0.1)
+        bn.running_mean.normal_(0, 0.1)
+        bn.running_var.uniform_(0.5, 1.5)
+    return conv, bn
+
+
+def _ref_unit(kind, conv, bn, x, res, relu, train, s, p, d):
+    w = conv.weight.detach().clone().requires_grad_(True)
+    b = conv.bias.detach().clone().requires_grad_(True) if conv.bias is not None else None
+    g = bn.weight.detach().clone().requires_grad_(True)
+    be = bn.bias.detach().clone().requires_grad_(True)
+    rm, rv = bn.running_mean.detach().clone(), bn.running_var.detach().clone()
+    xx = x.clone().requires_grad_(True)
+    if kind == "conv":
+        y = F.conv2d(xx, w, b, s, p, d)
+    else:
+        y = F.conv_transpose2d(xx, w, None, 2, 1, 1)
+    y = F.batch_norm(y, rm, rv, g, be, training=train, momentum=0.1, eps=1e-5)
+    if res is not None:
+        y = y + res
+    if relu:
+        y = F.relu(y)
+    return y, (xx, w, b, g, be), (rm, rv)
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("geom", GEOMS, ids=[f"{g[0]}{g[1]}-{g[2]}k{g[3]}s{g[4]}d{g[6]}" for g in GEOMS])
+@pytest.mark.parametrize("train", [False, True])
+def test_unit(gpu, geom, prec, train):
+    from zebrapose_amd.engine import Engine, Unit, Act, Tape
+    kind, cin, cout, k, s, p, d, bias, H = geom
+    torch.manual_seed(0)
+    B = 2
+    conv, bn = _mk(kind, cin, cout, k, s, p, d, bias)
+    x = torch.randn(B, cin, H, H)
+    unit = Unit(conv, bn, relu=True)
+    OH, OW = unit.out_hw(H, H)
+    use_res = (kind == "conv" and s == 1 and cin == cout)
+    res = torch.randn(B, cout, OH, OW) if use_res else None
+    y_ref, leaves, (rm_ref, rv_ref) = _ref_unit(kind, conv, bn, x, res, True, train, s, p, d)
+    gout = torch.randn_like(y_ref)
+    if train:
+        y_ref.backward(gout)
+
+    dt = torch.float32 if prec == "fp32" else torch.bfloat16
+    convg, bng = conv.to(gpu), bn.to(gpu)
+    eng = Engine(torch.nn.Module(), dt)
+    xa = Act(x.permute(0, 2, 3, 1).contiguous().to(gpu, dt))
+    ra = Act(res.permute(0, 2, 3, 1).contiguous().to(gpu, dt)) if res is not None else None
+    oa = Act(torch.empty(B, OH, OW, cout, device=gpu, dtype=dt))
+    tape = Tape() if train else None
+    if not train:
+        convg.eval(), bng.eval()
+    eng.unit_fwd(unit, xa, oa, tape, res=ra)
+    y = oa.buf.float().permute(0, 3, 1, 2).cpu()
+    tol = 2e-4 if prec == "fp32" else 3e-2
+    scale = y_ref.abs().max().item()
+    err = (y - y_ref.detach()).abs().max().item()
+    assert err <= tol * max(1.0, scale), f"forward max|d| {err} (scale {scale})"
+    if not train:
+        return
+    torch.cuda.synchronize()
+    assert torch.allclose(bng.running_mean.cpu(), rm_ref, atol=1e-4 if prec == "fp32" else 1e-2)
+    assert torch.allclose(bng.running_var.cpu(), rv_ref, rtol=1e-3 if prec == "fp32" else 3e-2)
+    gmap = {oa.buf.data_ptr(): gout.permute(0, 2, 3, 1).contiguous().to(gpu, dt)}
+    grads = {}
+    eng.unit_bwd(tape.recs[0], gmap, grads)
+    xx, w, b, g, be = leaves
+    checks = [("dW", grads[convg.weight], w.grad), ("dgamma", grads[bng.weight], g.grad),
+              ("dbeta", grads[bng.bias], be.grad)]
+    gx = gmap[xa.buf.data_ptr()].float().permute(0, 3, 1, 2).cpu()
+    checks.append(("dx", gx, xx.grad))
+    if ra is not None:
+        gr = gmap[ra.buf.data_ptr()].float().permute(0, 3, 1, 2).cpu()
+        checks.append(("dres", gr, gout * (y_ref.detach() > 0)))
+    # fp32: elementwise (max |d| / max |ref|); bf16: relative L2 -- a bf16 activation that lands on
+    # the other side of 0 flips a ReLU gate, so bf16 gradients are compared in norm, not per element.
+    errs = []
+    for name, got, want in checks:
+        got = got.float().cpu()
+        if prec == "fp32":
+            sc = want.abs().max().item()
+            e = (got - want).abs().max().item()
+            if e > 1e-3 * max(sc, 1e-6):
+                errs.append(f"{name}: max|d| {e:.4g} vs scale {sc:.4g}")
+        else:
+            rel = ((got - want).norm() / max(want.norm().item(), 1e-12)).item()
+            if rel > 0.05:
+                errs.append(f"{name}: rel L2 {rel:.4g}")
+    assert not errs, "; ".join(errs)
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_maxpool(gpu, prec):
+    from zebrapose_amd import _lib as L
+    torch.manual_seed(1)
+    dt = torch.float32 if prec == "fp32" else torch.bfloat16
+    x = torch.randn(2, 64, 17, 16).to(dt).float()
+    xx = x.clone().requires_grad_(True)
+    y = F.max_pool2d(xx, 3, 2, 1)
+    g = torch.randn_like(y).to(dt).float()
+    y.backward(g)
+    xd = x.permute(0, 2, 3, 1).contiguous().to(gpu, dt)
+    OH, OW = y.shape[2], y.shape[3]
+    yd = torch.empty(2, OH, OW, 64, device=gpu, dtype=dt)
+    dc = L.dtype_code(dt)
+    L.call("zp_maxpool3s2", xd.data_ptr(), 2, 17, 16, 64, 0, 64, dc, yd.data_ptr(), OH, OW, 64, 0, L.stream_ptr())
+    assert torch.equal(yd.float().permute(0, 3, 1, 2).cpu(), y.detach())
+    gd = g.permute(0, 2, 3, 1).contiguous().to(gpu, dt)
+    dx = torch.zeros_like(xd)
+    L.call("zp_maxpool3s2_bwd", xd.data_ptr(), 64, 0, gd.data_ptr(), 64, 0, 2, 17, 16, 64, OH, OW, dc, dx.data_ptr(), 64,
+           0, 1, L.stream_ptr())
+    got = dx.float().permute(0, 3, 1, 2).cpu()
+    assert (got - xx.grad).abs().max().item() <= (1e-6 if prec == "fp32" else 2e-2)

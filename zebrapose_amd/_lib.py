@@ -1,0 +1,147 @@
+"""ctypes binding of libzp.so (include/zp.h).
+
+The library is the product: there is no fallback.  If ``libzp.so`` is missing or
+a call fails, this module raises.  PyTorch is used only for device memory and the
+current HIP stream (``torch.cuda.current_stream().cuda_stream``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import torch  # noqa: F401  (load torch's HIP runtime first; libzp binds to the same libamdhip64.so.7)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("ZP_LIB", os.path.join(_HERE, "libzp.so"))
+
+ZP_F32, ZP_BF16 = 0, 1
+ZP_OUT_NHWC, ZP_OUT_HEAD_NCHW, ZP_OUT_NHWC_F32 = 0, 1, 2
+MAX_TAPS, MAX_SUB = 64, 4
+
+vp = C.c_void_p
+i32 = C.c_int
+i64 = C.c_longlong
+f32 = C.c_float
+f64 = C.c_double
+
+
+class ConvSub(C.Structure):
+    _fields_ = [("w", vp), ("scale", vp), ("shift", vp), ("y", vp), ("y2", vp),
+                ("ldy", i32), ("cy0", i32), ("OH", i32), ("OW", i32),
+                ("oys", i32), ("oyo", i32), ("oxs", i32), ("oxo", i32),
+                ("ntaps", i32), ("kw", i32), ("dil", i32), ("pad", i32),
+                ("ty", C.c_byte * MAX_TAPS), ("tx", C.c_byte * MAX_TAPS)]
+
+
+class ConvArgs(C.Structure):
+    _fields_ = [("dtype", i32), ("x", vp), ("ldx", i32), ("cx0", i32), ("IH", i32), ("IW", i32), ("Cin", i32),
+                ("N", i32), ("GH", i32), ("GW", i32), ("sy", i32), ("sx", i32),
+                ("Cout", i32), ("k_pad", i32), ("w_rows", i32),
+                ("res", vp), ("ldr", i32), ("cr0", i32), ("relu", i32), ("out_mode", i32),
+                ("stats", vp), ("nsub", i32), ("sub", ConvSub * MAX_SUB)]
+
+
+class WgradSub(C.Structure):
+    _fields_ = [("dy", vp), ("lddy", i32), ("cdy0", i32), ("OH", i32), ("OW", i32),
+                ("oys", i32), ("oyo", i32), ("oxs", i32), ("oxo", i32), ("ntaps", i32),
+                ("ky", C.c_byte * MAX_TAPS), ("kx", C.c_byte * MAX_TAPS),
+                ("ty", C.c_byte * MAX_TAPS), ("tx", C.c_byte * MAX_TAPS)]
+
+
+class WgradArgs(C.Structure):
+    _fields_ = [("dtype", i32), ("x", vp), ("ldx", i32), ("cx0", i32), ("IH", i32), ("IW", i32), ("Cin", i32),
+                ("N", i32), ("GH", i32), ("GW", i32), ("sy", i32), ("sx", i32),
+                ("Cout", i32), ("Cw", i32), ("kh", i32), ("kw", i32), ("transposed_w", i32),
+                ("nsub", i32), ("sub", WgradSub * MAX_SUB), ("dw", vp), ("accumulate", i32)]
+
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "zp_abi_version": (i32, []),
+    "zp_last_error": (C.c_char_p, []),
+    "zp_conv2d": (i32, [C.POINTER(ConvArgs), vp]),
+    "zp_conv_rows_pad": (i32, [i32]),
+    "zp_conv2d_grid": (i32, [C.POINTER(ConvArgs)]),
+    "zp_conv2d_stat_parts": (i32, [C.POINTER(ConvArgs)]),
+    "zp_pack_weight": (i32, [vp, i32, i32, i32, i32, i32, i32, C.POINTER(i32), C.POINTER(i32), i32, i32, vp, i32,
+                             i32, vp]),
+    "zp_conv2d_wgrad_ws_bytes": (i64, [C.POINTER(WgradArgs)]),
+    "zp_conv2d_wgrad": (i32, [C.POINTER(WgradArgs), vp, vp]),
+    "zp_bn_fold": (i32, [vp, vp, vp, vp, vp, f32, i32, vp, vp, vp]),
+    "zp_bn_train_finalize": (i32, [vp, i32, i32, i64, f32, f32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+    "zp_bn_apply": (i32, [vp, i32, i32, vp, vp, vp, i32, i32, i32, i32, vp, i32, i32, vp]),
+    "zp_bn_bwd_parts": (i32, [i32, i32]),
+    "zp_bn_bwd_reduce": (i32, [vp, i32, i32, vp, i32, i32, vp, i32, i32, vp, i32, i32, vp, vp, vp, i32, vp]),
+    "zp_bn_bwd_apply": (i32, [vp, i32, i32, vp, i32, i32, vp, i32, i32, vp, vp, vp, i32, i32, vp, vp, i32, i32, i32,
+                              vp]),
+    "zp_nchw_to_nhwc": (i32, [vp, i32, i32, i32, i32, i32, i32, vp, vp]),
+    "zp_maxpool3s2": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, vp, i32, i32, i32, i32, vp]),
+    "zp_maxpool3s2_bwd": (i32, [vp, i32, i32, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, i32, i32, i32,
+                                vp]),
+    "zp_global_avgpool": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, vp, vp]),
+    "zp_broadcast_hw": (i32, [vp, i32, i32, i32, vp, i32, i32, i32, i32, vp]),
+    "zp_sum_hw": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, vp, vp]),
+    "zp_add_broadcast_hw": (i32, [vp, f32, i32, i32, i32, vp, i32, i32, i32, i32, i32, vp]),
+    "zp_copy_slice": (i32, [vp, i32, i32, i32, vp, i32, i32, i32, i32, i32, i32, vp]),
+    "zp_head_grad_to_nhwc": (i32, [vp, vp, i32, i32, i32, i32, i32, i32, vp, vp]),
+    "zp_code_loss_ws_bytes": (i64, [i32, i32, i32, i32]),
+    "zp_code_loss": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp]),
+    "zp_code_loss_bwd": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp]),
+    "zp_mask_loss_ws_bytes": (i64, [i64]),
+    "zp_mask_loss": (i32, [vp, vp, i64, vp, vp, vp]),
+    "zp_mask_loss_bwd": (i32, [vp, vp, i64, vp, vp, vp]),
+    "zp_threshold": (i32, [vp, i64, i32, vp, vp]),
+    "zp_decode_ws_bytes": (i64, [i32, i32, i32]),
+    "zp_decode": (i32, [vp, vp, i32, i32, i32, i32, i32, vp, vp, vp, i32, vp, vp, vp, vp, vp, vp]),
+    "zp_lut_coarsen": (i32, [vp, i32, i32, vp, vp]),
+    "zp_adam": (i32, [vp, vp, vp, vp, i64, f64, f64, f64, f64, i64, vp]),
+}
+
+
+class ZPError(RuntimeError):
+    pass
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libzp.so not found at {LIB_PATH}: build it with `python -c 'import __graft_entry__ as g; "
+                          f"g.build()'` (make -C zebrapose_amd/csrc).  There is no CPU fallback.")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.zp_abi_version() != 1:
+        raise ImportError("libzp.so ABI version mismatch")
+    return lib
+
+
+lib = _load()
+
+
+def check(rc: int, what: str = ""):
+    if rc != 0:
+        msg = lib.zp_last_error().decode(errors="replace")
+        raise ZPError(f"{what or 'libzp'} failed (rc={rc}): {msg}")
+
+
+def call(name: str, *args):
+    check(getattr(lib, name)(*args), name)
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t) -> int | None:
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def dtype_code(dt) -> int:
+    if dt == torch.float32:
+        return ZP_F32
+    if dt == torch.bfloat16:
+        return ZP_BF16
+    raise ValueError(f"unsupported activation dtype {dt}")

@@ -1,0 +1,585 @@
+// Implicit-GEMM convolution for gfx950 (MI355X): forward / data-gradient (k_conv)
+// and weight-gradient (k_wgrad).  NHWC activations, packed [rows][tap*Cin] weights.
+//
+// Replaces the cuDNN convolutions behind nn.Conv2d / nn.ConvTranspose2d at
+// model/resnet.py:41-51, model/aspp.py:60-80, 89-112 and the torchvision ResNet
+// children reused at resnet.py:191-199 (see include/zp.h).
+//
+// Forward tile: one 256-thread workgroup = 4 waves (2 cout x 2 pixel) computes
+// TC (=32*WC) output channels x TP (=32*WP) pixels.  The MFMA A operand is the
+// weight tile (rows = output channels), B is the activation tile (cols = pixels),
+// so each lane ends up with 4 consecutive output channels of one pixel -> 8/16 B
+// NHWC stores.  K steps are 128 bytes per row (64 bf16 / 32 f32) of one tap;
+// the tile is staged global -> registers -> LDS (XOR-swizzled 16 B chunks,
+// double-buffered, one barrier per K step).
+#include "zp_common.h"
+
+namespace zp {
+
+template <typename T> struct MfmaTraits;
+template <> struct MfmaTraits<bf16_t> {
+  static constexpr int E = 8;  // elements per 16 B chunk
+  static __device__ __forceinline__ void mma(f32x4& acc, const uint4& a, const uint4& b) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b),
+                                                  acc, 0, 0, 0);
+  }
+};
+template <> struct MfmaTraits<float> {
+  static constexpr int E = 4;
+  // 16 B chunk = 4 consecutive k of one row; element e is k-substep e for every lane
+  // group, so the four 16x16x4 MFMAs together cover all 16 k of the 4 lane groups.
+  static __device__ __forceinline__ void mma(f32x4& acc, const uint4& a, const uint4& b) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.x), __uint_as_float(b.x), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.y), __uint_as_float(b.y), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.z), __uint_as_float(b.z), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.w), __uint_as_float(b.w), acc, 0, 0, 0);
+  }
+};
+
+__device__ __forceinline__ int swz(int row, int chunk) { return row * 8 + (chunk ^ (row & 7)); }
+
+template <typename T, int WC, int WP, bool SMALLC>
+__global__ void __launch_bounds__(256) k_conv(const zp_conv_args A) {
+  constexpr int E = MfmaTraits<T>::E;
+  constexpr int KE = 8 * E;  // elements per K step (128 B)
+  constexpr int TC = 32 * WC, TP = 32 * WP;
+  constexpr int LC = TC / 32, LP = TP / 32;
+  __shared__ uint4 lds[2][(TC + TP) * 8];
+
+  const zp_conv_sub& S = A.sub[blockIdx.z];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wc = wid >> 1, wp = wid & 1;
+  const int GHW = A.GH * A.GW;
+  const int M = A.N * GHW;
+  const int p0 = blockIdx.x * TP, c0 = blockIdx.y * TC;
+  const int qr = tid >> 3, qc = tid & 7;
+
+  int rn[LP], ry[LP], rx[LP];
+  bool rv[LP];
+#pragma unroll
+  for (int i = 0; i < LP; ++i) {
+    int m = p0 + qr + 32 * i;
+    rv[i] = m < M;
+    int mm = rv[i] ? m : 0;
+    int n = mm / GHW, r = mm - n * GHW;
+    int gy = r / A.GW, gx = r - gy * A.GW;
+    rn[i] = n;
+    ry[i] = gy * A.sy;
+    rx[i] = gx * A.sx;
+  }
+  const T* __restrict__ X = (const T*)A.x;
+  const T* __restrict__ Wt = (const T*)S.w;
+  const int CB = SMALLC ? 1 : A.Cin / KE;
+  const int nK = SMALLC ? A.k_pad / KE : S.ntaps * CB;
+
+  uint4 ra[LC], rb[LP];
+  auto gload = [&](int ks) {
+#pragma unroll
+    for (int i = 0; i < LC; ++i)
+      ra[i] = *(const uint4*)(Wt + (size_t)(c0 + qr + 32 * i) * A.k_pad + (size_t)ks * KE + qc * E);
+    int ty, tx, cc;
+    bool tok;
+    if (SMALLC) {
+      int k = ks * KE + qc * E;
+      int t = k / A.Cin;
+      cc = k - t * A.Cin;
+      tok = t < S.ntaps;
+      int kyy = t / S.kw;
+      ty = kyy * S.dil - S.pad;
+      tx = (t - kyy * S.kw) * S.dil - S.pad;
+    } else {
+      int t = ks / CB;
+      cc = (ks - t * CB) * KE + qc * E;
+      ty = S.ty[t];
+      tx = S.tx[t];
+      tok = true;
+    }
+#pragma unroll
+    for (int i = 0; i < LP; ++i) {
+      int iy = ry[i] + ty, ix = rx[i] + tx;
+      bool ok = tok && rv[i] && (unsigned)iy < (unsigned)A.IH && (unsigned)ix < (unsigned)A.IW;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (ok) v = *(const uint4*)(X + (((size_t)rn[i] * A.IH + iy) * A.IW + ix) * A.ldx + A.cx0 + cc);
+      rb[i] = v;
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < LC; ++i) lds[buf][swz(qr + 32 * i, qc)] = ra[i];
+#pragma unroll
+    for (int i = 0; i < LP; ++i) lds[buf][swz(TC + qr + 32 * i, qc)] = rb[i];
+  };
+
+  f32x4 acc[WC][WP];
+#pragma unroll
+  for (int i = 0; i < WC; ++i)
+#pragma unroll
+    for (int j = 0; j < WP; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  for (int ks = 0; ks < nK; ++ks) {
+    const int buf = ks & 1;
+    if (ks + 1 < nK) gload(ks + 1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int ch = s * 4 + (lane >> 4);
+      uint4 af[WC], bfr[WP];
+#pragma unroll
+      for (int i = 0; i < WC; ++i) af[i] = lds[buf][swz(wc * 16 * WC + i * 16 + (lane & 15), ch)];
+#pragma unroll
+      for (int j = 0; j < WP; ++j) bfr[j] = lds[buf][swz(TC + wp * 16 * WP + j * 16 + (lane & 15), ch)];
+#pragma unroll
+      for (int i = 0; i < WC; ++i)
+#pragma unroll
+        for (int j = 0; j < WP; ++j) MfmaTraits<T>::mma(acc[i][j], af[i], bfr[j]);
+    }
+    if (ks + 1 < nK) sstore(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---------------- epilogue ----------------
+  const int cbase = c0 + wc * 16 * WC + (lane >> 4) * 4;
+#pragma unroll
+  for (int j = 0; j < WP; ++j) {
+    const int p = p0 + wp * 16 * WP + j * 16 + (lane & 15);
+    if (p >= M) continue;
+    int n = p / GHW, rr = p - n * GHW;
+    int gy = rr / A.GW, gx = rr - gy * A.GW;
+    int oy = gy * S.oys + S.oyo, ox = gx * S.oxs + S.oxo;
+    size_t pix = ((size_t)n * S.OH + oy) * S.OW + ox;
+#pragma unroll
+    for (int i = 0; i < WC; ++i) {
+      const int cf = cbase + i * 16;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int c = cf + r;
+        float sc = (S.scale && c < A.Cout) ? S.scale[c] : 1.f;
+        float sh = (S.shift && c < A.Cout) ? S.shift[c] : 0.f;
+        v[r] = acc[i][j][r] * sc + sh;
+      }
+      if (A.res) {
+        const T* R = (const T*)A.res + pix * A.ldr + A.cr0 + cf;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (cf + r < A.Cout) v[r] += Elem<T>::ld(R + r);
+      }
+      if (A.relu) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+      }
+      if (A.out_mode == ZP_OUT_HEAD_NCHW) {
+        const size_t plane = (size_t)S.OH * S.OW;
+        const size_t sp = (size_t)oy * S.OW + ox;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          int c = cf + r;
+          if (c >= A.Cout) continue;
+          if (c == 0)
+            ((float*)S.y)[(size_t)n * plane + sp] = v[r];
+          else
+            ((float*)S.y2)[((size_t)n * (A.Cout - 1) + (c - 1)) * plane + sp] = v[r];
+        }
+        continue;
+      }
+      if (A.out_mode == ZP_OUT_NHWC_F32 || sizeof(T) == 4) {
+        float* Y = (float*)S.y + pix * S.ldy + S.cy0 + cf;
+        if (cf + 3 < A.Cout) {
+          *(float4*)Y = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (cf + r < A.Cout) Y[r] = v[r];
+        }
+      } else {
+        bf16_t b[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          b[r] = f2bf(v[r]);
+          v[r] = bf2f(b[r]);  // statistics of the stored value
+        }
+        bf16_t* Y = (bf16_t*)S.y + pix * S.ldy + S.cy0 + cf;
+        if (cf + 3 < A.Cout) {
+          *(uint2*)Y = make_uint2((uint32_t)b[0] | ((uint32_t)b[1] << 16), (uint32_t)b[2] | ((uint32_t)b[3] << 16));
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (cf + r < A.Cout) Y[r] = b[r];
+        }
+      }
+    }
+  }
+  if (A.stats) {
+    // Train-mode BatchNorm statistics of the raw (stored) conv output, per wave half:
+    // (count, mean, M2) with M2 centred on the local mean (two passes over the registers, no
+    // E[x^2] - E[x]^2 cancellation); zp_bn_train_finalize merges the parts (Chan et al.).
+    const int parts = gridDim.x * gridDim.z * 2;
+    const int part = (blockIdx.z * gridDim.x + blockIdx.x) * 2 + wp;
+    float cnt = 0.f;
+#pragma unroll
+    for (int j = 0; j < WP; ++j) cnt += (p0 + wp * 16 * WP + j * 16 + (lane & 15) < M) ? 1.f : 0.f;
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) cnt += __shfl_xor(cnt, off);
+#pragma unroll
+    for (int i = 0; i < WC; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float vv[WP];
+        float sm = 0.f;
+#pragma unroll
+        for (int j = 0; j < WP; ++j) {
+          const bool ok = p0 + wp * 16 * WP + j * 16 + (lane & 15) < M;
+          float v = acc[i][j][r];
+          if (sizeof(T) == 2 && A.out_mode != ZP_OUT_NHWC_F32) v = bf2f(f2bf(v));  // stored value
+          vv[j] = ok ? v : 0.f;
+          sm += vv[j];
+        }
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) sm += __shfl_xor(sm, off);
+        const float mean = cnt > 0.f ? sm / cnt : 0.f;
+        float m2 = 0.f;
+#pragma unroll
+        for (int j = 0; j < WP; ++j) {
+          const bool ok = p0 + wp * 16 * WP + j * 16 + (lane & 15) < M;
+          const float dlt = vv[j] - mean;
+          m2 += ok ? dlt * dlt : 0.f;
+        }
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) m2 += __shfl_xor(m2, off);
+        const int c = cbase + i * 16 + r;
+        if ((lane & 15) == 0 && c < A.Cout) {
+          A.stats[(size_t)part * A.Cout + c] = cnt;
+          A.stats[((size_t)parts + part) * A.Cout + c] = mean;
+          A.stats[((size_t)2 * parts + part) * A.Cout + c] = m2;
+        }
+      }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// weight gradient:  ws[split][sub][co][col] = sum over the split's grid points of
+//   dy[out pixel][co] * x[in pixel (tap of col)][ci of col],   col = t*Cin + ci
+// K (pixels) is the MFMA reduction axis, so both LDS tiles [pixel][channel] are read
+// transposed with ds_read_b64_tr_b16 (bf16) / per-lane b32 (f32).
+// ------------------------------------------------------------------------------------
+template <typename T> struct WgTraits;
+template <> struct WgTraits<bf16_t> { static constexpr int KP = 32; };  // pixels per K step
+template <> struct WgTraits<float> { static constexpr int KP = 16; };
+
+constexpr int WG_TILE = 128;            // co x col tile
+constexpr int WG_ROWB = 256 + 16;       // LDS row bytes (128 ch of bf16 / 64 of f32 -> see below)
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_wgrad(const zp_wgrad_args A, float* __restrict__ ws, int pix_per_split,
+                                                int col_tiles, int cols_max) {
+  constexpr int KP = WgTraits<T>::KP;
+  constexpr int CHE = 16 / sizeof(T);            // elements per 16 B chunk
+  constexpr int NCH = WG_TILE / CHE;             // chunks per 128-channel row (16 bf16 / 32 f32)
+  constexpr int ROWB = WG_TILE * sizeof(T) + 16; // padded LDS row bytes
+  constexpr int TILEB = KP * ROWB;
+  constexpr int LPT = KP * NCH / 256;            // chunk loads per thread per tile (2)
+  __shared__ __attribute__((aligned(16))) unsigned char lds[2][2][TILEB];
+
+  const int sub = blockIdx.z;
+  const auto& S = A.sub[sub];
+  const int cols = S.ntaps * A.Cin;
+  const int ct = blockIdx.y % col_tiles, cot = blockIdx.y / col_tiles;
+  const int col0 = ct * WG_TILE, co0 = cot * WG_TILE;
+  if (col0 >= cols) return;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wc = wid >> 1, wk = wid & 1;
+  const int GHW = A.GH * A.GW;
+  const int M = A.N * GHW;
+  const int pbeg = blockIdx.x * pix_per_split;
+  const int pend = min(M, pbeg + pix_per_split);
+
+  // thread -> (row, chunk) of both tiles; chunk column fixed for the whole kernel
+  const int qc = tid % NCH, qr = tid / NCH;      // rows qr + (256/NCH)*i
+  constexpr int RSTEP = 256 / NCH;
+  // dy channel of this chunk
+  const int dco = co0 + qc * CHE;
+  const bool dco_ok = dco < A.Cout;
+  // x column of this chunk -> (tap, ci)
+  const int xcol = col0 + qc * CHE;
+  const bool xcol_ok = xcol < cols;
+  const int xt = xcol_ok ? xcol / A.Cin : 0;
+  const int xci = xcol - xt * A.Cin;
+  const int xty = S.ty[xt], xtx = S.tx[xt];
+  const T* __restrict__ X = (const T*)A.x;
+  const T* __restrict__ DY = (const T*)S.dy;
+
+  uint4 rd[LPT], rx[LPT];
+  auto gload = [&](int pk) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      int p = pk + qr + RSTEP * i;
+      uint4 vd = make_uint4(0, 0, 0, 0), vx = make_uint4(0, 0, 0, 0);
+      if (p < pend) {
+        int n = p / GHW, rr = p - n * GHW;
+        int gy = rr / A.GW, gx = rr - gy * A.GW;
+        if (dco_ok) {
+          int oy = gy * S.oys + S.oyo, ox = gx * S.oxs + S.oxo;
+          vd = *(const uint4*)(DY + (((size_t)n * S.OH + oy) * S.OW + ox) * S.lddy + S.cdy0 + dco);
+        }
+        int iy = gy * A.sy + xty, ix = gx * A.sx + xtx;
+        if (xcol_ok && (unsigned)iy < (unsigned)A.IH && (unsigned)ix < (unsigned)A.IW)
+          vx = *(const uint4*)(X + (((size_t)n * A.IH + iy) * A.IW + ix) * A.ldx + A.cx0 + xci);
+      }
+      rd[i] = vd;
+      rx[i] = vx;
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      int row = qr + RSTEP * i;
+      *(uint4*)(&lds[buf][0][row * ROWB + qc * 16]) = rd[i];
+      *(uint4*)(&lds[buf][1][row * ROWB + qc * 16]) = rx[i];
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nsteps = pend > pbeg ? (pend - pbeg + KP - 1) / KP : 0;
+  if (nsteps > 0) {
+    gload(pbeg);
+    sstore(0);
+  }
+  __syncthreads();
+  for (int s = 0; s < nsteps; ++s) {
+    const int buf = s & 1;
+    if (s + 1 < nsteps) gload(pbeg + (s + 1) * KP);
+    const unsigned char* TD = lds[buf][0];
+    const unsigned char* TX = lds[buf][1];
+    if constexpr (sizeof(T) == 2) {
+      // A[co][k] and B[k][col]: lane l of group g = l>>4 needs k = 8g..8g+7 of column (l & 15)
+      typedef __attribute__((ext_vector_type(4))) short s4;
+      const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
+      bf16x8 af[4], bfm[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int cbase = wc * 64 + i * 16 + 4 * pp;
+        const unsigned char* a0 = TD + (8 * g + q) * ROWB + cbase * 2;
+        s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(a0));
+        s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(a0 + 4 * ROWB));
+        typedef __attribute__((ext_vector_type(8))) short s8;
+        s8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        af[i] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        int cbase = wk * 64 + j * 16 + 4 * pp;
+        const unsigned char* b0 = TX + (8 * g + q) * ROWB + cbase * 2;
+        s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(b0));
+        s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(b0 + 4 * ROWB));
+        typedef __attribute__((ext_vector_type(8))) short s8;
+        s8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        bfm[j] = __builtin_bit_cast(bf16x8, v);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfm[j], acc[i][j], 0, 0, 0);
+    } else {
+      // f32: A[i=l&15][k=l>>4], B[k=l>>4][j=l&15]; 4 MFMAs of K=4 per 16-pixel step
+      const int li = lane & 15, g = lane >> 4;
+#pragma unroll
+      for (int kk = 0; kk < KP; kk += 4) {
+        float av[4], bv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          av[i] = *(const float*)(TD + (kk + g) * ROWB + (wc * 64 + i * 16 + li) * 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          bv[j] = *(const float*)(TX + (kk + g) * ROWB + (wk * 64 + j * 16 + li) * 4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    if (s + 1 < nsteps) sstore(buf ^ 1);
+    __syncthreads();
+  }
+  // write partial tile: ws[((split*nsub + sub)*Cout + co)*cols_max + col]
+  float* W = ws + ((size_t)blockIdx.x * A.nsub + sub) * (size_t)A.Cout * cols_max;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int col = col0 + wk * 64 + j * 16 + (lane & 15);
+      if (col >= cols) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int co = co0 + wc * 64 + i * 16 + (lane >> 4) * 4 + r;
+        if (co < A.Cout) W[(size_t)co * cols_max + col] = acc[i][j][r];
+      }
+    }
+}
+
+// ws (summed over splits) -> dw in the weight's own layout
+__global__ void k_wgrad_reduce(const zp_wgrad_args A, const float* __restrict__ ws, int splits, int cols_max) {
+  const int sub = blockIdx.y;
+  const auto& S = A.sub[sub];
+  const int cols = S.ntaps * A.Cin;
+  const long total = (long)A.Cout * cols;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int co = (int)(e / cols), col = (int)(e - (long)co * cols);
+    const int t = col / A.Cin, ci = col - t * A.Cin;
+    const int ky = S.ky[t], kx = S.kx[t];
+    if (ci >= A.Cw || ky < 0) continue;  // padded input channels / padding taps
+    float s = 0.f;
+    for (int k = 0; k < splits; ++k) s += ws[(((size_t)k * A.nsub + sub) * A.Cout + co) * cols_max + col];
+    size_t idx = A.transposed_w ? (((size_t)ci * A.Cout + co) * A.kh + ky) * A.kw + kx
+                                : (((size_t)co * A.Cw + ci) * A.kh + ky) * A.kw + kx;
+    if (A.accumulate) A.dw[idx] += s;
+    else A.dw[idx] = s;
+  }
+}
+
+}  // namespace zp
+
+using namespace zp;
+
+// ------------------------------------------------------------------------------------ host
+template <typename T, int WC, bool SMALLC>
+static void launch_conv(const zp_conv_args& a, int gx, int gy, hipStream_t st) {
+  hipLaunchKernelGGL((k_conv<T, WC, 4, SMALLC>), dim3(gx, gy, a.nsub), dim3(256), 0, st, a);
+}
+
+static int conv_tc(int cout) { return cout > 64 ? 128 : (cout > 32 ? 64 : 32); }
+
+extern "C" int zp_conv2d_grid(const zp_conv_args* a) {
+  if (!a) return 0;
+  long M = (long)a->N * a->GH * a->GW;
+  return ceil_div(M, 128);
+}
+
+extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
+  ZP_CHECK_ARG(ap != nullptr, "zp_conv2d: null args");
+  const zp_conv_args& a = *ap;
+  ZP_CHECK_ARG(a.dtype == ZP_F32 || a.dtype == ZP_BF16, "zp_conv2d: bad dtype %d", a.dtype);
+  ZP_CHECK_ARG(a.nsub >= 1 && a.nsub <= ZP_MAX_SUB, "zp_conv2d: nsub %d", a.nsub);
+  ZP_CHECK_ARG(a.x && a.N > 0 && a.GH > 0 && a.GW > 0 && a.IH > 0 && a.IW > 0 && a.Cout > 0,
+               "zp_conv2d: bad geometry");
+  const int E = a.dtype == ZP_BF16 ? 8 : 4, KE = 8 * E;
+  const bool smallc = a.Cin < KE;
+  ZP_CHECK_ARG(a.Cin > 0 && a.Cin % E == 0 && (smallc || a.Cin % KE == 0),
+               "zp_conv2d: Cin %d must be a multiple of %d (or < %d and a multiple of %d)", a.Cin, KE, KE, E);
+  ZP_CHECK_ARG(a.ldx >= a.cx0 + a.Cin && a.cx0 % E == 0 && a.ldx % E == 0, "zp_conv2d: bad ldx/cx0");
+  ZP_CHECK_ARG(a.k_pad % KE == 0, "zp_conv2d: k_pad %d not a multiple of %d", a.k_pad, KE);
+  ZP_CHECK_ARG(a.w_rows % conv_tc(a.Cout) == 0 && a.w_rows >= a.Cout, "zp_conv2d: w_rows %d", a.w_rows);
+  ZP_CHECK_ARG(a.out_mode >= 0 && a.out_mode <= 2, "zp_conv2d: out_mode");
+  ZP_CHECK_ARG(!a.stats || (!a.res && !a.relu && a.out_mode != ZP_OUT_HEAD_NCHW && !a.sub[0].scale &&
+                            !a.sub[0].shift),
+               "zp_conv2d: stats are taken on the raw conv output (no scale/shift/residual/relu/head)");
+  for (int s = 0; s < a.nsub; ++s) {
+    const zp_conv_sub& S = a.sub[s];
+    ZP_CHECK_ARG(S.w && S.y, "zp_conv2d: sub %d null w/y", s);
+    ZP_CHECK_ARG(S.ntaps >= 1 && S.ntaps <= ZP_MAX_TAPS, "zp_conv2d: ntaps %d", S.ntaps);
+    if (smallc) {
+      ZP_CHECK_ARG(S.kw > 0 && (long)S.ntaps * a.Cin <= a.k_pad, "zp_conv2d: small-Cin taps/k_pad");
+    } else {
+      ZP_CHECK_ARG((long)S.ntaps * a.Cin <= a.k_pad, "zp_conv2d: k_pad %d < ntaps*Cin", a.k_pad);
+    }
+    if (a.out_mode != ZP_OUT_HEAD_NCHW) {
+      ZP_CHECK_ARG(S.ldy >= S.cy0 + a.Cout && S.cy0 % 4 == 0 && S.ldy % 4 == 0, "zp_conv2d: bad ldy/cy0");
+    } else {
+      ZP_CHECK_ARG(S.y2 || a.Cout == 1, "zp_conv2d: head needs y2");
+    }
+  }
+  if (a.res) ZP_CHECK_ARG(a.ldr >= a.cr0 + a.Cout && a.cr0 % 4 == 0, "zp_conv2d: bad residual ld");
+  const int tc = conv_tc(a.Cout);
+  const int gx = zp_conv2d_grid(&a), gy = ceil_div(a.Cout, tc);
+  hipStream_t st = (hipStream_t)stream;
+#define ZP_DISPATCH(T)                                                   \
+  if (tc == 128) {                                                       \
+    if (smallc) launch_conv<T, 4, true>(a, gx, gy, st);                  \
+    else launch_conv<T, 4, false>(a, gx, gy, st);                        \
+  } else if (tc == 64) {                                                 \
+    if (smallc) launch_conv<T, 2, true>(a, gx, gy, st);                  \
+    else launch_conv<T, 2, false>(a, gx, gy, st);                        \
+  } else {                                                               \
+    if (smallc) launch_conv<T, 1, true>(a, gx, gy, st);                  \
+    else launch_conv<T, 1, false>(a, gx, gy, st);                        \
+  }
+  if (a.dtype == ZP_BF16) {
+    ZP_DISPATCH(bf16_t)
+  } else {
+    ZP_DISPATCH(float)
+  }
+#undef ZP_DISPATCH
+  ZP_LAUNCH_CHECK("zp_conv2d");
+  return ZP_OK;
+}
+
+static void wgrad_plan(const zp_wgrad_args& a, int* splits, int* col_tiles, int* cols_max, int* pix_per) {
+  long M = (long)a.N * a.GH * a.GW;
+  int cm = 0;
+  for (int s = 0; s < a.nsub; ++s) cm = cm > a.sub[s].ntaps * a.Cin ? cm : a.sub[s].ntaps * a.Cin;
+  int ct = ceil_div(cm, WG_TILE);
+  int tiles = ct * ceil_div(a.Cout, WG_TILE) * a.nsub;
+  const int KP = a.dtype == ZP_BF16 ? 32 : 16;
+  // aim for >= 1024 workgroups, but keep >= 8 K steps per split
+  long sp = (1024 + tiles - 1) / tiles;
+  long maxsp = M / (8 * KP);
+  if (maxsp < 1) maxsp = 1;
+  if (sp > maxsp) sp = maxsp;
+  if (sp > 256) sp = 256;
+  long pp = (M + sp - 1) / sp;
+  pp = (pp + KP - 1) / KP * KP;
+  sp = (M + pp - 1) / pp;
+  *splits = (int)sp;
+  *col_tiles = ct;
+  *cols_max = cm;
+  *pix_per = (int)pp;
+}
+
+extern "C" long long zp_conv2d_wgrad_ws_bytes(const zp_wgrad_args* a) {
+  if (!a || a->nsub < 1 || a->nsub > ZP_MAX_SUB) return -1;
+  int sp, ct, cm, pp;
+  wgrad_plan(*a, &sp, &ct, &cm, &pp);
+  return (long long)sp * a->nsub * a->Cout * (long long)cm * 4;
+}
+
+extern "C" int zp_conv2d_wgrad(const zp_wgrad_args* ap, void* ws, void* stream) {
+  ZP_CHECK_ARG(ap && ws, "zp_conv2d_wgrad: null args/workspace");
+  const zp_wgrad_args& a = *ap;
+  ZP_CHECK_ARG(a.dtype == ZP_F32 || a.dtype == ZP_BF16, "zp_conv2d_wgrad: dtype");
+  ZP_CHECK_ARG(a.nsub >= 1 && a.nsub <= ZP_MAX_SUB && a.dw && a.x, "zp_conv2d_wgrad: bad args");
+  const int E = a.dtype == ZP_BF16 ? 8 : 4;
+  ZP_CHECK_ARG(a.Cin % E == 0 && a.cx0 % E == 0 && a.ldx % E == 0, "zp_conv2d_wgrad: Cin/cx0/ldx alignment");
+  ZP_CHECK_ARG(a.Cw >= 1 && a.Cw <= a.Cin, "zp_conv2d_wgrad: Cw");
+  for (int s = 0; s < a.nsub; ++s) {
+    ZP_CHECK_ARG(a.sub[s].dy && a.sub[s].ntaps >= 1 && a.sub[s].ntaps <= ZP_MAX_TAPS, "zp_conv2d_wgrad: sub %d", s);
+    ZP_CHECK_ARG(a.sub[s].cdy0 % E == 0 && a.sub[s].lddy % E == 0 &&
+                 a.sub[s].lddy >= a.sub[s].cdy0 + ((a.Cout + E - 1) / E) * E,
+                 "zp_conv2d_wgrad: dy ld must cover Cout rounded to %d", E);
+  }
+  int sp, ct, cm, pp;
+  wgrad_plan(a, &sp, &ct, &cm, &pp);
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid(sp, ct * ceil_div(a.Cout, WG_TILE), a.nsub);
+  if (a.dtype == ZP_BF16)
+    hipLaunchKernelGGL(k_wgrad<bf16_t>, grid, dim3(256), 0, st, a, (float*)ws, pp, ct, cm);
+  else
+    hipLaunchKernelGGL(k_wgrad<float>, grid, dim3(256), 0, st, a, (float*)ws, pp, ct, cm);
+  ZP_LAUNCH_CHECK("zp_conv2d_wgrad");
+  long tot = (long)a.Cout * cm;
+  int rb = (int)((tot + 255) / 256);
+  if (rb > 4096) rb = 4096;
+  hipLaunchKernelGGL(k_wgrad_reduce, dim3(rb, a.nsub), dim3(256), 0, st, a, (const float*)ws, sp, cm);
+  ZP_LAUNCH_CHECK("zp_conv2d_wgrad reduce");
+  return ZP_OK;
+}
+
+extern "C" int zp_conv2d_stat_parts(const zp_conv_args* a) {
+  if (!a) return 0;
+  return 2 * zp_conv2d_grid(a) * a->nsub;
+}

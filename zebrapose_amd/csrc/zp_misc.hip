@@ -1,0 +1,775 @@
+// Memory-bound kernels of the ZebraPose hot path on gfx950: weight packing, batch-norm
+// (eval fold, train statistics / apply / backward), pooling, layout conversion, slice
+// copies, and the Adam step.  All NHWC, 16-byte vectorised (8 bf16 / 4 f32 per access).
+#include <stdarg.h>
+#include <stdio.h>
+#include <math.h>
+#include "zp_common.h"
+
+namespace zp {
+
+static thread_local char g_err[512] = "";
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+// 16-byte vector of dtype T
+template <typename T> struct V16;
+template <> struct V16<bf16_t> {
+  static constexpr int N = 8;
+  static __device__ __forceinline__ void load(const bf16_t* p, float* f) {
+    uint4 u = *(const uint4*)p;
+    uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      f[2 * i] = __uint_as_float(w[i] << 16);
+      f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+  }
+  static __device__ __forceinline__ void store(bf16_t* p, const float* f) {
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(f[2 * i]) | ((uint32_t)f2bf(f[2 * i + 1]) << 16);
+    *(uint4*)p = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+};
+template <> struct V16<float> {
+  static constexpr int N = 4;
+  static __device__ __forceinline__ void load(const float* p, float* f) {
+    float4 v = *(const float4*)p;
+    f[0] = v.x; f[1] = v.y; f[2] = v.z; f[3] = v.w;
+  }
+  static __device__ __forceinline__ void store(float* p, const float* f) { *(float4*)p = make_float4(f[0], f[1], f[2], f[3]); }
+};
+
+static inline int grid_for(long n, int block = 256, int cap = 8192) {
+  long g = (n + block - 1) / block;
+  if (g < 1) g = 1;
+  return (int)(g > cap ? cap : g);
+}
+
+// ------------------------------------------------------------------ weight packing
+struct PackArgs {
+  const float* src;
+  void* dst;
+  int d0, d1, kh, kw, transposed, ntaps, cstride, rows_pad, k_pad;
+  signed char ky[ZP_MAX_TAPS], kx[ZP_MAX_TAPS];
+};
+
+template <typename T>
+__global__ void k_pack(const PackArgs a) {
+  const long total = (long)a.rows_pad * a.k_pad;
+  const int rows = a.transposed ? a.d1 : a.d0;
+  const int chans = a.transposed ? a.d0 : a.d1;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    int r = (int)(e / a.k_pad), k = (int)(e - (long)r * a.k_pad);
+    int t = k / a.cstride, c = k - t * a.cstride;
+    float v = 0.f;
+    if (r < rows && t < a.ntaps && c < chans) {
+      int ky = a.ky[t], kx = a.kx[t];
+      size_t idx = a.transposed ? (((size_t)c * a.d1 + r) * a.kh + ky) * a.kw + kx
+                                : (((size_t)r * a.d1 + c) * a.kh + ky) * a.kw + kx;
+      v = a.src[idx];
+    }
+    ((T*)a.dst)[e] = Elem<T>::cvt(v);
+  }
+}
+
+// ------------------------------------------------------------------ batch norm
+__global__ void k_bn_fold(const float* g, const float* b, const float* m, const float* v, const float* bias, float eps,
+                          int C, float* scale, float* shift) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  // PyTorch CPU eval: alpha = weight / sqrt(var + eps); out = in * alpha + (bias - mean * alpha)
+  float inv = 1.f / sqrtf(v[c] + eps);
+  float s = g[c] * inv;
+  float sh = b[c] - m[c] * s;
+  if (bias) sh += bias[c] * s;
+  scale[c] = s;
+  shift[c] = sh;
+}
+
+// block = 32 channels x 8 part lanes
+__global__ void k_bn_train_finalize(const float* __restrict__ part, int parts, int C, long long count, float eps,
+                                    float mom, const float* gamma, const float* beta, const float* bias, float* rm,
+                                    float* rv, int64_t* nbt, float* scale, float* shift, float* save) {
+  // partials: [0] count, [1] mean, [2] M2 (centred) per part; merged with Chan's formula in f64:
+  // n = sum n_k, mean = sum n_k mean_k / n, M2 = sum M2_k + sum n_k (mean_k - mean)^2
+  __shared__ double sh[3][8][33];
+  const int cl = threadIdx.x & 31, pl = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cl;
+  double n = 0, s = 0;
+  if (c < C)
+    for (int k = pl; k < parts; k += 8) {
+      double nk = part[(size_t)k * C + c];
+      n += nk;
+      s += nk * (double)part[((size_t)parts + k) * C + c];
+    }
+  sh[0][pl][cl] = n;
+  sh[1][pl][cl] = s;
+  __syncthreads();
+  double ntot = 0, stot = 0;
+  for (int k = 0; k < 8; ++k) {
+    ntot += sh[0][k][cl];
+    stot += sh[1][k][cl];
+  }
+  const double mean = ntot > 0 ? stot / ntot : 0.0;
+  double q = 0;
+  if (c < C)
+    for (int k = pl; k < parts; k += 8) {
+      double nk = part[(size_t)k * C + c];
+      double dm = (double)part[((size_t)parts + k) * C + c] - mean;
+      q += (double)part[((size_t)2 * parts + k) * C + c] + nk * dm * dm;
+    }
+  sh[2][pl][cl] = q;
+  __syncthreads();
+  if (pl != 0 || c >= C) return;
+  for (int k = 1; k < 8; ++k) q += sh[2][k][cl];
+  (void)count;
+  const double cntd = ntot;
+  double var = cntd > 0 ? q / cntd : 0.0;
+  if (var < 0) var = 0;
+  float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  float sc = gamma[c] * invstd;
+  scale[c] = sc;
+  shift[c] = beta[c] - (float)mean * sc;
+  save[c] = (float)mean;
+  save[C + c] = invstd;
+  double mt = mean + (bias ? (double)bias[c] : 0.0);
+  double unb = cntd > 1 ? var * cntd / (cntd - 1.0) : var;
+  rm[c] = (float)((1.0 - mom) * rm[c] + mom * mt);
+  rv[c] = (float)((1.0 - mom) * rv[c] + mom * unb);
+  if (c == 0 && nbt) nbt[0] += 1;
+}
+
+template <typename T>
+__global__ void k_bn_apply(const T* __restrict__ x, long P, int C, const float* __restrict__ scale,
+                           const float* __restrict__ shift, const T* __restrict__ res, int ldr, int cr0, int relu,
+                           T* __restrict__ y, int ldy, int cy0) {
+  constexpr int N = V16<T>::N;
+  const int CV = C / N;
+  const long total = P * CV;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    long p = e / CV;
+    int c = (int)(e - p * CV) * N;
+    float v[N], r[N];
+    V16<T>::load(x + p * C + c, v);
+    if (res) V16<T>::load(res + p * ldr + cr0 + c, r);
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      float o = v[i] * scale[c + i] + shift[c + i];
+      if (res) o += r[i];
+      if (relu) o = fmaxf(o, 0.f);
+      v[i] = o;
+    }
+    V16<T>::store(y + p * ldy + cy0 + c, v);
+  }
+}
+
+constexpr int BNB_PIX = 512;  // pixels per partial slot in the backward reduction
+
+// block: 256 threads = (C/N) chunk lanes x R rows
+template <typename T>
+__global__ void k_bn_bwd_reduce(const T* __restrict__ dy, int lddy, int cdy0, const T* __restrict__ y, int ldy, int cy0,
+                                const T* __restrict__ x, long P, int C, const float* __restrict__ save, int relu,
+                                float* __restrict__ part, int parts, int cgroups) {
+  constexpr int N = V16<T>::N;
+  __shared__ float red[2][256][N];
+  const int CV = C / N;
+  const int lanes = CV < 256 ? CV : 256;  // chunk lanes per row
+  const int R = 256 / lanes;
+  const int cgi = blockIdx.y;
+  const int cl = threadIdx.x % lanes, row = threadIdx.x / lanes;
+  const int c = (cgi * lanes + cl) * N;
+  const long p0 = (long)blockIdx.x * BNB_PIX;
+  const long p1 = min(P, p0 + BNB_PIX);
+  float sg[N], sgx[N], mean[N], inv[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    sg[i] = sgx[i] = 0.f;
+    mean[i] = (x && c < C) ? save[c + i] : 0.f;
+    inv[i] = (x && c < C) ? save[C + c + i] : 0.f;
+  }
+  if (row < R && c < C) {
+    for (long p = p0 + row; p < p1; p += R) {
+      float g[N], yy[N], xx[N];
+      V16<T>::load(dy + p * lddy + cdy0 + c, g);
+      if (relu) {
+        V16<T>::load(y + p * ldy + cy0 + c, yy);
+#pragma unroll
+        for (int i = 0; i < N; ++i) g[i] = yy[i] > 0.f ? g[i] : 0.f;
+      }
+      if (x) {
+        V16<T>::load(x + p * C + c, xx);
+#pragma unroll
+        for (int i = 0; i < N; ++i) sgx[i] += g[i] * (xx[i] - mean[i]) * inv[i];
+      }
+#pragma unroll
+      for (int i = 0; i < N; ++i) sg[i] += g[i];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    red[0][threadIdx.x][i] = sg[i];
+    red[1][threadIdx.x][i] = sgx[i];
+  }
+  __syncthreads();
+  if (row == 0 && c < C) {
+    for (int r = 1; r < R; ++r)
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        sg[i] += red[0][r * lanes + cl][i];
+        sgx[i] += red[1][r * lanes + cl][i];
+      }
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      part[(size_t)blockIdx.x * C + c + i] = sg[i];
+      part[((size_t)(parts + 1) + blockIdx.x) * C + c + i] = sgx[i];
+    }
+  }
+  (void)cgroups;
+}
+
+// totals over parts -> part[0][parts][c], part[1][parts][c]; dgamma / dbeta
+__global__ void k_bn_bwd_totals(float* __restrict__ part, int parts, int C, float* dgamma, float* dbeta, int accumulate) {
+  __shared__ double sh[2][8][33];
+  const int cl = threadIdx.x & 31, pl = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cl;
+  double s = 0, q = 0;
+  if (c < C)
+    for (int k = pl; k < parts; k += 8) {
+      s += part[(size_t)k * C + c];
+      q += part[((size_t)parts + 1 + k) * C + c];
+    }
+  sh[0][pl][cl] = s;
+  sh[1][pl][cl] = q;
+  __syncthreads();
+  if (pl != 0 || c >= C) return;
+  for (int k = 1; k < 8; ++k) {
+    s += sh[0][k][cl];
+    q += sh[1][k][cl];
+  }
+  part[(size_t)parts * C + c] = (float)s;
+  part[((size_t)parts + 1 + parts) * C + c] = (float)q;
+  if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)q : (float)q;
+  if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)s : (float)s;
+}
+
+template <typename T>
+__global__ void k_bn_bwd_apply(const T* __restrict__ dy, int lddy, int cdy0, const T* __restrict__ y, int ldy, int cy0,
+                               const T* __restrict__ x, long P, int C, const float* __restrict__ save,
+                               const float* __restrict__ part, int parts, const float* __restrict__ gamma, int relu,
+                               T* __restrict__ dx, T* __restrict__ dres, int lddres, int cdres0, int racc) {
+  constexpr int N = V16<T>::N;
+  const int CV = C / N;
+  const long total = P * CV;
+  const float invP = 1.f / (float)P;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    long p = e / CV;
+    int c = (int)(e - p * CV) * N;
+    float g[N], yy[N], xx[N], o[N];
+    V16<T>::load(dy + p * lddy + cdy0 + c, g);
+    if (relu) {
+      V16<T>::load(y + p * ldy + cy0 + c, yy);
+#pragma unroll
+      for (int i = 0; i < N; ++i) g[i] = yy[i] > 0.f ? g[i] : 0.f;
+    }
+    if (dx) {
+      V16<T>::load(x + p * C + c, xx);
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        int cc = c + i;
+        float mean = save[cc], inv = save[C + cc];
+        float sg = part[(size_t)parts * C + cc] * invP;
+        float sgx = part[((size_t)parts + 1 + parts) * C + cc] * invP;
+        float xh = (xx[i] - mean) * inv;
+        o[i] = gamma[cc] * inv * (g[i] - sg - xh * sgx);
+      }
+      V16<T>::store(dx + p * C + c, o);
+    }
+    if (dres) {
+      T* d = dres + p * lddres + cdres0 + c;
+      if (racc) {
+        float r[N];
+        V16<T>::load(d, r);
+#pragma unroll
+        for (int i = 0; i < N; ++i) r[i] += g[i];
+        V16<T>::store(d, r);
+      } else {
+        V16<T>::store(d, g);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ layout / pooling
+template <typename T>
+__global__ void k_nchw_to_nhwc(const float* __restrict__ x, int B, int C, int H, int W, int cpad, T* __restrict__ y) {
+  const long HW = (long)H * W, total = (long)B * HW;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    long b = e / HW, s = e - b * HW;
+    T* o = y + e * cpad;
+    for (int c = 0; c < cpad; ++c) o[c] = Elem<T>::cvt(c < C ? x[(b * C + c) * HW + s] : 0.f);
+  }
+}
+
+template <typename T>
+__global__ void k_maxpool(const T* __restrict__ x, int B, int IH, int IW, int ldx, int cx0, int C, T* __restrict__ y,
+                          int OH, int OW, int ldy, int cy0) {
+  constexpr int N = V16<T>::N;
+  const int CV = C / N;
+  const long total = (long)B * OH * OW * CV;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    long pix = e / CV;
+    int c = (int)(e - pix * CV) * N;
+    int ox = (int)(pix % OW);
+    long t = pix / OW;
+    int oy = (int)(t % OH), b = (int)(t / OH);
+    float m[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) m[i] = -INFINITY;
+    for (int ky = 0; ky < 3; ++ky) {
+      int iy = oy * 2 - 1 + ky;
+      if ((unsigned)iy >= (unsigned)IH) continue;
+      for (int kx = 0; kx < 3; ++kx) {
+        int ix = ox * 2 - 1 + kx;
+        if ((unsigned)ix >= (unsigned)IW) continue;
+        float v[N];
+        V16<T>::load(x + (((size_t)b * IH + iy) * IW + ix) * ldx + cx0 + c, v);
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+          if (v[i] > m[i] || isnan(v[i])) m[i] = v[i];  // PyTorch CPU max_pool2d rule
+      }
+    }
+    V16<T>::store(y + pix * ldy + cy0 + c, m);
+  }
+}
+
+// gather form: each input element receives dy of every window whose (first) argmax it is
+template <typename T>
+__global__ void k_maxpool_bwd(const T* __restrict__ x, int ldx, int cx0, const T* __restrict__ dy, int lddy, int cdy0,
+                              int B, int IH, int IW, int C, int OH, int OW, T* __restrict__ dx, int lddx, int cdx0,
+                              int accumulate) {
+  constexpr int N = V16<T>::N;
+  const int CV = C / N;
+  const long total = (long)B * IH * IW * CV;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    long pix = e / CV;
+    int c = (int)(e - pix * CV) * N;
+    int ix = (int)(pix % IW);
+    long t = pix / IW;
+    int iy = (int)(t % IH), b = (int)(t / IH);
+    float acc[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) acc[i] = 0.f;
+    int oy0 = (iy) / 2, oy1 = (iy + 1) / 2;  // windows oy with 2oy-1 <= iy <= 2oy+1
+    int ox0 = (ix) / 2, ox1 = (ix + 1) / 2;
+    for (int oy = oy0; oy <= oy1 && oy < OH; ++oy) {
+      if (oy * 2 - 1 > iy || oy * 2 + 1 < iy) continue;
+      for (int ox = ox0; ox <= ox1 && ox < OW; ++ox) {
+        if (ox * 2 - 1 > ix || ox * 2 + 1 < ix) continue;
+        float m[N];
+        int am[N];
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+          m[i] = -INFINITY;
+          am[i] = -1;
+        }
+        for (int ky = 0; ky < 3; ++ky) {
+          int yy = oy * 2 - 1 + ky;
+          if ((unsigned)yy >= (unsigned)IH) continue;
+          for (int kx = 0; kx < 3; ++kx) {
+            int xx = ox * 2 - 1 + kx;
+            if ((unsigned)xx >= (unsigned)IW) continue;
+            float v[N];
+            V16<T>::load(x + (((size_t)b * IH + yy) * IW + xx) * ldx + cx0 + c, v);
+#pragma unroll
+            for (int i = 0; i < N; ++i)
+              if (v[i] > m[i] || isnan(v[i])) {
+                m[i] = v[i];
+                am[i] = yy * IW + xx;
+              }
+          }
+        }
+        float g[N];
+        V16<T>::load(dy + (((size_t)b * OH + oy) * OW + ox) * lddy + cdy0 + c, g);
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+          if (am[i] == iy * IW + ix) acc[i] += g[i];
+      }
+    }
+    T* o = dx + pix * lddx + cdx0 + c;
+    if (accumulate) {
+      float r[N];
+      V16<T>::load(o, r);
+#pragma unroll
+      for (int i = 0; i < N; ++i) acc[i] += r[i];
+    }
+    V16<T>::store(o, acc);
+  }
+}
+
+template <typename T>
+__global__ void k_avgpool(const T* __restrict__ x, int H, int W, int ldx, int cx0, int C, T* __restrict__ y) {
+  const int b = blockIdx.y;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const long HW = (long)H * W;
+  double s = 0;  // CPU adaptive_avg_pool2d accumulates in acc_type<float> = double
+  for (long p = 0; p < HW; ++p) s += (double)Elem<T>::ld(x + ((size_t)b * HW + p) * ldx + cx0 + c);
+  y[(size_t)b * C + c] = Elem<T>::cvt((float)(s / (double)HW));
+}
+
+template <typename T>
+__global__ void k_sum_hw(const T* __restrict__ dy, int H, int W, int lddy, int cdy0, int C, T* __restrict__ out) {
+  const int b = blockIdx.y;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const long HW = (long)H * W;
+  float s = 0.f;
+  for (long p = 0; p < HW; ++p) s += Elem<T>::ld(dy + ((size_t)b * HW + p) * lddy + cdy0 + c);
+  out[(size_t)b * C + c] = Elem<T>::cvt(s);
+}
+
+template <typename T>
+__global__ void k_broadcast(const T* __restrict__ src, int B, int C, float mul, T* __restrict__ y, int H, int W, int ldy,
+                            int cy0, int accumulate, int convert) {
+  const long HW = (long)H * W, total = (long)B * HW * C;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    long pix = e / C;
+    int c = (int)(e - pix * C);
+    long b = pix / HW;
+    T* o = y + pix * ldy + cy0 + c;
+    if (!convert) {
+      *o = src[b * C + c];
+    } else {
+      float v = Elem<T>::ld(src + b * C + c) * mul;
+      if (accumulate) v += Elem<T>::ld(o);
+      *o = Elem<T>::cvt(v);
+    }
+  }
+}
+
+template <typename TX, typename TY>
+__global__ void k_copy_slice(const TX* __restrict__ x, int ldx, int cx0, TY* __restrict__ y, int ldy, int cy0, long P,
+                             int C, int accumulate) {
+  const long total = P * C;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    long p = e / C;
+    int c = (int)(e - p * C);
+    float v = Elem<TX>::ld(x + p * ldx + cx0 + c);
+    TY* o = y + p * ldy + cy0 + c;
+    if (accumulate) v += Elem<TY>::ld(o);
+    *o = Elem<TY>::cvt(v);
+  }
+}
+
+template <typename T>
+__global__ void k_head_grad(const float* __restrict__ dmask, const float* __restrict__ dcode, int B, int L, int H, int W,
+                            int ldy, T* __restrict__ y) {
+  const long HW = (long)H * W, total = (long)B * HW;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    long b = e / HW, s = e - b * HW;
+    T* o = y + e * ldy;
+    o[0] = Elem<T>::cvt(dmask[b * HW + s]);
+    for (int c = 0; c < L; ++c) o[1 + c] = Elem<T>::cvt(dcode[(b * L + c) * HW + s]);
+    for (int c = L + 1; c < ldy; ++c) o[c] = Elem<T>::cvt(0.f);
+  }
+}
+
+__global__ void k_threshold(const float* __restrict__ x, long n, int f64, void* out) {
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    bool b = x[e] > 8.940696716308594e-08f;  // NaN -> false
+    if (f64) ((double*)out)[e] = b ? 1.0 : 0.0;
+    else ((uint8_t*)out)[e] = b ? 1 : 0;
+  }
+}
+
+__global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
+                       long n, float lr_bc1, float b1, float b2, float bc2_sqrt, float eps) {
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    float gg = g[e];
+    float mm = m[e];
+    mm = mm + (1.f - b1) * (gg - mm);  // exp_avg.lerp_(grad, 1 - beta1)
+    float vv = v[e] * b2 + (1.f - b2) * gg * gg;
+    m[e] = mm;
+    v[e] = vv;
+    float denom = sqrtf(vv) / bc2_sqrt + eps;
+    p[e] = p[e] - lr_bc1 * (mm / denom);
+  }
+}
+
+}  // namespace zp
+
+using namespace zp;
+
+#define ZP_DTYPE_CHECK(fn, dt) ZP_CHECK_ARG((dt) == ZP_F32 || (dt) == ZP_BF16, fn ": bad dtype %d", (int)(dt))
+#define ZP_BY_DTYPE(dt, KERNEL, grid, block, st, ...)                                   \
+  do {                                                                                  \
+    if ((dt) == ZP_BF16) hipLaunchKernelGGL(KERNEL<bf16_t>, grid, block, 0, st, __VA_ARGS__); \
+    else hipLaunchKernelGGL(KERNEL<float>, grid, block, 0, st, __VA_ARGS__);            \
+  } while (0)
+
+extern "C" int zp_abi_version(void) { return ZP_ABI_VERSION; }
+extern "C" const char* zp_last_error(void) { return g_err; }
+extern "C" int zp_conv_rows_pad(int Cout) {
+  int tc = Cout > 64 ? 128 : (Cout > 32 ? 64 : 32);
+  return (Cout + tc - 1) / tc * tc;
+}
+
+extern "C" int zp_pack_weight(const float* src, int d0, int d1, int kh, int kw, int transposed, int ntaps, const int* ky,
+                              const int* kx, int cstride, int dtype, void* dst, int rows_pad, int k_pad, void* stream) {
+  ZP_DTYPE_CHECK("zp_pack_weight", dtype);
+  ZP_CHECK_ARG(src && dst && ky && kx, "zp_pack_weight: null pointer");
+  ZP_CHECK_ARG(ntaps >= 1 && ntaps <= ZP_MAX_TAPS, "zp_pack_weight: ntaps %d", ntaps);
+  ZP_CHECK_ARG(cstride >= (transposed ? d0 : d1) && (long)ntaps * cstride <= k_pad, "zp_pack_weight: cstride/k_pad");
+  ZP_CHECK_ARG(rows_pad >= (transposed ? d1 : d0), "zp_pack_weight: rows_pad");
+  PackArgs a;
+  a.src = src; a.dst = dst; a.d0 = d0; a.d1 = d1; a.kh = kh; a.kw = kw; a.transposed = transposed;
+  a.ntaps = ntaps; a.cstride = cstride; a.rows_pad = rows_pad; a.k_pad = k_pad;
+  for (int t = 0; t < ntaps; ++t) {
+    ZP_CHECK_ARG(ky[t] >= 0 && ky[t] < kh && kx[t] >= 0 && kx[t] < kw, "zp_pack_weight: tap %d out of range", t);
+    a.ky[t] = (signed char)ky[t];
+    a.kx[t] = (signed char)kx[t];
+  }
+  ZP_BY_DTYPE(dtype, k_pack, dim3(grid_for((long)rows_pad * k_pad)), dim3(256), (hipStream_t)stream, a);
+  ZP_LAUNCH_CHECK("zp_pack_weight");
+  return ZP_OK;
+}
+
+extern "C" int zp_bn_fold(const float* g, const float* b, const float* m, const float* v, const float* bias, float eps,
+                          int C, float* scale, float* shift, void* stream) {
+  ZP_CHECK_ARG(g && b && m && v && scale && shift && C > 0, "zp_bn_fold: bad args");
+  hipLaunchKernelGGL(k_bn_fold, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, g, b, m, v, bias, eps, C,
+                     scale, shift);
+  ZP_LAUNCH_CHECK("zp_bn_fold");
+  return ZP_OK;
+}
+
+extern "C" int zp_bn_train_finalize(const float* partials, int parts, int C, long long count, float eps, float momentum,
+                                    const float* gamma, const float* beta, const float* conv_bias, float* running_mean,
+                                    float* running_var, int64_t* nbt, float* scale, float* shift, float* save,
+                                    void* stream) {
+  ZP_CHECK_ARG(partials && gamma && beta && running_mean && running_var && scale && shift && save && parts > 0 &&
+                   C > 0 && count > 0,
+               "zp_bn_train_finalize: bad args");
+  hipLaunchKernelGGL(k_bn_train_finalize, dim3((C + 31) / 32), dim3(256), 0, (hipStream_t)stream, partials, parts, C,
+                     count, eps, momentum, gamma, beta, conv_bias, running_mean, running_var, nbt, scale, shift, save);
+  ZP_LAUNCH_CHECK("zp_bn_train_finalize");
+  return ZP_OK;
+}
+
+extern "C" int zp_bn_apply(const void* x, int P, int C, const float* scale, const float* shift, const void* res, int ldr,
+                           int cr0, int relu, int dtype, void* y, int ldy, int cy0, void* stream) {
+  ZP_DTYPE_CHECK("zp_bn_apply", dtype);
+  const int N = dtype == ZP_BF16 ? 8 : 4;
+  ZP_CHECK_ARG(x && y && scale && shift && P > 0 && C % N == 0 && ldy % N == 0 && cy0 % N == 0,
+               "zp_bn_apply: bad args");
+  if (res) ZP_CHECK_ARG(ldr % N == 0 && cr0 % N == 0, "zp_bn_apply: residual alignment");
+  long total = (long)P * (C / N);
+  if (dtype == ZP_BF16)
+    hipLaunchKernelGGL(k_bn_apply<bf16_t>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
+                       (long)P, C, scale, shift, (const bf16_t*)res, ldr, cr0, relu, (bf16_t*)y, ldy, cy0);
+  else
+    hipLaunchKernelGGL(k_bn_apply<float>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, (const float*)x,
+                       (long)P, C, scale, shift, (const float*)res, ldr, cr0, relu, (float*)y, ldy, cy0);
+  ZP_LAUNCH_CHECK("zp_bn_apply");
+  return ZP_OK;
+}
+
+extern "C" int zp_bn_bwd_parts(int P, int C) {
+  (void)C;
+  return (P + BNB_PIX - 1) / BNB_PIX;
+}
+
+extern "C" int zp_bn_bwd_reduce(const void* dy, int lddy, int cdy0, const void* y, int ldy, int cy0, const void* x, int P,
+                                int C, const float* save, int relu, int dtype, float* partials, float* dgamma,
+                                float* dbeta, int accumulate, void* stream) {
+  ZP_DTYPE_CHECK("zp_bn_bwd_reduce", dtype);
+  const int N = dtype == ZP_BF16 ? 8 : 4;
+  ZP_CHECK_ARG(dy && partials && P > 0 && C % N == 0 && (!relu || y) && (!x || save), "zp_bn_bwd_reduce: bad args");
+  ZP_CHECK_ARG(C / N <= 256 || (C / N) % 256 == 0, "zp_bn_bwd_reduce: C %d", C);
+  const int parts = zp_bn_bwd_parts(P, C);
+  const int CV = C / N;
+  const int cgroups = CV > 256 ? CV / 256 : 1;
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid(parts, cgroups);
+  if (dtype == ZP_BF16)
+    hipLaunchKernelGGL(k_bn_bwd_reduce<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)dy, lddy, cdy0, (const bf16_t*)y,
+                       ldy, cy0, (const bf16_t*)x, (long)P, C, save, relu, partials, parts, cgroups);
+  else
+    hipLaunchKernelGGL(k_bn_bwd_reduce<float>, grid, dim3(256), 0, st, (const float*)dy, lddy, cdy0, (const float*)y,
+                       ldy, cy0, (const float*)x, (long)P, C, save, relu, partials, parts, cgroups);
+  ZP_LAUNCH_CHECK("zp_bn_bwd_reduce");
+  hipLaunchKernelGGL(k_bn_bwd_totals, dim3((C + 31) / 32), dim3(256), 0, st, partials, parts, C, dgamma, dbeta,
+                     accumulate);
+  ZP_LAUNCH_CHECK("zp_bn_bwd_reduce totals");
+  return ZP_OK;
+}
+
+extern "C" int zp_bn_bwd_apply(const void* dy, int lddy, int cdy0, const void* y, int ldy, int cy0, const void* x, int P,
+                               int C, const float* save, const float* partials, const float* gamma, int relu, int dtype,
+                               void* dx, void* dres, int lddres, int cdres0, int res_accumulate, void* stream) {
+  ZP_DTYPE_CHECK("zp_bn_bwd_apply", dtype);
+  const int N = dtype == ZP_BF16 ? 8 : 4;
+  ZP_CHECK_ARG(dy && P > 0 && C % N == 0 && (!relu || y) && (!dx || (x && save && partials && gamma)),
+               "zp_bn_bwd_apply: bad args");
+  const int parts = zp_bn_bwd_parts(P, C);
+  long total = (long)P * (C / N);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == ZP_BF16)
+    hipLaunchKernelGGL(k_bn_bwd_apply<bf16_t>, dim3(grid_for(total)), dim3(256), 0, st, (const bf16_t*)dy, lddy, cdy0,
+                       (const bf16_t*)y, ldy, cy0, (const bf16_t*)x, (long)P, C, save, partials, parts, gamma, relu,
+                       (bf16_t*)dx, (bf16_t*)dres, lddres, cdres0, res_accumulate);
+  else
+    hipLaunchKernelGGL(k_bn_bwd_apply<float>, dim3(grid_for(total)), dim3(256), 0, st, (const float*)dy, lddy, cdy0,
+                       (const float*)y, ldy, cy0, (const float*)x, (long)P, C, save, partials, parts, gamma, relu,
+                       (float*)dx, (float*)dres, lddres, cdres0, res_accumulate);
+  ZP_LAUNCH_CHECK("zp_bn_bwd_apply");
+  return ZP_OK;
+}
+
+#define ZP_TLAUNCH(dt, KERNEL, grid, st, ...)                                                \
+  do {                                                                                      \
+    if ((dt) == ZP_BF16) {                                                                  \
+      using T = bf16_t;                                                                     \
+      hipLaunchKernelGGL(KERNEL<T>, grid, dim3(256), 0, st, __VA_ARGS__);                   \
+    } else {                                                                                \
+      using T = float;                                                                      \
+      hipLaunchKernelGGL(KERNEL<T>, grid, dim3(256), 0, st, __VA_ARGS__);                   \
+    }                                                                                       \
+  } while (0)
+
+extern "C" int zp_nchw_to_nhwc(const float* x, int B, int C, int H, int W, int cpad, int dtype, void* y, void* stream) {
+  ZP_DTYPE_CHECK("zp_nchw_to_nhwc", dtype);
+  ZP_CHECK_ARG(x && y && B > 0 && C > 0 && cpad >= C, "zp_nchw_to_nhwc: bad args");
+  ZP_TLAUNCH(dtype, k_nchw_to_nhwc, dim3(grid_for((long)B * H * W)), (hipStream_t)stream, x, B, C, H, W, cpad, (T*)y);
+  ZP_LAUNCH_CHECK("zp_nchw_to_nhwc");
+  return ZP_OK;
+}
+
+extern "C" int zp_maxpool3s2(const void* x, int B, int IH, int IW, int ldx, int cx0, int C, int dtype, void* y, int OH,
+                             int OW, int ldy, int cy0, void* stream) {
+  ZP_DTYPE_CHECK("zp_maxpool3s2", dtype);
+  const int N = dtype == ZP_BF16 ? 8 : 4;
+  ZP_CHECK_ARG(x && y && C % N == 0 && cx0 % N == 0 && ldx % N == 0 && cy0 % N == 0 && ldy % N == 0,
+               "zp_maxpool3s2: bad args / alignment");
+  ZP_CHECK_ARG(OH == (IH - 1) / 2 + 1 && OW == (IW - 1) / 2 + 1, "zp_maxpool3s2: OH/OW");
+  long total = (long)B * OH * OW * (C / N);
+  ZP_TLAUNCH(dtype, k_maxpool, dim3(grid_for(total)), (hipStream_t)stream, (const T*)x, B, IH, IW, ldx, cx0, C, (T*)y,
+             OH, OW, ldy, cy0);
+  ZP_LAUNCH_CHECK("zp_maxpool3s2");
+  return ZP_OK;
+}
+
+extern "C" int zp_maxpool3s2_bwd(const void* x, int ldx, int cx0, const void* dy, int lddy, int cdy0, int B, int IH,
+                                 int IW, int C, int OH, int OW, int dtype, void* dx, int lddx, int cdx0, int accumulate,
+                                 void* stream) {
+  ZP_DTYPE_CHECK("zp_maxpool3s2_bwd", dtype);
+  const int N = dtype == ZP_BF16 ? 8 : 4;
+  ZP_CHECK_ARG(x && dy && dx && C % N == 0 && cx0 % N == 0 && cdy0 % N == 0 && cdx0 % N == 0,
+               "zp_maxpool3s2_bwd: bad args");
+  long total = (long)B * IH * IW * (C / N);
+  ZP_TLAUNCH(dtype, k_maxpool_bwd, dim3(grid_for(total)), (hipStream_t)stream, (const T*)x, ldx, cx0, (const T*)dy,
+             lddy, cdy0, B, IH, IW, C, OH, OW, (T*)dx, lddx, cdx0, accumulate);
+  ZP_LAUNCH_CHECK("zp_maxpool3s2_bwd");
+  return ZP_OK;
+}
+
+extern "C" int zp_global_avgpool(const void* x, int B, int H, int W, int ldx, int cx0, int C, int dtype, void* y,
+                                 void* stream) {
+  ZP_DTYPE_CHECK("zp_global_avgpool", dtype);
+  ZP_CHECK_ARG(x && y && B > 0 && H > 0 && W > 0 && C > 0, "zp_global_avgpool: bad args");
+  ZP_TLAUNCH(dtype, k_avgpool, dim3((C + 255) / 256, B), (hipStream_t)stream, (const T*)x, H, W, ldx, cx0, C, (T*)y);
+  ZP_LAUNCH_CHECK("zp_global_avgpool");
+  return ZP_OK;
+}
+
+extern "C" int zp_broadcast_hw(const void* src, int B, int C, int dtype, void* y, int H, int W, int ldy, int cy0,
+                               void* stream) {
+  ZP_DTYPE_CHECK("zp_broadcast_hw", dtype);
+  ZP_CHECK_ARG(src && y && B > 0 && C > 0, "zp_broadcast_hw: bad args");
+  long total = (long)B * H * W * C;
+  ZP_TLAUNCH(dtype, k_broadcast, dim3(grid_for(total)), (hipStream_t)stream, (const T*)src, B, C, 1.f, (T*)y, H, W,
+             ldy, cy0, 0, 0);
+  ZP_LAUNCH_CHECK("zp_broadcast_hw");
+  return ZP_OK;
+}
+
+extern "C" int zp_sum_hw(const void* dy, int B, int H, int W, int lddy, int cdy0, int C, int dtype, void* out,
+                         void* stream) {
+  ZP_DTYPE_CHECK("zp_sum_hw", dtype);
+  ZP_CHECK_ARG(dy && out && B > 0 && C > 0, "zp_sum_hw: bad args");
+  ZP_TLAUNCH(dtype, k_sum_hw, dim3((C + 255) / 256, B), (hipStream_t)stream, (const T*)dy, H, W, lddy, cdy0, C,
+             (T*)out);
+  ZP_LAUNCH_CHECK("zp_sum_hw");
+  return ZP_OK;
+}
+
+extern "C" int zp_add_broadcast_hw(const void* src, float mul, int B, int C, int dtype, void* y, int H, int W, int ldy,
+                                   int cy0, int accumulate, void* stream) {
+  ZP_DTYPE_CHECK("zp_add_broadcast_hw", dtype);
+  ZP_CHECK_ARG(src && y && B > 0 && C > 0, "zp_add_broadcast_hw: bad args");
+  long total = (long)B * H * W * C;
+  ZP_TLAUNCH(dtype, k_broadcast, dim3(grid_for(total)), (hipStream_t)stream, (const T*)src, B, C, mul, (T*)y, H, W,
+             ldy, cy0, accumulate, 1);
+  ZP_LAUNCH_CHECK("zp_add_broadcast_hw");
+  return ZP_OK;
+}
+
+extern "C" int zp_copy_slice(const void* x, int ldx, int cx0, int xdtype, void* y, int ldy, int cy0, int ydtype, int P,
+                             int C, int accumulate, void* stream) {
+  ZP_DTYPE_CHECK("zp_copy_slice", xdtype);
+  ZP_DTYPE_CHECK("zp_copy_slice", ydtype);
+  ZP_CHECK_ARG(x && y && P > 0 && C > 0, "zp_copy_slice: bad args");
+  long total = (long)P * C;
+  dim3 g(grid_for(total));
+  hipStream_t st = (hipStream_t)stream;
+  if (xdtype == ZP_BF16 && ydtype == ZP_BF16)
+    hipLaunchKernelGGL((k_copy_slice<bf16_t, bf16_t>), g, dim3(256), 0, st, (const bf16_t*)x, ldx, cx0, (bf16_t*)y, ldy,
+                       cy0, (long)P, C, accumulate);
+  else if (xdtype == ZP_BF16)
+    hipLaunchKernelGGL((k_copy_slice<bf16_t, float>), g, dim3(256), 0, st, (const bf16_t*)x, ldx, cx0, (float*)y, ldy,
+                       cy0, (long)P, C, accumulate);
+  else if (ydtype == ZP_BF16)
+    hipLaunchKernelGGL((k_copy_slice<float, bf16_t>), g, dim3(256), 0, st, (const float*)x, ldx, cx0, (bf16_t*)y, ldy,
+                       cy0, (long)P, C, accumulate);
+  else
+    hipLaunchKernelGGL((k_copy_slice<float, float>), g, dim3(256), 0, st, (const float*)x, ldx, cx0, (float*)y, ldy,
+                       cy0, (long)P, C, accumulate);
+  ZP_LAUNCH_CHECK("zp_copy_slice");
+  return ZP_OK;
+}
+
+extern "C" int zp_head_grad_to_nhwc(const float* dmask, const float* dcode, int B, int L, int H, int W, int ldy,
+                                    int dtype, void* y, void* stream) {
+  ZP_DTYPE_CHECK("zp_head_grad_to_nhwc", dtype);
+  ZP_CHECK_ARG(dmask && dcode && y && ldy >= L + 1, "zp_head_grad_to_nhwc: bad args");
+  ZP_TLAUNCH(dtype, k_head_grad, dim3(grid_for((long)B * H * W)), (hipStream_t)stream, dmask, dcode, B, L, H, W, ldy,
+             (T*)y);
+  ZP_LAUNCH_CHECK("zp_head_grad_to_nhwc");
+  return ZP_OK;
+}
+
+extern "C" int zp_threshold(const float* logits, long long n, int out_f64, void* bits, void* stream) {
+  ZP_CHECK_ARG(logits && bits && n >= 0, "zp_threshold: bad args");
+  if (n == 0) return ZP_OK;
+  hipLaunchKernelGGL(k_threshold, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, logits, (long)n, out_f64, bits);
+  ZP_LAUNCH_CHECK("zp_threshold");
+  return ZP_OK;
+}
+
+extern "C" int zp_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long long n, double lr,
+                       double beta1, double beta2, double eps, long long step, void* stream) {
+  ZP_CHECK_ARG(param && grad && exp_avg && exp_avg_sq && n >= 0 && step >= 1, "zp_adam: bad args");
+  if (n == 0) return ZP_OK;
+  double bc1 = 1.0 - pow(beta1, (double)step);
+  double bc2 = 1.0 - pow(beta2, (double)step);
+  hipLaunchKernelGGL(k_adam, dim3(grid_for(n, 256, 16384)), dim3(256), 0, (hipStream_t)stream, param, grad, exp_avg,
+                     exp_avg_sq, (long)n, (float)(lr / bc1), (float)beta1, (float)beta2, (float)sqrt(bc2), (float)eps);
+  ZP_LAUNCH_CHECK("zp_adam");
+  return ZP_OK;
+}

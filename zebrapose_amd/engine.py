@@ -1,0 +1,533 @@
+"""Network executor: runs BinaryCodeNet_Deeplab's forward / backward as a sequence of libzp
+calls over NHWC activation buffers (host orchestration only -- every arithmetic op is a
+HIP kernel in libzp.so).
+
+Reference forward (what is executed, in order):
+  model/BinaryCodeNet.py:161-174  DeepLabV3.forward (concat branch) -> split [1, L]
+  model/resnet.py:233-246         stem (torchvision conv1/bn1/relu) -> x_128; maxpool + layer1 -> x_64;
+                                  layer2 -> x_32; layer4 (d2) -> x_16; layer5 (d4) -> x_high
+  model/aspp.py:83-114            4 ASPP branches + image pool -> cat(1280) -> 1x1 -> upsample_1
+                                  -> cat(x_64) -> upsample_2 -> cat(x_128) -> conv_1x1_4
+The torch.cat's are never materialised: producers write into channel slices of one buffer.
+
+Modes
+  eval  : BatchNorm folded into a per-channel scale/shift applied in the conv epilogue
+          (with bias, residual add and ReLU), one launch per conv (ASPP's four branches in one).
+  train : BatchNorm with batch statistics (per-channel sums emitted by the conv epilogue,
+          finalised on device, running stats updated with momentum 0.1, unbiased var), then
+          a fused scale/shift/residual/ReLU pass; the tape keeps what the backward needs.
+Backward (train): for each recorded op in reverse, BN backward (two passes), weight
+gradient (split-K implicit GEMM), data gradient (implicit GEMM accumulating into the
+input's gradient buffer).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import weakref
+
+import torch
+
+from . import _lib as L
+from . import geometry as G
+from .model.resnet import TVBottleneck
+
+_KE = {L.ZP_F32: 32, L.ZP_BF16: 64}
+_E = {L.ZP_F32: 4, L.ZP_BF16: 8}
+
+
+class Act:
+    """A channel slice [c0, c0 + C) of an NHWC buffer [B, H, W, ld]."""
+    __slots__ = ("buf", "c0", "C")
+
+    def __init__(self, buf, c0=0, C=None):
+        self.buf, self.c0 = buf, c0
+        self.C = buf.shape[3] - c0 if C is None else C
+
+    B = property(lambda s: s.buf.shape[0])
+    H = property(lambda s: s.buf.shape[1])
+    W = property(lambda s: s.buf.shape[2])
+    ld = property(lambda s: s.buf.shape[3])
+    P = property(lambda s: s.buf.shape[0] * s.buf.shape[1] * s.buf.shape[2])
+    ptr = property(lambda s: s.buf.data_ptr())
+
+
+def _i32arr(v):
+    return (C.c_int * len(v))(*v)
+
+
+class Unit:
+    """conv / transposed conv (+ bias) (+ BatchNorm) (+ residual) (+ ReLU)."""
+
+    def __init__(self, conv, bn=None, relu=True, cin_act=None):
+        self.conv, self.bn, self.relu = conv, bn, relu
+        self.kind = "convT" if isinstance(conv, torch.nn.ConvTranspose2d) else "conv"
+        self.k = conv.kernel_size[0]
+        self.s = conv.stride[0]
+        self.p = conv.padding[0]
+        self.d = conv.dilation[0]
+        self.cin_w, self.cout = conv.in_channels, conv.out_channels
+        self.cin = cin_act or self.cin_w
+
+    # geometry ---------------------------------------------------------------------------------
+    def fwd_plan(self, IH, IW):
+        if self.kind == "convT":
+            return G.convT_fwd(IH, IW, self.k, self.s, self.p, self.conv.output_padding[0])
+        return G.conv_fwd(IH, IW, self.k, self.s, self.p, self.d)
+
+    def dgrad_plan(self, IH, IW):
+        if self.kind == "convT":
+            return G.convT_dgrad(IH, IW, self.k, self.s, self.p)
+        return G.conv_dgrad(IH, IW, self.k, self.s, self.p, self.d)
+
+    def out_hw(self, IH, IW):
+        if self.kind == "convT":
+            op = self.conv.output_padding[0]
+            return (IH - 1) * self.s - 2 * self.p + self.k + op, (IW - 1) * self.s - 2 * self.p + self.k + op
+        return G.out_size(IH, self.k, self.s, self.p, self.d), G.out_size(IW, self.k, self.s, self.p, self.d)
+
+
+class Tape:
+    def __init__(self):
+        self.recs = []
+
+
+class Engine:
+    """Executes a BinaryCodeNet_Deeplab module tree (zebrapose_amd.model) with libzp."""
+
+    def __init__(self, net, dtype=torch.bfloat16):
+        self._net = weakref.ref(net)
+        self.dtype = dtype
+        self.dt = L.dtype_code(dtype)
+        self._packed = {}
+        self._folds = {}
+        self._fold_epoch = 0
+        self.timing = None  # optional list of (label, start_event, end_event) for conv launches
+
+    # ------------------------------------------------------------------ weight / BN caches
+    def invalidate(self):
+        self._packed.clear()
+        self._folds.clear()
+
+    def _pack(self, unit, sub, transposed, cstride, k_pad, rows, tag, cache):
+        w = unit.conv.weight
+        key = (id(unit.conv), tag, tuple(sub.taps), cstride, k_pad, self.dt)
+        ver = (w._version, w.data_ptr())
+        hit = self._packed.get(key) if cache else None
+        if hit is not None and hit[0] == ver:
+            return hit[1]
+        d0, d1 = w.shape[0], w.shape[1]
+        out = torch.empty((rows, k_pad), dtype=self.dtype, device=w.device)
+        ky = [t[0] for t in sub.taps]
+        kx = [t[1] for t in sub.taps]
+        L.call("zp_pack_weight", w.data_ptr(), d0, d1, w.shape[2], w.shape[3], transposed, len(sub.taps),
+               _i32arr(ky), _i32arr(kx), cstride, self.dt, out.data_ptr(), rows, k_pad, L.stream_ptr())
+        if cache:
+            self._packed[key] = (ver, out)
+        return out
+
+    def _fold(self, unit):
+        bn, bias = unit.bn, unit.conv.bias
+        if bn is None:
+            return None, bias
+        key = id(bn)
+        vers = (bn.weight._version, bn.bias._version, bn.running_mean._version, bn.running_var._version,
+                None if bias is None else bias._version, self._fold_epoch)
+        hit = self._folds.get(key)
+        if hit is not None and hit[0] == vers:
+            return hit[1], hit[2]
+        dev = bn.weight.device
+        scale = torch.empty(unit.cout, dtype=torch.float32, device=dev)
+        shift = torch.empty_like(scale)
+        L.call("zp_bn_fold", bn.weight.data_ptr(), bn.bias.data_ptr(), bn.running_mean.data_ptr(),
+               bn.running_var.data_ptr(), L.ptr(bias), C.c_float(bn.eps), unit.cout, scale.data_ptr(),
+               shift.data_ptr(), L.stream_ptr())
+        self._folds[key] = (vers, scale, shift)
+        return scale, shift
+
+    # ------------------------------------------------------------------ conv launch
+    def _conv(self, x: Act, plan, cout, weights, k_pad, rows, outs, res=None, relu=False,
+              out_mode=L.ZP_OUT_NHWC, stats=None, small=None, label=None):
+        """weights / outs: per sub.  outs[i] = (y_ptr, ldy, cy0, OH, OW, scale, shift, y2)."""
+        a = L.ConvArgs()
+        a.dtype = self.dt
+        a.x = x.ptr
+        a.ldx, a.cx0, a.IH, a.IW, a.Cin = x.ld, x.c0, x.H, x.W, x.C
+        a.N, a.GH, a.GW, a.sy, a.sx = x.B, plan.GH, plan.GW, plan.sy, plan.sy
+        a.Cout, a.k_pad, a.w_rows = cout, k_pad, rows
+        if res is not None:
+            a.res, a.ldr, a.cr0 = res.ptr, res.ld, res.c0
+        a.relu, a.out_mode = int(relu), out_mode
+        a.nsub = len(plan.subs)
+        for i, sb in enumerate(plan.subs):
+            s = a.sub[i]
+            y, ldy, cy0, OH, OW, scale, shift, y2 = outs[i]
+            s.w = weights[i].data_ptr()
+            s.scale, s.shift = L.ptr(scale), L.ptr(shift)
+            s.y, s.y2 = y, y2
+            s.ldy, s.cy0, s.OH, s.OW = ldy, cy0, OH, OW
+            s.oys, s.oyo, s.oxs, s.oxo = sb.oys, sb.oyo, sb.oxs, sb.oxo
+            s.ntaps = len(sb.taps)
+            for t, (ty, tx) in enumerate(sb.offs):
+                s.ty[t], s.tx[t] = ty, tx
+            if small is not None:
+                s.kw, s.dil, s.pad = small
+        parts = 0
+        if stats == "alloc":
+            parts = L.lib.zp_conv2d_stat_parts(C.byref(a))
+            stats = torch.empty(3 * parts * cout, dtype=torch.float32, device=x.buf.device)
+        if stats is not None:
+            a.stats = stats.data_ptr()
+        st = L.stream_ptr()
+        if self.timing is not None:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            L.check(L.lib.zp_conv2d(C.byref(a), st), "zp_conv2d")
+            e1.record()
+            flops = 2.0 * x.B * plan.GH * plan.GW * sum(len(sb.taps) for sb in plan.subs) * x.C * cout
+            self.timing.append((label, e0, e1, flops))
+        else:
+            L.check(L.lib.zp_conv2d(C.byref(a), st), "zp_conv2d")
+        return stats, parts
+
+    def _kpad(self, ntaps, cin):
+        return G.ceil_to(ntaps * cin, _KE[self.dt])
+
+    def _fwd_weights(self, unit, plan, cache):
+        kp = max(self._kpad(len(sb.taps), unit.cin) for sb in plan.subs)
+        rows = L.lib.zp_conv_rows_pad(unit.cout)
+        tr = 1 if unit.kind == "convT" else 0
+        ws = [self._pack(unit, sb, tr, unit.cin, kp, rows, "fwd", cache) for sb in plan.subs]
+        return ws, kp, rows
+
+    def _small(self, cin, k, d, p):
+        return (k, d, p) if cin < _KE[self.dt] else None
+
+    # ------------------------------------------------------------------ unit forward
+    def unit_fwd(self, unit, x: Act, out: Act, tape, res: Act = None, label=None):
+        assert x.C == unit.cin, (x.C, unit.cin)
+        plan = unit.fwd_plan(x.H, x.W)
+        OH, OW = unit.out_hw(x.H, x.W)
+        assert (out.H, out.W, out.C) == (OH, OW, unit.cout), ((out.H, out.W, out.C), (OH, OW, unit.cout))
+        train = tape is not None
+        ws, kp, rows = self._fwd_weights(unit, plan, cache=not train)
+        small = self._small(unit.cin, unit.k, unit.d, unit.p)
+        if not train or unit.bn is None:
+            scale, shift = self._fold(unit)
+            outs = [(out.ptr, out.ld, out.c0, OH, OW, scale, shift, None)] * len(plan.subs)
+            self._conv(x, plan, unit.cout, ws, kp, rows, outs, res, unit.relu, small=small, label=label)
+            if train:
+                tape.recs.append(("plain", unit, x, out, res, None, None))
+            return
+        bn = unit.bn
+        if bn.momentum is None:
+            raise NotImplementedError("BatchNorm momentum=None (cumulative average) is not supported")
+        P = x.B * OH * OW
+        if P <= 1:
+            raise ValueError("Expected more than 1 value per channel when training")
+        raw = torch.empty((x.B, OH, OW, unit.cout), dtype=self.dtype, device=x.buf.device)
+        outs = [(raw.data_ptr(), unit.cout, 0, OH, OW, None, None, None)] * len(plan.subs)
+        stats, parts = self._conv(x, plan, unit.cout, ws, kp, rows, outs, None, False, stats="alloc", small=small,
+                                  label=label)
+        dev = x.buf.device
+        scale = torch.empty(unit.cout, dtype=torch.float32, device=dev)
+        shift = torch.empty_like(scale)
+        save = torch.empty(2 * unit.cout, dtype=torch.float32, device=dev)
+        L.call("zp_bn_train_finalize", stats.data_ptr(), parts, unit.cout, P, C.c_float(bn.eps),
+               C.c_float(bn.momentum), bn.weight.data_ptr(), bn.bias.data_ptr(), L.ptr(unit.conv.bias),
+               bn.running_mean.data_ptr(), bn.running_var.data_ptr(), bn.num_batches_tracked.data_ptr(),
+               scale.data_ptr(), shift.data_ptr(), save.data_ptr(), L.stream_ptr())
+        L.call("zp_bn_apply", raw.data_ptr(), P, unit.cout, scale.data_ptr(), shift.data_ptr(),
+               None if res is None else res.ptr, 0 if res is None else res.ld, 0 if res is None else res.c0,
+               int(unit.relu), self.dt, out.ptr, out.ld, out.c0, L.stream_ptr())
+        self._fold_epoch += 1
+        tape.recs.append(("bn", unit, x, out, res, raw, save))
+
+    def aspp_branches_fwd(self, units, x: Act, outs_act, tape):
+        """The four parallel ASPP branches (aspp.py:89-92) -- one launch with four sub-problems in
+        eval mode (same input, own weights / BN / output slice)."""
+        if tape is not None:
+            for u, o in zip(units, outs_act):
+                self.unit_fwd(u, x, o, tape, label="aspp")
+            return
+        plans = [u.fwd_plan(x.H, x.W) for u in units]
+        kp = max(self._kpad(len(p.subs[0].taps), x.C) for p in plans)
+        rows = L.lib.zp_conv_rows_pad(256)
+        merged = G.Plan(plans[0].GH, plans[0].GW, 1, [p.subs[0] for p in plans])
+        ws, outs = [], []
+        for u, p, o in zip(units, plans, outs_act):
+            ws.append(self._pack(u, p.subs[0], 0, x.C, kp, rows, "fwd", True))
+            scale, shift = self._fold(u)
+            outs.append((o.ptr, o.ld, o.c0, o.H, o.W, scale, shift, None))
+        self._conv(x, merged, 256, ws, kp, rows, outs, None, True, label="aspp")
+
+    def head_fwd(self, unit, x: Act, mask, code, tape):
+        plan = unit.fwd_plan(x.H, x.W)
+        OH, OW = unit.out_hw(x.H, x.W)
+        ws, kp, rows = self._fwd_weights(unit, plan, cache=tape is None)
+        outs = [(mask.data_ptr(), 0, 0, OH, OW, None, unit.conv.bias, code.data_ptr())]
+        self._conv(x, plan, unit.cout, ws, kp, rows, outs, None, False, out_mode=L.ZP_OUT_HEAD_NCHW,
+                   small=self._small(unit.cin, unit.k, unit.d, unit.p), label="head")
+        if tape is not None:
+            tape.recs.append(("head", unit, x, None, None, None, None))
+
+    # ------------------------------------------------------------------ backward pieces
+    def _grad(self, gmap, act: Act):
+        """gradient slice twin of an activation slice (zero-initialised buffer per activation buffer)."""
+        key = act.buf.data_ptr()
+        g = gmap.get(key)
+        if g is None:
+            g = torch.zeros_like(act.buf)
+            gmap[key] = g
+        return Act(g, act.c0, act.C)
+
+    def _wgrad(self, unit, x: Act, plan, dy: Act, dw):
+        a = L.WgradArgs()
+        a.dtype = self.dt
+        a.x, a.ldx, a.cx0, a.IH, a.IW, a.Cin = x.ptr, x.ld, x.c0, x.H, x.W, x.C
+        a.N, a.GH, a.GW, a.sy, a.sx = x.B, plan.GH, plan.GW, plan.sy, plan.sy
+        a.Cout, a.Cw, a.kh, a.kw = unit.cout, unit.cin_w, unit.k, unit.k
+        a.transposed_w = 1 if unit.kind == "convT" else 0
+        a.nsub = len(plan.subs)
+        for i, sb in enumerate(plan.subs):
+            s = a.sub[i]
+            s.dy, s.lddy, s.cdy0, s.OH, s.OW = dy.ptr, dy.ld, dy.c0, dy.H, dy.W
+            s.oys, s.oyo, s.oxs, s.oxo = sb.oys, sb.oyo, sb.oxs, sb.oxo
+            s.ntaps = len(sb.taps)
+            for t, ((ky, kx), (ty, tx)) in enumerate(zip(sb.taps, sb.offs)):
+                s.ky[t], s.kx[t], s.ty[t], s.tx[t] = ky, kx, ty, tx
+        a.dw = dw.data_ptr()
+        a.accumulate = 0
+        nbytes = L.lib.zp_conv2d_wgrad_ws_bytes(C.byref(a))
+        ws = torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=dw.device)
+        L.check(L.lib.zp_conv2d_wgrad(C.byref(a), ws.data_ptr(), L.stream_ptr()), "zp_conv2d_wgrad")
+
+    def _dgrad(self, unit, gy: Act, gx: Act):
+        """gx (+)= dgrad(gy): accumulate into the input gradient slice (residual = itself)."""
+        plan = unit.dgrad_plan(gx.H, gx.W)
+        cin_l = gy.C  # = cout (padded for the head)
+        kp = max(self._kpad(len(sb.taps), cin_l) for sb in plan.subs)
+        rows = L.lib.zp_conv_rows_pad(unit.cin)
+        tr = 0 if unit.kind == "convT" else 1
+        ws = [self._pack(unit, sb, tr, cin_l, kp, rows, "dgrad", False) for sb in plan.subs]
+        outs = [(gx.ptr, gx.ld, gx.c0, gx.H, gx.W, None, None, None)] * len(plan.subs)
+        small = self._small(cin_l, unit.k, -unit.d, -unit.p) if unit.kind == "conv" and unit.s == 1 else None
+        if cin_l < _KE[self.dt]:
+            assert small is not None, "small-channel dgrad only for stride-1 convs"
+        self._conv(gy, plan, unit.cin, ws, kp, rows, outs, res=gx, relu=False, small=small, label="dgrad")
+
+    def unit_bwd(self, rec, gmap, grads, need_dx=True):
+        kind, unit, x, out, res, raw, save = rec
+        conv, bn = unit.conv, unit.bn
+        dev = x.buf.device
+        st = L.stream_ptr()
+        plan = unit.fwd_plan(x.H, x.W)
+        if kind == "head":
+            gy = gmap["head"]
+        else:
+            gout = self._grad(gmap, out)
+            if kind == "bn":
+                P = out.P
+                parts = L.lib.zp_bn_bwd_parts(P, unit.cout)
+                partials = torch.empty(2 * (parts + 1) * unit.cout, dtype=torch.float32, device=dev)
+                dgamma = torch.empty_like(bn.weight)
+                dbeta = torch.empty_like(bn.bias)
+                L.call("zp_bn_bwd_reduce", gout.ptr, gout.ld, gout.c0, out.ptr, out.ld, out.c0, raw.data_ptr(), P,
+                       unit.cout, save.data_ptr(), int(unit.relu), self.dt, partials.data_ptr(), dgamma.data_ptr(),
+                       dbeta.data_ptr(), 0, st)
+                graw = torch.empty_like(raw)
+                gres = self._grad(gmap, res) if res is not None else None
+                L.call("zp_bn_bwd_apply", gout.ptr, gout.ld, gout.c0, out.ptr, out.ld, out.c0, raw.data_ptr(), P,
+                       unit.cout, save.data_ptr(), partials.data_ptr(), bn.weight.data_ptr(), int(unit.relu),
+                       self.dt, graw.data_ptr(), None if gres is None else gres.ptr,
+                       0 if gres is None else gres.ld, 0 if gres is None else gres.c0, 1, st)
+                grads[bn.weight] = dgamma
+                grads[bn.bias] = dbeta
+                if conv.bias is not None:
+                    # train-mode BN removes the per-channel mean: d loss / d conv bias == 0 exactly
+                    grads[conv.bias] = torch.zeros_like(conv.bias)
+                gy = Act(graw)
+            else:
+                raise NotImplementedError("eval-mode backward")
+        if kind == "head" and conv.bias is not None:
+            partials = torch.empty(2 * (L.lib.zp_bn_bwd_parts(gy.P, gy.ld) + 1) * gy.ld, dtype=torch.float32,
+                                   device=dev)
+            db = torch.empty(gy.ld, dtype=torch.float32, device=dev)
+            L.call("zp_bn_bwd_reduce", gy.ptr, gy.ld, 0, None, 0, 0, None, gy.P, gy.ld, None, 0, self.dt,
+                   partials.data_ptr(), None, db.data_ptr(), 0, st)
+            grads[conv.bias] = db[:unit.cout]
+        dw = torch.empty_like(conv.weight)
+        wdy = Act(gy.buf, 0, unit.cout) if kind == "head" else gy
+        self._wgrad(unit, x, plan, wdy, dw)
+        grads[conv.weight] = dw
+        if need_dx:
+            self._dgrad(unit, gy, self._grad(gmap, x))
+
+    # ------------------------------------------------------------------ network
+    def forward(self, x, train):
+        """x f32 NCHW [B, 3, H, W] -> (mask [B,1,H/2,W/2], code [B,L,H/2,W/2]) f32, tape (train)."""
+        dl = self._net()
+        rn, aspp = dl.resnet, dl.aspp
+        if not rn.concat_decoder:
+            raise NotImplementedError("concat=False: the reference forward cannot run this configuration "
+                                      "(aspp.py:112 concatenates x_128=None)")
+        if x.dim() != 4 or x.shape[1] != 3:
+            raise ValueError(f"expected input [B, 3, H, W], got {tuple(x.shape)}")
+        if x.dtype != torch.float32 or not x.is_cuda:
+            raise ValueError("input must be a float32 CUDA (HIP) tensor")
+        x = x.contiguous()
+        B, _, H, W = x.shape
+        if H % 8 or W % 8:
+            raise ValueError("input height / width must be multiples of 8")
+        dev, dt = x.device, self.dtype
+        tape = Tape() if train else None
+
+        def new(h, w, c):
+            return Act(torch.empty((B, h, w, c), dtype=dt, device=dev))
+
+        st = L.stream_ptr()
+        xin = new(H, W, 8)
+        L.call("zp_nchw_to_nhwc", x.data_ptr(), B, 3, H, W, 8, self.dt, xin.ptr, st)
+        r = rn.resnet
+        H2, W2 = H // 2, W // 2
+        H4, W4, H8, W8 = H // 4, W // 4, H // 8, W // 8
+        c64 = 64 if rn.num_layers == 34 else 256
+        head_in = torch.empty((B, H2, W2, 320), dtype=dt, device=dev)
+        x128 = Act(head_in, 256, 64)
+        self.unit_fwd(self._u(r[0], r[1], True, cin_act=8), xin, x128, tape, label="stem")
+        pooled = new(H4, W4, 64)
+        L.call("zp_maxpool3s2", x128.ptr, B, H2, W2, x128.ld, x128.c0, 64, self.dt, pooled.ptr, H4, W4, 64, 0, st)
+        if tape is not None:
+            tape.recs.append(("maxpool", x128, pooled))
+        up2_in = torch.empty((B, H4, W4, 256 + c64), dtype=dt, device=dev)
+        x64 = Act(up2_in, 256, c64)
+        h = self._layer(r[4], pooled, x64, tape)
+        h = self._layer(r[5], h, None, tape)
+        h = self._layer(rn.layer4, h, None, tape)
+        xh = self._layer(rn.layer5, h, None, tape)
+        # ---- ASPP (aspp.py:83-99)
+        A = torch.empty((B, H8, W8, 1280), dtype=dt, device=dev)
+        br = [self._u(aspp.conv_1x1_1, aspp.bn_conv_1x1_1), self._u(aspp.conv_3x3_1, aspp.bn_conv_3x3_1),
+              self._u(aspp.conv_3x3_2, aspp.bn_conv_3x3_2), self._u(aspp.conv_3x3_3, aspp.bn_conv_3x3_3)]
+        self.aspp_branches_fwd(br, xh, [Act(A, 256 * i, 256) for i in range(4)], tape)
+        pool = Act(torch.empty((B, 1, 1, xh.C), dtype=dt, device=dev))
+        L.call("zp_global_avgpool", xh.ptr, B, H8, W8, xh.ld, xh.c0, xh.C, self.dt, pool.ptr, st)
+        if tape is not None:  # tape order = forward order (the backward walks it reversed)
+            tape.recs.append(("avgpool", xh, pool))
+        imgo = Act(torch.empty((B, 1, 1, 256), dtype=dt, device=dev))
+        self.unit_fwd(self._u(aspp.conv_1x1_2, aspp.bn_conv_1x1_2), pool, imgo, tape, label="aspp_pool")
+        L.call("zp_broadcast_hw", imgo.ptr, B, 256, self.dt, A.data_ptr(), H8, W8, 1280, 1024, st)
+        if tape is not None:
+            tape.recs.append(("broadcast", imgo, Act(A, 1024, 256)))
+        o = new(H8, W8, 256)
+        self.unit_fwd(self._u(aspp.conv_1x1_3, aspp.bn_conv_1x1_3), Act(A), o, tape, label="aspp_proj")
+        # ---- decoder (aspp.py:101-112)
+        self._upsample(aspp.upsample_1, o, Act(up2_in, 0, 256), tape)
+        self._upsample(aspp.upsample_2, Act(up2_in), Act(head_in, 0, 256), tape)
+        ncls = aspp.conv_1x1_4.out_channels
+        mask = torch.empty((B, 1, H2, W2), dtype=torch.float32, device=dev)
+        code = torch.empty((B, ncls - 1, H2, W2), dtype=torch.float32, device=dev)
+        self.head_fwd(self._u(aspp.conv_1x1_4, None, False), Act(head_in), mask, code, tape)
+        return mask, code, tape
+
+    def _u(self, conv, bn=None, relu=True, cin_act=None):
+        key = (id(conv), id(bn), relu, cin_act)
+        cache = self.__dict__.setdefault("_units", {})
+        u = cache.get(key)
+        if u is None:
+            u = cache[key] = Unit(conv, bn, relu, cin_act)
+        return u
+
+    def _upsample(self, seq, x: Act, out: Act, tape):
+        h1 = self._u(seq[0], seq[1])
+        OH, OW = h1.out_hw(x.H, x.W)
+        dev, dt = x.buf.device, self.dtype
+        t1 = Act(torch.empty((x.B, OH, OW, 256), dtype=dt, device=dev))
+        self.unit_fwd(h1, x, t1, tape, label="upconvT")
+        t2 = Act(torch.empty((x.B, OH, OW, 256), dtype=dt, device=dev))
+        self.unit_fwd(self._u(seq[3], seq[4]), t1, t2, tape, label="upconv")
+        self.unit_fwd(self._u(seq[6], seq[7]), t2, out, tape, label="upconv")
+
+    def _layer(self, seq, x: Act, final_out: Act, tape):
+        n = len(seq)
+        for i, blk in enumerate(seq):
+            x = self._block(blk, x, final_out if i == n - 1 else None, tape)
+        return x
+
+    def _block(self, blk, x: Act, out: Act, tape):
+        dev, dt = x.buf.device, self.dtype
+        if isinstance(blk, TVBottleneck):
+            u1 = self._u(blk.conv1, blk.bn1)
+            u2 = self._u(blk.conv2, blk.bn2)
+            u3 = self._u(blk.conv3, blk.bn3)
+            h1, w1 = u1.out_hw(x.H, x.W)
+            t1 = Act(torch.empty((x.B, h1, w1, u1.cout), dtype=dt, device=dev))
+            self.unit_fwd(u1, x, t1, tape, label="enc")
+            h2, w2 = u2.out_hw(h1, w1)
+            t2 = Act(torch.empty((x.B, h2, w2, u2.cout), dtype=dt, device=dev))
+            self.unit_fwd(u2, t1, t2, tape, label="enc")
+            last, mid = u3, t2
+        else:
+            u1 = self._u(blk.conv1, blk.bn1)
+            h1, w1 = u1.out_hw(x.H, x.W)
+            t1 = Act(torch.empty((x.B, h1, w1, u1.cout), dtype=dt, device=dev))
+            self.unit_fwd(u1, x, t1, tape, label="enc")
+            last, mid = self._u(blk.conv2, blk.bn2, True), t1
+        ds = blk.downsample
+        if ds is not None and len(ds) > 0:
+            ud = self._u(ds[0], ds[1], False)
+            hd, wd = ud.out_hw(x.H, x.W)
+            res = Act(torch.empty((x.B, hd, wd, ud.cout), dtype=dt, device=dev))
+            self.unit_fwd(ud, x, res, tape, label="enc_ds")
+        else:
+            res = x
+        if out is None:
+            oh, ow = last.out_hw(mid.H, mid.W)
+            out = Act(torch.empty((x.B, oh, ow, last.cout), dtype=dt, device=dev))
+        self.unit_fwd(last, mid, out, tape, res=res, label="enc")
+        return out
+
+    def backward(self, tape, dmask, dcode):
+        """Returns {parameter: gradient} for every parameter of the network."""
+        gmap, grads = {}, {}
+        st = L.stream_ptr()
+        head_rec = tape.recs[-1]
+        assert head_rec[0] == "head"
+        hin = head_rec[2]
+        B, H2, W2 = hin.B, hin.H, hin.W
+        ncls = head_rec[1].cout
+        dev = hin.buf.device
+        if dmask is None:
+            dmask = torch.zeros((B, 1, H2, W2), dtype=torch.float32, device=dev)
+        if dcode is None:
+            dcode = torch.zeros((B, ncls - 1, H2, W2), dtype=torch.float32, device=dev)
+        dmask, dcode = dmask.contiguous().float(), dcode.contiguous().float()
+        ldh = 32 if ncls <= 32 else G.ceil_to(ncls, 64)
+        ghead = torch.empty((B, H2, W2, ldh), dtype=self.dtype, device=dev)
+        L.call("zp_head_grad_to_nhwc", dmask.data_ptr(), dcode.data_ptr(), B, ncls - 1, H2, W2, ldh, self.dt,
+               ghead.data_ptr(), st)
+        gmap["head"] = Act(ghead)
+        for rec in reversed(tape.recs):
+            kind = rec[0]
+            if kind in ("plain", "bn", "head"):
+                need_dx = rec[2].ld != 8  # the NHWC image input needs no gradient
+                self.unit_bwd(rec, gmap, grads, need_dx=need_dx)
+            elif kind == "maxpool":
+                _, xa, pa = rec
+                gp = self._grad(gmap, pa)
+                gx = self._grad(gmap, xa)
+                L.call("zp_maxpool3s2_bwd", xa.ptr, xa.ld, xa.c0, gp.ptr, gp.ld, gp.c0, xa.B, xa.H, xa.W, xa.C, pa.H,
+                       pa.W, self.dt, gx.ptr, gx.ld, gx.c0, 1, st)
+            elif kind == "broadcast":
+                _, src, dst = rec
+                gd = self._grad(gmap, dst)
+                gs = self._grad(gmap, src)
+                L.call("zp_sum_hw", gd.ptr, gd.B, gd.H, gd.W, gd.ld, gd.c0, gd.C, self.dt, gs.ptr, st)
+            elif kind == "avgpool":
+                _, xa, pa = rec
+                gp = self._grad(gmap, pa)
+                gx = self._grad(gmap, xa)
+                L.call("zp_add_broadcast_hw", gp.ptr, C.c_float(1.0 / (xa.H * xa.W)), xa.B, xa.C, self.dt, gx.ptr,
+                       xa.H, xa.W, gx.ld, gx.c0, 1, st)
+        return grads
+
