@@ -1,0 +1,248 @@
+#!/usr/bin/env python3
+"""ZebraPose hot-path benchmark on MI355X (BASELINE.json metric: 256x256 crops/s/GPU).
+
+One *step* = one pass of the hot path over one batch of synthetic crops resident in HBM:
+BinaryCodeNet_Deeplab(34, 16, 2, concat=True) forward at bs=32 (bf16 MFMA, f32 accumulate)
++ the on-device code->vertex decode (configs[1] of BASELINE.json).  `value` is the whole-job
+throughput (crops/s summed over ranks; each rank runs its own independent batch: the inference
+path shards by crop with no collective -> weak scaling).
+
+Extra fields: the training step (configs[2]/[3]: bs=32 per GPU, hist-weighted BCE + mask loss,
+backward, Adam; DDP over RCCL when N > 1), the dominant kernel's roofline (HIP events around its
+launches over a timed pass), and the CPU baseline (the oracle restatement on the host cores,
+rank 0, N = 1, bounded sample).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-train] [--no-cpu]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+os.environ.setdefault("ZP_QUIET", "1")
+
+PEAK = {"bf16": 2516.6, "fp32": 157.3}  # TFLOP/s dense MFMA (256 CU x 4 SIMD x 2.4 GHz; MI355X_MICROARCH.md)
+FWD_GFLOP_PER_CROP = 109.136  # 2 x 54,568,026,112 MAC per 256x256 crop (R34)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-train", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--train-steps", type=int, default=None)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    return ap.parse_args()
+
+
+def calibrate_bn(net, x):
+    """Synthetic checkpoint: BN running stats := batch statistics of one train-mode pass."""
+    bns = [m for m in net.modules() if isinstance(m, torch.nn.BatchNorm2d)]
+    for m in bns:
+        m.momentum = 1.0
+    net.train()
+    with torch.no_grad():
+        net(x)
+    for m in bns:
+        m.momentum = 0.1
+    net.eval()
+
+
+def synthetic_crops(B, S, device, seed):
+    """uint8 HWC crops normalised as the reference's loader does (bop_dataset_pytorch.py:333-347;
+    BGR order with RGB ImageNet constants)."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    u8 = torch.randint(0, 256, (B, 3, S, S), generator=g, dtype=torch.uint8)
+    mean = torch.tensor([0.485, 0.456, 0.406]).view(1, 3, 1, 1)
+    std = torch.tensor([0.229, 0.224, 0.225]).view(1, 3, 1, 1)
+    return ((u8.float() / 255.0 - mean) / std).to(device)
+
+
+def synthetic_lut(seed=0):
+    rng = np.random.default_rng(seed)
+    lut = rng.standard_normal((65536, 3)) * 50.0
+    lut[::97] = np.nan
+    return lut
+
+
+def kernel_name(dt, cout, cin_l):
+    wc = 4 if cout > 64 else (2 if cout > 32 else 1)
+    small = cin_l < (64 if dt == "bf16" else 32)
+    return f"k_conv<{'bf16' if dt == 'bf16' else 'f32'},WC={wc},WP=4,smallC={int(small)}>"
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from zebrapose_amd.model.BinaryCodeNet import BinaryCodeNet_Deeplab
+    from zebrapose_amd.decode import Decoder
+
+    torch.manual_seed(1234)
+    net = BinaryCodeNet_Deeplab(34, 16, 2, concat=True, output_kernel_size=1, precision=args.precision).to(dev)
+    B, S = args.batch, args.size
+    x = synthetic_crops(B, S, dev, seed=100 + rank)
+    calibrate_bn(net, x)
+    dec = Decoder(synthetic_lut(), device=dev)
+    rng = np.random.default_rng(rank)
+    side = rng.integers(64, 401, B)
+    bboxes = np.stack([rng.integers(0, 300, B), rng.integers(0, 200, B), side, side], 1)
+
+    def step():
+        with torch.no_grad():
+            m, c = net(x)
+            return dec(m, c, bboxes, bbox_size=S // 2)
+
+    # ------------------------------------------------------------------ inference (value)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = t.item()
+    ms_per_step = el / args.steps * 1e3
+    value = world * B * args.steps / el
+    n_corr = int(out[0].sum().item())
+
+    # ------------------------------------------------------------------ roofline of the dominant kernel
+    eng = net.net._engine
+    eng.timing = []
+    with torch.no_grad():
+        for _ in range(args.steps):
+            net(x)
+    torch.cuda.synchronize()
+    per = {}
+    eng_t = eng.timing
+    eng.timing = None
+    # group launches by kernel instantiation (the names rocprofv3 reports)
+    for rec in eng_t:
+        label, e0, e1, flops, kname = rec
+        d = per.setdefault(kname, [0.0, 0.0, 0])
+        d[0] += flops
+        d[1] += e0.elapsed_time(e1) * 1e-3
+        d[2] += 1
+    dom = max(per.items(), key=lambda kv: kv[1][1])
+    kname, (fl, tsec, nl) = dom
+    achieved = fl / tsec / 1e12
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+    if os.path.exists(pmc_path):
+        try:
+            traffic = json.load(open(pmc_path)).get(kname)
+        except Exception:
+            traffic = None
+    all_conv_flops = sum(v[0] for v in per.values())
+    all_conv_time = sum(v[1] for v in per.values())
+    roofline = {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 2), "peak": PEAK[args.precision],
+                "unit": "TFLOP/s", "frac": round(achieved / PEAK[args.precision], 4), "traffic": traffic,
+                "launches_per_step": nl // args.steps, "avg_launch_us": round(tsec / nl * 1e6, 2),
+                "all_conv_tflops": round(all_conv_flops / all_conv_time / 1e12, 2),
+                "whole_step_tflops": round(FWD_GFLOP_PER_CROP * 1e9 * B / (ms_per_step * 1e-3) / 1e12, 2)}
+
+    # ------------------------------------------------------------------ training step (extra)
+    train = None
+    if not args.no_train:
+        from zebrapose_amd.train import TrainStep
+        tnet = BinaryCodeNet_Deeplab(34, 16, 2, concat=True, output_kernel_size=1, precision=args.precision).to(dev)
+        calibrate_bn(tnet, x)
+        tnet.train()
+        lr = 2e-4 * world  # train_v6.py:89-91
+        ts = TrainStep(tnet, learning_rate=lr)
+        g = torch.Generator(device="cpu").manual_seed(7 + rank)
+        gt_code = (torch.rand((B, 16, S // 2, S // 2), generator=g) < 0.5).to(torch.uint8).to(dev)
+        gt_mask = (torch.rand((B, S // 2, S // 2), generator=g) < 0.7).float().to(dev)
+        K = args.train_steps or max(3, args.steps // 2)
+        for _ in range(max(2, args.warmup // 2)):
+            ts(x, gt_code, gt_mask)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(K):
+            loss = ts(x, gt_code, gt_mask)
+        torch.cuda.synchronize()
+        tel = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([tel], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            tel = t.item()
+        train = {"crops_per_s": round(world * B * K / tel, 2), "ms_per_step": round(tel / K * 1e3, 3),
+                 "steps": K, "global_batch": world * B, "loss": round(float(loss[0].item()), 5),
+                 "achieved_tflops": round(3 * FWD_GFLOP_PER_CROP * 1e9 * world * B * K / tel / 1e12 / world, 2),
+                 "parallelism": f"ddp{world}" if world > 1 else "single"}
+        del ts, tnet
+
+    # ------------------------------------------------------------------ CPU baseline (rank 0, N = 1)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        from oracle import ref_cpu
+        threads = min(16, os.cpu_count() or 1)
+        torch.set_num_threads(threads)
+        sd = {k: v.detach().cpu() for k, v in net.state_dict().items()}
+        xb = x[:2].cpu()
+        lut = synthetic_lut()
+        with torch.no_grad():
+            ref_cpu.forward(sd, xb, 34)
+            n = 0
+            t0 = time.perf_counter()
+            while True:
+                m, c = ref_cpu.forward(sd, xb, 34)
+                for b in range(xb.shape[0]):
+                    ref_cpu.decode_crop(m[b, 0].numpy(), c[b].numpy(), lut, bboxes[b])
+                n += xb.shape[0]
+                if time.perf_counter() - t0 > args.cpu_seconds:
+                    break
+            cel = time.perf_counter() - t0
+        cpu = {"value": round(n / cel, 3), "unit": "crops/s", "cores": threads, "kind": "port",
+               "sample": f"{n} crops (batches of 2, 256x256) through oracle/ref_cpu.py forward (torch CPU fp32) + "
+                         f"numpy decode, {cel:.1f} s on {threads} threads"}
+
+    if rank == 0:
+        line = {"metric": "256x256 crops/sec (R34 DeepLabv3 inference bs=32, forward + code->vertex decode)",
+                "value": round(value, 2), "unit": "crops/s", "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+                "scaling": "weak", "vs_baseline": None, "dtype": args.precision, "data": "synthetic",
+                "config": {"workload": "configs[1]: ResNet34+DeepLabv3 inference bs=32 on 1xMI355X, synthetic "
+                                       "256x256 crops, 16-bit code head, on-device decode",
+                           "model": "BinaryCodeNet_Deeplab(34, 16, 2, concat=True)", "global_batch": world * B,
+                           "per_gpu_batch": B, "input": f"{S}x{S}", "parallelism": f"replicas{world}",
+                           "correspondences_last_step": n_corr},
+                "roofline": roofline, "cpu_baseline": cpu, "train": train}
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -185,7 +185,10 @@ class Engine:
             L.check(L.lib.zp_conv2d(C.byref(a), st), "zp_conv2d")
             e1.record()
             flops = 2.0 * x.B * plan.GH * plan.GW * sum(len(sb.taps) for sb in plan.subs) * x.C * cout
-            self.timing.append((label, e0, e1, flops))
+            wc = 4 if cout > 64 else (2 if cout > 32 else 1)
+            kname = (f"k_conv<{'bf16' if self.dt == L.ZP_BF16 else 'f32'},WC={wc},WP=4,"
+                     f"smallC={int(x.C < _KE[self.dt])}>")
+            self.timing.append((label, e0, e1, flops, kname))
         else:
             L.check(L.lib.zp_conv2d(C.byref(a), st), "zp_conv2d")
         return stats, parts
@@ -241,6 +244,8 @@ class Engine:
                None if res is None else res.ptr, 0 if res is None else res.ld, 0 if res is None else res.c0,
                int(unit.relu), self.dt, out.ptr, out.ld, out.c0, L.stream_ptr())
         self._fold_epoch += 1
+        for buf in (bn.running_mean, bn.running_var, bn.num_batches_tracked):  # written in place by the kernel
+            torch.autograd.graph.increment_version(buf)
         tape.recs.append(("bn", unit, x, out, res, raw, save))
 
     def aspp_branches_fwd(self, units, x: Act, outs_act, tape):

@@ -1,0 +1,43 @@
+"""Adam on the device through ``zp_adam`` (torch.optim.Adam semantics: no weight decay, no
+amsgrad; the update order of torch's implementation -- lerp of the first moment, bias-corrected
+step size, sqrt(v)/sqrt(bc2) + eps).  Reference use: train_v6.py:268-269 (Adam(lr)), :338 (step).
+State dict layout matches torch.optim.Adam ('step', 'exp_avg', 'exp_avg_sq' per parameter) so
+checkpoints stay interchangeable (utils_v2.py:15-23)."""
+from __future__ import annotations
+
+import torch
+
+from . import _lib as L
+
+
+class FusedAdam(torch.optim.Optimizer):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
+        if weight_decay != 0.0:
+            raise NotImplementedError("weight decay is not used by the ZebraPose trainers")
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=0.0))
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        st = L.stream_ptr()
+        for group in self.param_groups:
+            b1, b2 = group["betas"]
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                if p.dtype != torch.float32 or not p.is_contiguous() or not p.grad.is_contiguous():
+                    raise ValueError("FusedAdam expects contiguous float32 parameters and gradients")
+                state = self.state[p]
+                if len(state) == 0:
+                    state["step"] = torch.tensor(0.0)
+                    state["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    state["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                state["step"] += 1
+                step = int(state["step"].item())
+                L.call("zp_adam", p.data_ptr(), p.grad.data_ptr(), state["exp_avg"].data_ptr(),
+                       state["exp_avg_sq"].data_ptr(), p.numel(), float(group["lr"]), float(b1), float(b2),
+                       float(group["eps"]), step, st)
+                # the kernel wrote p in place behind autograd's back: bump its version counter so
+                # version-keyed caches (packed eval weights in the engine) see the update
+                torch.autograd.graph.increment_version(p)
+        return loss

@@ -1,0 +1,49 @@
+"""The ZebraPose training step on MI355X (train_v6.py:319-338 semantics) and its data-parallel
+wrapper (train_v6.py:47-51, 82-91, 252-264).
+
+Per step: forward (train-mode BN) -> visible-mask threshold on device (train_v6.py:325-326 does
+it on the host in f64) -> loss_b = BinaryCodeLoss('BCE', True, 2, hist=True) (f64) and
+loss_m = MaskLoss -> loss = 3 loss_b + loss_m -> backward -> Adam.  Under torch.distributed
+(one process per GPU, backend 'nccl' = RCCL over xGMI) the network is wrapped in DDP exactly as
+the reference does, so the gradient all-reduce (mean) runs over RCCL; lr is multiplied and the
+iteration budget divided by the world size (train_v6.py:82-91); BN statistics stay per rank and
+rank 0's BN buffers are broadcast at every forward (DDP default broadcast_buffers=True).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from .model.BinaryCodeNet import BinaryCodeLoss, MaskLoss
+from .optim import FusedAdam
+
+
+def scale_for_world(learning_rate, total_iteration, world_size):
+    """train_v6.py:82-91."""
+    return learning_rate * world_size, total_iteration // world_size
+
+
+class TrainStep:
+    def __init__(self, net, learning_rate=2e-4, binary_loss_weight=3.0, ddp=None, device=None):
+        self.module = net
+        self.net = net
+        if ddp is None:
+            ddp = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+        if ddp:
+            dev = device if device is not None else torch.cuda.current_device()
+            self.net = torch.nn.parallel.DistributedDataParallel(net, device_ids=[dev])
+        self.binary_loss_weight = binary_loss_weight
+        self.code_loss = BinaryCodeLoss("BCE", True, 2, use_histgramm_weighted_binary_loss=True)
+        self.mask_loss = MaskLoss()
+        self.optimizer = FusedAdam(self.net.parameters(), lr=learning_rate)
+
+    def __call__(self, x, gt_code, gt_mask):
+        """x f32 [B,3,H,W]; gt_code u8/f64 [B,L,H/2,W/2]; gt_mask f32 [B,H/2,W/2] -> (loss, loss_b, loss_m)."""
+        self.optimizer.zero_grad(set_to_none=True)
+        mask, code = self.net(x)
+        loss_b = self.code_loss.forward_from_logits(code, mask, gt_code)
+        loss_m = self.mask_loss(mask, gt_mask)
+        loss = self.binary_loss_weight * loss_b + loss_m
+        loss.backward()
+        self.optimizer.step()
+        return loss.detach(), loss_b.detach(), loss_m.detach()
