@@ -1,0 +1,101 @@
+"""The oracle (oracle/ref_cpu.py) pinned against golden vectors captured from the real reference
+(oracle/capture_fixtures.py imports /root/reference/zebrapose and runs it on CPU)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref_cpu
+
+
+@pytest.fixture(scope="module")
+def state(golden):
+    bn = dict(golden("r34_bn_buffers.npz"))
+    return lambda: ref_cpu.synthetic_state(34, 16, 0, bn)
+
+
+def test_state_spec_matches_reference_keys(golden):
+    import os
+    from tests.conftest import GOLDEN
+    want = open(os.path.join(GOLDEN, "state_keys_r34.txt")).read().splitlines()
+    entries, aliases = ref_cpu.state_spec(34, 16)
+    got = [f"{k} {list(s)}" for k, s, _ in entries]
+    assert got == want
+    assert len(aliases) == 96
+
+
+def test_forward64_matches_reference(golden, state):
+    f = golden("r34_fwd64.npz")
+    with torch.no_grad():
+        m, c = ref_cpu.forward(state(), torch.from_numpy(f["fwd64_x"]), 34)
+    np.testing.assert_allclose(m.numpy(), f["fwd64_mask"], atol=1e-5, rtol=0)
+    np.testing.assert_allclose(c.numpy(), f["fwd64_code"], atol=1e-5, rtol=0)
+
+
+def test_forward256_matches_reference(golden, state):
+    f = golden("r34_fwd256_b1.npz")
+    with torch.no_grad():
+        m, c = ref_cpu.forward(state(), torch.from_numpy(f["x"]), 34)
+    scale = max(1.0, float(np.abs(f["code"]).max()))
+    np.testing.assert_allclose(m.numpy(), f["mask"], atol=1e-4 * scale, rtol=0)
+    np.testing.assert_allclose(c.numpy(), f["code"], atol=1e-4 * scale, rtol=0)
+
+
+def test_train_step_matches_reference(golden, state):
+    f = golden("r34_train_step.npz")
+    sd = state()
+    entries, aliases = ref_cpu.state_spec(34, 16)
+    leaves = {}
+    for k, s, kind in entries:
+        if k in aliases or kind in ("bn_rm", "bn_rv", "bn_nbt"):
+            continue
+        sd[k].requires_grad_(True)
+        leaves[k] = sd[k]
+    for ak, ck in aliases.items():
+        sd[ak] = sd[ck]
+    x = torch.from_numpy(f["x"])
+    m, c = ref_cpu.forward(sd, x, 34, train=True)
+    np.testing.assert_allclose(m.detach().numpy(), f["mask_logits"], atol=1e-5)
+    np.testing.assert_allclose(c.detach().numpy(), f["code_logits"], atol=1e-5)
+    st = ref_cpu.HistLossState()
+    loss, lb, lm = ref_cpu.train_step_loss(st, m, c, torch.from_numpy(f["gt_code"]), torch.from_numpy(f["gt_mask"]))
+    assert lb.dtype == torch.float64
+    np.testing.assert_allclose(lb.item(), float(f["loss_b"]), rtol=1e-9)
+    np.testing.assert_allclose(lm.item(), float(f["loss_m"]), rtol=1e-6)
+    np.testing.assert_allclose(st.histogram.numpy(), f["hist1"], rtol=0, atol=1e-12)
+    loss.backward()
+    for k in f.files:
+        if k.startswith("grad:"):
+            name = k[5:]
+            g = leaves[name].grad.numpy()[:8]
+            np.testing.assert_allclose(g, f[k], atol=1e-5 * max(1e-3, np.abs(f[k]).max()) + 1e-9, rtol=1e-3)
+    for k in f.files:
+        if k.startswith("after:"):
+            np.testing.assert_allclose(sd[k[6:]].detach().numpy(), f[k], rtol=1e-5, atol=1e-7)
+    # second BinaryCodeLoss call: histogram EMA (BinaryCodeNet.py:37-41)
+    mask01 = torch.from_numpy(ref_cpu.threshold_np(m.detach().numpy()))
+    lb2 = ref_cpu.binary_code_loss(st, c.detach(), mask01, torch.from_numpy(f["gt_code2"]))
+    np.testing.assert_allclose(st.histogram.numpy(), f["hist2"], atol=1e-12)
+    np.testing.assert_allclose(lb2.item(), float(f["loss_b2"]), rtol=1e-9)
+
+
+def test_threshold_boundary_matches_reference(golden):
+    d = golden("decode.npz")
+    assert np.array_equal(ref_cpu.threshold_np(d["mask_logits"]).astype(np.uint8), d["mask_bits"])
+    assert np.array_equal(ref_cpu.threshold_np(d["code_logits"]).astype(np.uint8), d["code_bits"])
+    probe = np.array([8.940696716308594e-08, 8.94069742685133e-08, 0.0, -1e-8, np.nan], np.float32)
+    assert ref_cpu.threshold_np(probe).tolist() == [0.0, 1.0, 0.0, 0.0, 0.0]
+
+
+@pytest.mark.parametrize("ignore_bit", [0, 2])
+def test_decode_matches_reference(golden, ignore_bit):
+    d = golden("decode.npz")
+    lut = d["lut"] if ignore_bit == 0 else ref_cpu.coarse_lut(d["lut"], 16, 16 - ignore_bit)
+    if ignore_bit:
+        np.testing.assert_array_equal(lut, d[f"lut_ib{ignore_bit}"])
+    for b in range(d["mask_logits"].shape[0]):
+        n, p2d, p3d, ids = ref_cpu.decode_crop(d["mask_logits"][b, 0], d["code_logits"][b], lut, d["bboxes"][b],
+                                               ignore_bit=ignore_bit)
+        assert n == int(d[f"ib{ignore_bit}_b{b}_count"])
+        assert np.array_equal(ids, d[f"ib{ignore_bit}_b{b}_ids"])
+        assert np.array_equal(p2d, d[f"ib{ignore_bit}_b{b}_p2d"])
+        assert np.array_equal(p3d, d[f"ib{ignore_bit}_b{b}_p3d"])

@@ -489,16 +489,21 @@ __global__ void k_threshold(const float* __restrict__ x, long n, int f64, void* 
 }
 
 __global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
-                       long n, float lr_bc1, float b1, float b2, float bc2_sqrt, float eps) {
+                       long n, float lr_bc1, float w1, float b2, float w2, float bc2_sqrt, float eps) {
+  // torch.optim.Adam (_single_tensor_adam) op by op, each op rounded separately (no FMA contraction):
+  //   exp_avg.lerp_(grad, w1 = 1 - beta1)      (w1 < 0.5: m + w1 * (g - m))
+  //   exp_avg_sq.mul_(beta2).addcmul_(grad, grad, value=w2 = 1 - beta2)
+  //   denom = exp_avg_sq.sqrt() / sqrt(bc2) + eps;  param.addcdiv_(exp_avg, denom, value=-lr/bc1)
   for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
-    float gg = g[e];
+    const float gg = g[e];
     float mm = m[e];
-    mm = mm + (1.f - b1) * (gg - mm);  // exp_avg.lerp_(grad, 1 - beta1)
-    float vv = v[e] * b2 + (1.f - b2) * gg * gg;
+    mm = fmaf(w1, __fsub_rn(gg, mm), mm);  // ATen lerp: fmadd(weight, end - self, self)
+    float vv = __fmul_rn(v[e], b2);
+    vv = __fadd_rn(vv, __fmul_rn(__fmul_rn(w2, gg), gg));
     m[e] = mm;
     v[e] = vv;
-    float denom = sqrtf(vv) / bc2_sqrt + eps;
-    p[e] = p[e] - lr_bc1 * (mm / denom);
+    const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(vv), bc2_sqrt), eps);
+    p[e] = __fadd_rn(p[e], __fmul_rn(-lr_bc1, __fdiv_rn(mm, denom)));
   }
 }
 
@@ -769,7 +774,8 @@ extern "C" int zp_adam(float* param, const float* grad, float* exp_avg, float* e
   double bc1 = 1.0 - pow(beta1, (double)step);
   double bc2 = 1.0 - pow(beta2, (double)step);
   hipLaunchKernelGGL(k_adam, dim3(grid_for(n, 256, 16384)), dim3(256), 0, (hipStream_t)stream, param, grad, exp_avg,
-                     exp_avg_sq, (long)n, (float)(lr / bc1), (float)beta1, (float)beta2, (float)sqrt(bc2), (float)eps);
+                     exp_avg_sq, (long)n, (float)(lr / bc1), (float)(1.0 - beta1), (float)beta2,
+                     (float)(1.0 - beta2), (float)sqrt(bc2), (float)eps);
   ZP_LAUNCH_CHECK("zp_adam");
   return ZP_OK;
 }
