@@ -217,3 +217,25 @@ def test_fused_adam_matches_torch():
     st = o.state_dict()["state"][0]
     np.testing.assert_allclose(st["exp_avg"].cpu().numpy(), o_ref.state_dict()["state"][0]["exp_avg"].numpy(),
                                rtol=1e-5, atol=1e-7)
+
+
+def test_binary_code_helper_dropins(golden):
+    """Reference-signature helpers (host arrays in/out, device decode inside)."""
+    from zebrapose_amd.binary_code_helper.CNN_output_to_pose import decode_correspondences
+    from zebrapose_amd.binary_code_helper.generate_new_dict import generate_new_corres_dict
+    d = golden("decode.npz")
+    lut_dict = {float(i): d["lut"][i] for i in range(65536)}
+    for ib in (0, 2):
+        dd = lut_dict if ib == 0 else generate_new_corres_dict(lut_dict, 16, 16 - ib)
+        if ib:
+            got = np.stack([dd[i].reshape(3) for i in range(2 ** 14)])
+            np.testing.assert_array_equal(got.astype(np.float32), d["lut_ib2"].astype(np.float32))
+            dd = {float(k): v for k, v in dd.items()}
+        for b in range(2):
+            mask = d["mask_bits"][b, 0]
+            code = d["code_bits"][b].transpose(1, 2, 0)
+            if ib:
+                code = code[:, :, :-ib]
+            p2d, p3d = decode_correspondences(mask, code, d["bboxes"][b], 128, dd)
+            np.testing.assert_array_equal(p2d, d[f"ib{ib}_b{b}_p2d"])
+            np.testing.assert_array_equal(p3d, d[f"ib{ib}_b{b}_p3d"])

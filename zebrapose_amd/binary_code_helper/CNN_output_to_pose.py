@@ -1,0 +1,103 @@
+"""Drop-in for reference ``zebrapose/binary_code_helper/CNN_output_to_pose.py``.
+
+The correspondence building (id fold, LUT gather, row-major compaction, coordinate map) runs in
+the ``zp_decode`` HIP kernel: these functions take the reference's host arrays, run the device
+decode and return the reference's host arrays.  For batched inference use
+``zebrapose_amd.decode.Decoder`` directly on the network's device outputs.
+
+PnP (:132-158) stays with OpenCV / pyprogressivex as in the reference (out of scope: SURVEY §8f).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ..decode import Decoder, read_lut_file
+
+try:  # PnP backends, exactly as the reference probes them (:3-8)
+    import pyprogressivex  # noqa: F401
+    USE_PYPROGRESSIVEX = True
+except Exception:
+    USE_PYPROGRESSIVEX = False
+
+
+def load_dict_class_id_3D_points(path):
+    """:10-32 -> (total_class, divide_number, iterations, {float(id): f64[3]})."""
+    total, divide, iters, lut = read_lut_file(path)
+    d = {float(i): lut[i].copy() for i in range(lut.shape[0])}
+    return total, divide, iters, d
+
+
+def _lut_from_dict(dict_class_id_3D_points):
+    n = len(dict_class_id_3D_points)
+    bits = int(round(np.log2(n)))
+    if 2 ** bits != n:
+        raise ValueError("the class-id dictionary must hold 2^L entries")
+    return np.stack([np.asarray(dict_class_id_3D_points[float(i)], dtype=np.float64).reshape(3) for i in range(n)])
+
+
+_DEC_CACHE = {}
+
+
+def _decoder_for(dict_class_id_3D_points, device):
+    key = (id(dict_class_id_3D_points), str(device))
+    dec = _DEC_CACHE.get(key)
+    if dec is None:
+        dec = _DEC_CACHE[key] = Decoder(_lut_from_dict(dict_class_id_3D_points), device=device)
+    return dec
+
+
+def _bits_to_logits(bits):
+    """0/1 arrays -> logits the device threshold maps back to the same bits (exact)."""
+    return np.where(np.asarray(bits) > 0.5, np.float32(1.0), np.float32(-1.0)).astype(np.float32)
+
+
+def decode_correspondences(mask_image, class_code_image, Bbox, Bbox_Size, dict_class_id_3D_points, device="cuda"):
+    """Device version of :110-129 for one crop: (Original_Points_2D int64 [N,2], Points_3D f32 [N,3])."""
+    L = class_code_image.shape[2]
+    dec = _decoder_for(dict_class_id_3D_points, device)
+    if dec.bits != L:
+        raise ValueError(f"code image has {L} bits but the dictionary has {dec.bits}")
+    m = torch.from_numpy(_bits_to_logits(mask_image)[None, None]).to(device)
+    c = torch.from_numpy(np.ascontiguousarray(_bits_to_logits(class_code_image).transpose(2, 0, 1))[None]).to(device)
+    counts, xy, xyz = dec(m, c, np.asarray(Bbox).reshape(1, 4), bbox_size=Bbox_Size)
+    return Decoder.to_host(counts, xy, xyz)[0]
+
+
+def CNN_outputs_to_object_pose(mask_image, class_code_image, Bbox, Bbox_Size, class_base=2,
+                               dict_class_id_3D_points=None, intrinsic_matrix=None):
+    """:100-160 -- correspondences on the device, then RANSAC-EPnP (cv2) / Progressive-X as in the
+    reference.  Returns (R, t, success)."""
+    if class_base != 2:
+        raise NotImplementedError("only binary codes (class_base 2) are on the hot path")
+    if intrinsic_matrix is None:
+        intrinsic_matrix = np.zeros((3, 3))
+        intrinsic_matrix[0, 0] = 572.4114
+        intrinsic_matrix[1, 1] = 573.57043
+        intrinsic_matrix[0, 2] = 325.2611
+        intrinsic_matrix[1, 2] = 242.04899
+        intrinsic_matrix[2, 2] = 1.0
+    success, rot, tvecs = False, [], []
+    p2d, p3d = decode_correspondences(mask_image, class_code_image, Bbox, Bbox_Size, dict_class_id_3D_points)
+    if len(p2d) >= 6:
+        success = True
+        coord_2d = np.ascontiguousarray(p2d.astype(np.float32))
+        coord_3d = np.ascontiguousarray(p3d.astype(np.float32))
+        if USE_PYPROGRESSIVEX:
+            import pyprogressivex
+            pose_ests, _ = pyprogressivex.find6DPoses(
+                x1y1=coord_2d.astype(np.float64), x2y2z2=coord_3d.astype(np.float64),
+                K=np.ascontiguousarray(intrinsic_matrix).astype(np.float64), threshold=2,
+                neighborhood_ball_radius=20, spatial_coherence_weight=0.1, maximum_tanimoto_similarity=0.9,
+                max_iters=400, minimum_point_number=6, maximum_model_number=1)
+            if pose_ests.shape[0] != 0:
+                rot, tvecs = pose_ests[0:3, :3], pose_ests[0:3, 3].reshape((3, 1))
+            else:
+                rot, tvecs, success = np.zeros((3, 3)), np.zeros((3, 1)), False
+        else:
+            import cv2  # OpenCV is the reference's default PnP (not part of this package)
+            _, rvecs, tvecs, _ = cv2.solvePnPRansac(coord_3d, coord_2d, intrinsic_matrix, distCoeffs=None,
+                                                    reprojectionError=2, iterationsCount=150,
+                                                    flags=cv2.SOLVEPNP_EPNP)
+            rot, _ = cv2.Rodrigues(rvecs, jacobian=None)
+    return rot, tvecs, success
