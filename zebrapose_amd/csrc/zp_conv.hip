@@ -38,49 +38,61 @@ template <> struct MfmaTraits<float> {
 
 __device__ __forceinline__ int swz(int row, int chunk) { return row * 8 + (chunk ^ (row & 7)); }
 
-template <typename T, int WC, int WP, bool SMALLC>
-__global__ void __launch_bounds__(256) k_conv(const zp_conv_args A) {
+// all-zero source for out-of-image / padding taps of the direct-to-LDS loads
+__device__ uint4 g_zero_page[8];
+
+// Staging: every K step moves TC weight rows + TP activation rows of 128 B each straight
+// from global memory into LDS with global_load_lds_dwordx4 (one wave-instruction = 8 rows x
+// 128 B, lane-linear in LDS).  The 16 B chunk swizzle (chunk ^ (row & 7), conflict-free
+// ds_read_b128 of the MFMA fragments) is applied on the per-lane SOURCE address.  Out-of-
+// image taps read g_zero_page.  Two LDS buffers: the loads of step k+1 are in flight while
+// step k's MFMAs run; one __syncthreads (vmcnt(0) + s_barrier) per step.
+template <typename T, int WC, int WP, int NWP, bool SMALLC>
+__global__ void __launch_bounds__(128 * NWP) k_conv(const zp_conv_args A) {
   constexpr int E = MfmaTraits<T>::E;
   constexpr int KE = 8 * E;  // elements per K step (128 B)
-  constexpr int TC = 32 * WC, TP = 32 * WP;
-  constexpr int LC = TC / 32, LP = TP / 32;
+  constexpr int TC = 32 * WC, TP = 16 * WP * NWP;
+  constexpr int NW = 2 * NWP;                 // waves
+  constexpr int G = (TC + TP) / 8;            // 8-row groups per K step
+  static_assert(G % NW == 0, "row groups must split evenly over the waves");
+  constexpr int GPW = G / NW;                 // groups per wave
   __shared__ uint4 lds[2][(TC + TP) * 8];
 
   const zp_conv_sub& S = A.sub[blockIdx.z];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wc = wid >> 1, wp = wid & 1;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar branches)
+  const int wc = wid / NWP, wp = wid % NWP;
   const int GHW = A.GH * A.GW;
   const int M = A.N * GHW;
   const int p0 = blockIdx.x * TP, c0 = blockIdx.y * TC;
-  const int qr = tid >> 3, qc = tid & 7;
+  const int lrow = lane >> 3;                  // row within the 8-row group
+  const int csrc = (lane & 7) ^ lrow;          // source chunk (swizzle on the source side)
 
-  int rn[LP], ry[LP], rx[LP];
-  bool rv[LP];
+  // per group: weight row or activation row (pixel) of this lane
+  int gpix_n[GPW], gpix_y[GPW], gpix_x[GPW];
+  bool gvalid[GPW];
 #pragma unroll
-  for (int i = 0; i < LP; ++i) {
-    int m = p0 + qr + 32 * i;
-    rv[i] = m < M;
-    int mm = rv[i] ? m : 0;
-    int n = mm / GHW, r = mm - n * GHW;
-    int gy = r / A.GW, gx = r - gy * A.GW;
-    rn[i] = n;
-    ry[i] = gy * A.sy;
-    rx[i] = gx * A.sx;
+  for (int i = 0; i < GPW; ++i) {
+    const int r = (wid + NW * i) * 8 + lrow;
+    int m = p0 + (r - TC);
+    gvalid[i] = r >= TC && m < M;
+    int mm = gvalid[i] ? m : 0;
+    int n = mm / GHW, rr = mm - n * GHW;
+    int gy = rr / A.GW, gx = rr - gy * A.GW;
+    gpix_n[i] = n;
+    gpix_y[i] = gy * A.sy;
+    gpix_x[i] = gx * A.sx;
   }
   const T* __restrict__ X = (const T*)A.x;
   const T* __restrict__ Wt = (const T*)S.w;
   const int CB = SMALLC ? 1 : A.Cin / KE;
   const int nK = SMALLC ? A.k_pad / KE : S.ntaps * CB;
 
-  uint4 ra[LC], rb[LP];
-  auto gload = [&](int ks) {
-#pragma unroll
-    for (int i = 0; i < LC; ++i)
-      ra[i] = *(const uint4*)(Wt + (size_t)(c0 + qr + 32 * i) * A.k_pad + (size_t)ks * KE + qc * E);
+  auto issue = [&](int ks, int buf) {
     int ty, tx, cc;
     bool tok;
     if (SMALLC) {
-      int k = ks * KE + qc * E;
+      int k = ks * KE + csrc * E;
       int t = k / A.Cin;
       cc = k - t * A.Cin;
       tok = t < S.ntaps;
@@ -89,25 +101,39 @@ __global__ void __launch_bounds__(256) k_conv(const zp_conv_args A) {
       tx = (t - kyy * S.kw) * S.dil - S.pad;
     } else {
       int t = ks / CB;
-      cc = (ks - t * CB) * KE + qc * E;
+      cc = (ks - t * CB) * KE + csrc * E;
       ty = S.ty[t];
       tx = S.tx[t];
       tok = true;
     }
+    // all source addresses first (distinct registers), then the DMA issues back to back: hipcc
+    // waits vmcnt(0) before it rewrites the address VGPRs of an in-flight global_load_lds
+    const void* srcs[GPW];
 #pragma unroll
-    for (int i = 0; i < LP; ++i) {
-      int iy = ry[i] + ty, ix = rx[i] + tx;
-      bool ok = tok && rv[i] && (unsigned)iy < (unsigned)A.IH && (unsigned)ix < (unsigned)A.IW;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (ok) v = *(const uint4*)(X + (((size_t)rn[i] * A.IH + iy) * A.IW + ix) * A.ldx + A.cx0 + cc);
-      rb[i] = v;
+    for (int i = 0; i < GPW; ++i) {
+      const int g = wid + NW * i;
+      const int r = g * 8 + lrow;
+      const void* src;
+      if (g * 8 < TC) {  // wave-uniform: groups never straddle the weight / activation boundary
+        src = Wt + (size_t)(c0 + r) * A.k_pad + (size_t)ks * KE + csrc * E;
+      } else {
+        int iy = gpix_y[i] + ty, ix = gpix_x[i] + tx;
+        bool ok = tok && gvalid[i] && (unsigned)iy < (unsigned)A.IH && (unsigned)ix < (unsigned)A.IW;
+        // branch-free: address of a clamped (always valid) pixel, then a pointer select
+        int iyc = min(max(iy, 0), A.IH - 1), ixc = min(max(ix, 0), A.IW - 1);
+        const T* pv = X + (((size_t)gpix_n[i] * A.IH + iyc) * A.IW + ixc) * A.ldx + A.cx0 + cc;
+        src = ok ? (const void*)pv : (const void*)&g_zero_page[lane & 7];
+      }
+      srcs[i] = src;
     }
-  };
-  auto sstore = [&](int buf) {
+#if defined(__HIP_DEVICE_COMPILE__)  // device-only builtin: the host pass would silently drop the kernel stubs
 #pragma unroll
-    for (int i = 0; i < LC; ++i) lds[buf][swz(qr + 32 * i, qc)] = ra[i];
-#pragma unroll
-    for (int i = 0; i < LP; ++i) lds[buf][swz(TC + qr + 32 * i, qc)] = rb[i];
+    for (int i = 0; i < GPW; ++i) {
+      const int g = wid + NW * i;
+      __builtin_amdgcn_global_load_lds(srcs[i], (__attribute__((address_space(3))) void*)&lds[buf][g * 64], 16, 0,
+                                       0);
+    }
+#endif
   };
 
   f32x4 acc[WC][WP];
@@ -116,26 +142,31 @@ __global__ void __launch_bounds__(256) k_conv(const zp_conv_args A) {
 #pragma unroll
     for (int j = 0; j < WP; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  gload(0);
-  sstore(0);
+  issue(0, 0);
   __syncthreads();
   for (int ks = 0; ks < nK; ++ks) {
     const int buf = ks & 1;
-    if (ks + 1 < nK) gload(ks + 1);
+    // all fragment reads of this step first, THEN the next step's LDS-DMA: a ds_read placed
+    // after an in-flight global_load_lds makes hipcc drain vmcnt(0) in front of it.
+    uint4 af[2][WC], bfr[2][WP];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int ch = s * 4 + (lane >> 4);
-      uint4 af[WC], bfr[WP];
 #pragma unroll
-      for (int i = 0; i < WC; ++i) af[i] = lds[buf][swz(wc * 16 * WC + i * 16 + (lane & 15), ch)];
+      for (int i = 0; i < WC; ++i) af[s][i] = lds[buf][swz(wc * 16 * WC + i * 16 + (lane & 15), ch)];
 #pragma unroll
-      for (int j = 0; j < WP; ++j) bfr[j] = lds[buf][swz(TC + wp * 16 * WP + j * 16 + (lane & 15), ch)];
+      for (int j = 0; j < WP; ++j) bfr[s][j] = lds[buf][swz(TC + wp * 16 * WP + j * 16 + (lane & 15), ch)];
+    }
+    if (ks + 1 < nK) issue(ks + 1, buf ^ 1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int i = 0; i < WC; ++i)
 #pragma unroll
-        for (int j = 0; j < WP; ++j) MfmaTraits<T>::mma(acc[i][j], af[i], bfr[j]);
-    }
-    if (ks + 1 < nK) sstore(buf ^ 1);
+        for (int j = 0; j < WP; ++j) MfmaTraits<T>::mma(acc[i][j], af[s][i], bfr[s][j]);
+    // keep the MFMAs in front of the barrier: hipcc otherwise hoists the barrier's vmcnt(0)
+    // into the MFMA run and the next step's loads stop overlapping the math
+    __builtin_amdgcn_sched_barrier(0);
     __syncthreads();
   }
 
@@ -215,8 +246,8 @@ __global__ void __launch_bounds__(256) k_conv(const zp_conv_args A) {
     // Train-mode BatchNorm statistics of the raw (stored) conv output, per wave half:
     // (count, mean, M2) with M2 centred on the local mean (two passes over the registers, no
     // E[x^2] - E[x]^2 cancellation); zp_bn_train_finalize merges the parts (Chan et al.).
-    const int parts = gridDim.x * gridDim.z * 2;
-    const int part = (blockIdx.z * gridDim.x + blockIdx.x) * 2 + wp;
+    const int parts = gridDim.x * gridDim.z * NWP;
+    const int part = (blockIdx.z * gridDim.x + blockIdx.x) * NWP + wp;
     float cnt = 0.f;
 #pragma unroll
     for (int j = 0; j < WP; ++j) cnt += (p0 + wp * 16 * WP + j * 16 + (lane & 15) < M) ? 1.f : 0.f;
@@ -448,17 +479,26 @@ __global__ void k_wgrad_reduce(const zp_wgrad_args A, const float* __restrict__ 
 using namespace zp;
 
 // ------------------------------------------------------------------------------------ host
-template <typename T, int WC, bool SMALLC>
+template <typename T, int WC, int NWP, bool SMALLC>
 static void launch_conv(const zp_conv_args& a, int gx, int gy, hipStream_t st) {
-  hipLaunchKernelGGL((k_conv<T, WC, 4, SMALLC>), dim3(gx, gy, a.nsub), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((k_conv<T, WC, 4, NWP, SMALLC>), dim3(gx, gy, a.nsub), dim3(128 * NWP), 0, st, a);
 }
 
 static int conv_tc(int cout) { return cout > 64 ? 128 : (cout > 32 ? 64 : 32); }
 
+// pixel tile: 256 (8 waves) when that still gives >= 1024 workgroups, else 128 (4 waves)
+static int conv_tp(const zp_conv_args& a) {
+  long M = (long)a.N * a.GH * a.GW;
+  int tc = a.Cout > 64 ? 128 : (a.Cout > 32 ? 64 : 32);
+  if (tc == 32) return 128;
+  long blocks256 = (long)ceil_div(M, 256) * ceil_div(a.Cout, tc) * a.nsub;
+  return blocks256 >= 1024 ? 256 : 128;
+}
+
 extern "C" int zp_conv2d_grid(const zp_conv_args* a) {
   if (!a) return 0;
   long M = (long)a->N * a->GH * a->GW;
-  return ceil_div(M, 128);
+  return ceil_div(M, conv_tp(*a));
 }
 
 extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
@@ -498,22 +538,24 @@ extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
   const int tc = conv_tc(a.Cout);
   const int gx = zp_conv2d_grid(&a), gy = ceil_div(a.Cout, tc);
   hipStream_t st = (hipStream_t)stream;
+  const int nwp = conv_tp(a) / 64;
+#define ZP_DISPATCH_NWP(T, WC, NWP)                                      \
+  if (smallc) launch_conv<T, WC, NWP, true>(a, gx, gy, st);              \
+  else launch_conv<T, WC, NWP, false>(a, gx, gy, st);
 #define ZP_DISPATCH(T)                                                   \
   if (tc == 128) {                                                       \
-    if (smallc) launch_conv<T, 4, true>(a, gx, gy, st);                  \
-    else launch_conv<T, 4, false>(a, gx, gy, st);                        \
+    if (nwp == 4) { ZP_DISPATCH_NWP(T, 4, 4) } else { ZP_DISPATCH_NWP(T, 4, 2) } \
   } else if (tc == 64) {                                                 \
-    if (smallc) launch_conv<T, 2, true>(a, gx, gy, st);                  \
-    else launch_conv<T, 2, false>(a, gx, gy, st);                        \
+    if (nwp == 4) { ZP_DISPATCH_NWP(T, 2, 4) } else { ZP_DISPATCH_NWP(T, 2, 2) } \
   } else {                                                               \
-    if (smallc) launch_conv<T, 1, true>(a, gx, gy, st);                  \
-    else launch_conv<T, 1, false>(a, gx, gy, st);                        \
+    ZP_DISPATCH_NWP(T, 1, 2)                                             \
   }
   if (a.dtype == ZP_BF16) {
     ZP_DISPATCH(bf16_t)
   } else {
     ZP_DISPATCH(float)
   }
+#undef ZP_DISPATCH_NWP
 #undef ZP_DISPATCH
   ZP_LAUNCH_CHECK("zp_conv2d");
   return ZP_OK;
@@ -581,5 +623,5 @@ extern "C" int zp_conv2d_wgrad(const zp_wgrad_args* ap, void* ws, void* stream) 
 
 extern "C" int zp_conv2d_stat_parts(const zp_conv_args* a) {
   if (!a) return 0;
-  return 2 * zp_conv2d_grid(a) * a->nsub;
+  return (conv_tp(*a) / 64) * zp_conv2d_grid(a) * a->nsub;
 }
