@@ -12,6 +12,7 @@
 // NHWC stores.  K steps are 128 bytes per row (64 bf16 / 32 f32) of one tap;
 // the tile is staged global -> registers -> LDS (XOR-swizzled 16 B chunks,
 // double-buffered, one barrier per K step).
+#include <type_traits>
 #include "zp_common.h"
 
 namespace zp {
@@ -41,6 +42,13 @@ __device__ __forceinline__ int swz(int row, int chunk) { return row * 8 + (chunk
 // all-zero source for out-of-image / padding taps of the direct-to-LDS loads
 __device__ uint4 g_zero_page[8];
 
+// s_waitcnt vmcnt(N) only (LDS-DMA loads count on vmcnt); "memory" keeps LDS accesses in place
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 // Staging: every K step moves TC weight rows + TP activation rows of 128 B each straight
 // from global memory into LDS with global_load_lds_dwordx4 (one wave-instruction = 8 rows x
 // 128 B, lane-linear in LDS).  The 16 B chunk swizzle (chunk ^ (row & 7), conflict-free
@@ -56,7 +64,15 @@ __global__ void __launch_bounds__(128 * NWP) k_conv(const zp_conv_args A) {
   constexpr int G = (TC + TP) / 8;            // 8-row groups per K step
   static_assert(G % NW == 0, "row groups must split evenly over the waves");
   constexpr int GPW = G / NW;                 // groups per wave
-  __shared__ uint4 lds[2][(TC + TP) * 8];
+  __shared__ uint4 lds0[(TC + TP) * 8];
+  __shared__ uint4 lds1[(TC + TP) * 8];
+  __shared__ uint4 lds2[(TC + TP) * 8];
+  auto bufp = [&](auto i_c) -> uint4* {
+    constexpr int i = decltype(i_c)::value;
+    if constexpr (i == 0) return lds0;
+    else if constexpr (i == 1) return lds1;
+    else return lds2;
+  };
 
   const zp_conv_sub& S = A.sub[blockIdx.z];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -88,7 +104,7 @@ __global__ void __launch_bounds__(128 * NWP) k_conv(const zp_conv_args A) {
   const int CB = SMALLC ? 1 : A.Cin / KE;
   const int nK = SMALLC ? A.k_pad / KE : S.ntaps * CB;
 
-  auto issue = [&](int ks, int buf) {
+  auto issue = [&](int ks, uint4* dst) {
     int ty, tx, cc;
     bool tok;
     if (SMALLC) {
@@ -102,8 +118,12 @@ __global__ void __launch_bounds__(128 * NWP) k_conv(const zp_conv_args A) {
     } else {
       int t = ks / CB;
       cc = (ks - t * CB) * KE + csrc * E;
-      ty = S.ty[t];
-      tx = S.tx[t];
+      // tap offsets through scalar dword loads (s_load, counted by lgkmcnt): a byte load would be
+      // a vector load, and waiting for it would also drain the in-flight LDS-DMA ring (vmcnt)
+      const int wy = ((const int*)S.ty)[t >> 2], wx = ((const int*)S.tx)[t >> 2];
+      const int sh = 24 - 8 * (t & 3);
+      ty = (wy << sh) >> 24;
+      tx = (wx << sh) >> 24;
       tok = true;
     }
     // all source addresses first (distinct registers), then the DMA issues back to back: hipcc
@@ -130,8 +150,7 @@ __global__ void __launch_bounds__(128 * NWP) k_conv(const zp_conv_args A) {
 #pragma unroll
     for (int i = 0; i < GPW; ++i) {
       const int g = wid + NW * i;
-      __builtin_amdgcn_global_load_lds(srcs[i], (__attribute__((address_space(3))) void*)&lds[buf][g * 64], 16, 0,
-                                       0);
+      __builtin_amdgcn_global_load_lds(srcs[i], (__attribute__((address_space(3))) void*)&dst[g * 64], 16, 0, 0);
     }
 #endif
   };
@@ -142,32 +161,55 @@ __global__ void __launch_bounds__(128 * NWP) k_conv(const zp_conv_args A) {
 #pragma unroll
     for (int j = 0; j < WP; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  issue(0, 0);
-  __syncthreads();
-  for (int ks = 0; ks < nK; ++ks) {
-    const int buf = ks & 1;
-    // all fragment reads of this step first, THEN the next step's LDS-DMA: a ds_read placed
-    // after an in-flight global_load_lds makes hipcc drain vmcnt(0) in front of it.
+  // Three-stage ring: while step k computes from buffer k%3, the DMA of steps k+1 (issued one
+  // step earlier) and k+2 (issued now) are in flight.  End of step k: counted vmcnt(GPW) (only
+  // step k+2's loads may remain outstanding) + raw s_barrier -- never __syncthreads(), whose
+  // vmcnt(0) would drain the ring.  Buffer indices are compile-time (loop unrolled by 3) and the
+  // three buffers are distinct LDS objects, so hipcc can prove a ds_read never aliases an
+  // in-flight global_load_lds and inserts no vmcnt wait in front of it.
+  auto step = [&](auto cur_c, auto nxt_c, int ks) {
+    const uint4* cur = bufp(cur_c);
     uint4 af[2][WC], bfr[2][WP];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int ch = s * 4 + (lane >> 4);
 #pragma unroll
-      for (int i = 0; i < WC; ++i) af[s][i] = lds[buf][swz(wc * 16 * WC + i * 16 + (lane & 15), ch)];
+      for (int i = 0; i < WC; ++i) af[s][i] = cur[swz(wc * 16 * WC + i * 16 + (lane & 15), ch)];
 #pragma unroll
-      for (int j = 0; j < WP; ++j) bfr[s][j] = lds[buf][swz(TC + wp * 16 * WP + j * 16 + (lane & 15), ch)];
+      for (int j = 0; j < WP; ++j) bfr[s][j] = cur[swz(TC + wp * 16 * WP + j * 16 + (lane & 15), ch)];
     }
-    if (ks + 1 < nK) issue(ks + 1, buf ^ 1);
+    const bool more = ks + 2 < nK;
+    if (more) issue(ks + 2, bufp(nxt_c));
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int i = 0; i < WC; ++i)
 #pragma unroll
         for (int j = 0; j < WP; ++j) MfmaTraits<T>::mma(acc[i][j], af[s][i], bfr[s][j]);
-    // keep the MFMAs in front of the barrier: hipcc otherwise hoists the barrier's vmcnt(0)
-    // into the MFMA run and the next step's loads stop overlapping the math
+    __builtin_amdgcn_sched_barrier(0);  // keep the MFMAs in front of the wait + barrier
+    if (more) vm_wait<GPW>();
+    else vm_wait<0>();
+    __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    __syncthreads();
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  issue(0, lds0);
+  if (nK > 1) {
+    issue(1, lds1);
+    vm_wait<GPW>();
+  } else {
+    vm_wait<0>();
+  }
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  for (int ks = 0; ks < nK; ks += 3) {
+    step(I0{}, I2{}, ks);
+    if (ks + 1 >= nK) break;
+    step(I1{}, I0{}, ks + 1);
+    if (ks + 2 >= nK) break;
+    step(I2{}, I1{}, ks + 2);
   }
 
   // ---------------- epilogue ----------------

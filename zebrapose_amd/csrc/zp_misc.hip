@@ -412,26 +412,39 @@ __global__ void k_maxpool_bwd(const T* __restrict__ x, int ldx, int cx0, const T
   }
 }
 
-template <typename T>
-__global__ void k_avgpool(const T* __restrict__ x, int H, int W, int ldx, int cx0, int C, T* __restrict__ y) {
-  const int b = blockIdx.y;
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  const long HW = (long)H * W;
-  double s = 0;  // CPU adaptive_avg_pool2d accumulates in acc_type<float> = double
-  for (long p = 0; p < HW; ++p) s += (double)Elem<T>::ld(x + ((size_t)b * HW + p) * ldx + cx0 + c);
-  y[(size_t)b * C + c] = Elem<T>::cvt((float)(s / (double)HW));
+// Per-channel sums over H*W: block = (image b, 64 channels), 256 threads = 64 channels x 4 pixel
+// slices (coalesced 64-channel rows), slices combined through LDS in a fixed order.
+template <typename T, typename ACC>
+__device__ __forceinline__ ACC sum_hw_block(const T* __restrict__ x, long HW, int ld, int c0, int C, int b) {
+  __shared__ ACC red[4][64];
+  const int cl = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  ACC s = 0;
+  if (c < C)
+    for (long p = sl; p < HW; p += 4) s += (ACC)Elem<T>::ld(x + ((size_t)b * HW + p) * ld + c0 + c);
+  red[sl][cl] = s;
+  __syncthreads();
+  return red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
 }
 
 template <typename T>
-__global__ void k_sum_hw(const T* __restrict__ dy, int H, int W, int lddy, int cdy0, int C, T* __restrict__ out) {
+__global__ void __launch_bounds__(256) k_avgpool(const T* __restrict__ x, int H, int W, int ldx, int cx0, int C,
+                                                 T* __restrict__ y) {
   const int b = blockIdx.y;
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
   const long HW = (long)H * W;
-  float s = 0.f;
-  for (long p = 0; p < HW; ++p) s += Elem<T>::ld(dy + ((size_t)b * HW + p) * lddy + cdy0 + c);
-  out[(size_t)b * C + c] = Elem<T>::cvt(s);
+  // CPU adaptive_avg_pool2d accumulates in acc_type<float> = double
+  double s = sum_hw_block<T, double>(x, HW, ldx, cx0, C, b);
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  if (threadIdx.x < 64 && c < C) y[(size_t)b * C + c] = Elem<T>::cvt((float)(s / (double)HW));
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_sum_hw(const T* __restrict__ dy, int H, int W, int lddy, int cdy0, int C,
+                                                T* __restrict__ out) {
+  const int b = blockIdx.y;
+  float s = sum_hw_block<T, float>(dy, (long)H * W, lddy, cdy0, C, b);
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  if (threadIdx.x < 64 && c < C) out[(size_t)b * C + c] = Elem<T>::cvt(s);
 }
 
 template <typename T>
@@ -688,7 +701,7 @@ extern "C" int zp_global_avgpool(const void* x, int B, int H, int W, int ldx, in
                                  void* stream) {
   ZP_DTYPE_CHECK("zp_global_avgpool", dtype);
   ZP_CHECK_ARG(x && y && B > 0 && H > 0 && W > 0 && C > 0, "zp_global_avgpool: bad args");
-  ZP_TLAUNCH(dtype, k_avgpool, dim3((C + 255) / 256, B), (hipStream_t)stream, (const T*)x, H, W, ldx, cx0, C, (T*)y);
+  ZP_TLAUNCH(dtype, k_avgpool, dim3((C + 63) / 64, B), (hipStream_t)stream, (const T*)x, H, W, ldx, cx0, C, (T*)y);
   ZP_LAUNCH_CHECK("zp_global_avgpool");
   return ZP_OK;
 }
@@ -708,7 +721,7 @@ extern "C" int zp_sum_hw(const void* dy, int B, int H, int W, int lddy, int cdy0
                          void* stream) {
   ZP_DTYPE_CHECK("zp_sum_hw", dtype);
   ZP_CHECK_ARG(dy && out && B > 0 && C > 0, "zp_sum_hw: bad args");
-  ZP_TLAUNCH(dtype, k_sum_hw, dim3((C + 255) / 256, B), (hipStream_t)stream, (const T*)dy, H, W, lddy, cdy0, C,
+  ZP_TLAUNCH(dtype, k_sum_hw, dim3((C + 63) / 64, B), (hipStream_t)stream, (const T*)dy, H, W, lddy, cdy0, C,
              (T*)out);
   ZP_LAUNCH_CHECK("zp_sum_hw");
   return ZP_OK;

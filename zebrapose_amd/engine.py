@@ -186,7 +186,10 @@ class Engine:
             e1.record()
             flops = 2.0 * x.B * plan.GH * plan.GW * sum(len(sb.taps) for sb in plan.subs) * x.C * cout
             wc = 4 if cout > 64 else (2 if cout > 32 else 1)
-            kname = (f"k_conv<{'bf16' if self.dt == L.ZP_BF16 else 'f32'},WC={wc},WP=4,"
+            nwp = 4 if L.lib.zp_conv2d_stat_parts(C.byref(a)) == 4 * L.lib.zp_conv2d_grid(C.byref(a)) * a.nsub \
+                else 2
+            # rocprofv3 name: k_conv<T, WC, WP=4, NWP, smallC>
+            kname = (f"k_conv<{'bf16' if self.dt == L.ZP_BF16 else 'f32'},WC={wc},WP=4,NWP={nwp},"
                      f"smallC={int(x.C < _KE[self.dt])}>")
             self.timing.append((label, e0, e1, flops, kname))
         else:
