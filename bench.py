@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--train-steps", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--layer-report", default=None, help="write per-launch conv timings (JSON) here")
     return ap.parse_args()
 
 
@@ -152,6 +153,17 @@ def main():
         d[0] += flops
         d[1] += e0.elapsed_time(e1) * 1e-3
         d[2] += 1
+    if args.layer_report and rank == 0:
+        lay = {}
+        for label, e0, e1, flops, kname in eng_t:
+            d = lay.setdefault(label, [kname, 0.0, 0.0, 0])
+            d[1] += e0.elapsed_time(e1) * 1e3
+            d[2] += flops
+            d[3] += 1
+        rows = [{"label": k, "kernel": v[0], "us": round(v[1] / v[3], 2), "tflops": round(v[2] / v[1] * 1e-6, 1)}
+                for k, v in lay.items()]
+        with open(args.layer_report, "w") as f:
+            json.dump(rows, f, indent=0)
     dom = max(per.items(), key=lambda kv: kv[1][1])
     kname, (fl, tsec, nl) = dom
     achieved = fl / tsec / 1e12

@@ -27,7 +27,9 @@ def golden():
     import numpy as np
 
     def load(name):
-        return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
+        # materialised: an NpzFile re-reads (and re-inflates) the member on every item access
+        with np.load(os.path.join(GOLDEN, name), allow_pickle=False) as z:
+            return {k: z[k] for k in z.files}
     return load
 
 

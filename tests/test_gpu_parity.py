@@ -185,7 +185,7 @@ def test_train_step_fp32_matches_reference(net_and_state, golden):
     np.testing.assert_allclose(lm.item(), float(f["loss_m"]), rtol=1e-4)
     (3 * lb + lm).backward()
     named = dict(net.named_parameters())
-    for k in f.files:
+    for k in f:
         if k.startswith("grad:"):
             name = k[5:]
             got = named[name].grad.cpu().numpy()[:8]
@@ -194,7 +194,7 @@ def test_train_step_fp32_matches_reference(net_and_state, golden):
             budget = 0.01 if "aspp.conv_1x1_4" in name else 0.10
             assert rel <= budget, (name, rel)
     sd2 = net.state_dict()
-    for k in f.files:
+    for k in f:
         if k.startswith("after:"):
             np.testing.assert_allclose(sd2[k[6:]].cpu().numpy(), f[k], rtol=1e-3, atol=1e-4)
 
@@ -223,8 +223,9 @@ def test_binary_code_helper_dropins(golden):
     """Reference-signature helpers (host arrays in/out, device decode inside)."""
     from zebrapose_amd.binary_code_helper.CNN_output_to_pose import decode_correspondences
     from zebrapose_amd.binary_code_helper.generate_new_dict import generate_new_corres_dict
-    d = golden("decode.npz")
-    lut_dict = {float(i): d["lut"][i] for i in range(65536)}
+    d = dict(golden("decode.npz"))  # materialise once: NpzFile re-reads the member on every access
+    lut = d["lut"]
+    lut_dict = {float(i): lut[i] for i in range(lut.shape[0])}
     for ib in (0, 2):
         dd = lut_dict if ib == 0 else generate_new_corres_dict(lut_dict, 16, 16 - ib)
         if ib:

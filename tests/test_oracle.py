@@ -63,12 +63,12 @@ def test_train_step_matches_reference(golden, state):
     np.testing.assert_allclose(lm.item(), float(f["loss_m"]), rtol=1e-6)
     np.testing.assert_allclose(st.histogram.numpy(), f["hist1"], rtol=0, atol=1e-12)
     loss.backward()
-    for k in f.files:
+    for k in f:
         if k.startswith("grad:"):
             name = k[5:]
             g = leaves[name].grad.numpy()[:8]
             np.testing.assert_allclose(g, f[k], atol=1e-5 * max(1e-3, np.abs(f[k]).max()) + 1e-9, rtol=1e-3)
-    for k in f.files:
+    for k in f:
         if k.startswith("after:"):
             np.testing.assert_allclose(sd[k[6:]].detach().numpy(), f[k], rtol=1e-5, atol=1e-7)
     # second BinaryCodeLoss call: histogram EMA (BinaryCodeNet.py:37-41)

@@ -5,13 +5,12 @@
 // model/resnet.py:41-51, model/aspp.py:60-80, 89-112 and the torchvision ResNet
 // children reused at resnet.py:191-199 (see include/zp.h).
 //
-// Forward tile: one 256-thread workgroup = 4 waves (2 cout x 2 pixel) computes
-// TC (=32*WC) output channels x TP (=32*WP) pixels.  The MFMA A operand is the
-// weight tile (rows = output channels), B is the activation tile (cols = pixels),
-// so each lane ends up with 4 consecutive output channels of one pixel -> 8/16 B
-// NHWC stores.  K steps are 128 bytes per row (64 bf16 / 32 f32) of one tap;
-// the tile is staged global -> registers -> LDS (XOR-swizzled 16 B chunks,
-// double-buffered, one barrier per K step).
+// Forward tile: one workgroup of 2*NWP waves (2 cout x NWP pixel) computes TC (=32*WC)
+// output channels x TP (=64*NWP) pixels.  The MFMA A operand is the weight tile (rows =
+// output channels), B is the activation tile (cols = pixels), so each lane ends up with 4
+// consecutive output channels of one pixel -> 8/16 B NHWC stores.  K steps are 128 bytes per
+// row (64 bf16 / 32 f32) of one tap, staged global -> LDS by LDS-DMA through a STAGES-deep
+// ring (XOR-swizzled 16 B chunks, one barrier per K step).
 #include <type_traits>
 #include "zp_common.h"
 
@@ -53,10 +52,12 @@ __device__ __forceinline__ void vm_wait() {
 // from global memory into LDS with global_load_lds_dwordx4 (one wave-instruction = 8 rows x
 // 128 B, lane-linear in LDS).  The 16 B chunk swizzle (chunk ^ (row & 7), conflict-free
 // ds_read_b128 of the MFMA fragments) is applied on the per-lane SOURCE address.  Out-of-
-// image taps read g_zero_page.  Two LDS buffers: the loads of step k+1 are in flight while
-// step k's MFMAs run; one __syncthreads (vmcnt(0) + s_barrier) per step.
-template <typename T, int WC, int WP, int NWP, bool SMALLC>
+// image taps read g_zero_page.  STAGES LDS buffers: the loads of steps k+1..k+STAGES-1 are
+// in flight while step k's MFMAs run; each step ends with a counted vmcnt wait (only the
+// oldest step's loads) and a raw s_barrier.
+template <typename T, int WC, int WP, int NWP, int STAGES, bool SMALLC>
 __global__ void __launch_bounds__(128 * NWP) k_conv(const zp_conv_args A) {
+  static_assert(STAGES == 2 || STAGES == 3, "2- or 3-deep LDS ring");
   constexpr int E = MfmaTraits<T>::E;
   constexpr int KE = 8 * E;  // elements per K step (128 B)
   constexpr int TC = 32 * WC, TP = 16 * WP * NWP;
@@ -66,7 +67,7 @@ __global__ void __launch_bounds__(128 * NWP) k_conv(const zp_conv_args A) {
   constexpr int GPW = G / NW;                 // groups per wave
   __shared__ uint4 lds0[(TC + TP) * 8];
   __shared__ uint4 lds1[(TC + TP) * 8];
-  __shared__ uint4 lds2[(TC + TP) * 8];
+  __shared__ uint4 lds2[STAGES == 3 ? (TC + TP) * 8 : 1];
   auto bufp = [&](auto i_c) -> uint4* {
     constexpr int i = decltype(i_c)::value;
     if constexpr (i == 0) return lds0;
@@ -178,8 +179,8 @@ __global__ void __launch_bounds__(128 * NWP) k_conv(const zp_conv_args A) {
 #pragma unroll
       for (int j = 0; j < WP; ++j) bfr[s][j] = cur[swz(TC + wp * 16 * WP + j * 16 + (lane & 15), ch)];
     }
-    const bool more = ks + 2 < nK;
-    if (more) issue(ks + 2, bufp(nxt_c));
+    const bool more = ks + (STAGES - 1) < nK;
+    if (more) issue(ks + (STAGES - 1), bufp(nxt_c));
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -187,7 +188,7 @@ __global__ void __launch_bounds__(128 * NWP) k_conv(const zp_conv_args A) {
 #pragma unroll
         for (int j = 0; j < WP; ++j) MfmaTraits<T>::mma(acc[i][j], af[s][i], bfr[s][j]);
     __builtin_amdgcn_sched_barrier(0);  // keep the MFMAs in front of the wait + barrier
-    if (more) vm_wait<GPW>();
+    if (more) vm_wait<GPW * (STAGES - 2)>();
     else vm_wait<0>();
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
@@ -196,20 +197,28 @@ __global__ void __launch_bounds__(128 * NWP) k_conv(const zp_conv_args A) {
   using I1 = std::integral_constant<int, 1>;
   using I2 = std::integral_constant<int, 2>;
   issue(0, lds0);
-  if (nK > 1) {
+  if (STAGES == 3 && nK > 1) {
     issue(1, lds1);
-    vm_wait<GPW>();
+    vm_wait<GPW * (STAGES - 2)>();
   } else {
     vm_wait<0>();
   }
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
-  for (int ks = 0; ks < nK; ks += 3) {
-    step(I0{}, I2{}, ks);
-    if (ks + 1 >= nK) break;
-    step(I1{}, I0{}, ks + 1);
-    if (ks + 2 >= nK) break;
-    step(I2{}, I1{}, ks + 2);
+  if constexpr (STAGES == 3) {
+    for (int ks = 0; ks < nK; ks += 3) {
+      step(I0{}, I2{}, ks);
+      if (ks + 1 >= nK) break;
+      step(I1{}, I0{}, ks + 1);
+      if (ks + 2 >= nK) break;
+      step(I2{}, I1{}, ks + 2);
+    }
+  } else {
+    for (int ks = 0; ks < nK; ks += 2) {
+      step(I0{}, I1{}, ks);
+      if (ks + 1 >= nK) break;
+      step(I1{}, I0{}, ks + 1);
+    }
   }
 
   // ---------------- epilogue ----------------
@@ -521,20 +530,47 @@ __global__ void k_wgrad_reduce(const zp_wgrad_args A, const float* __restrict__ 
 using namespace zp;
 
 // ------------------------------------------------------------------------------------ host
-template <typename T, int WC, int NWP, bool SMALLC>
+template <typename T, int WC, int NWP, int STAGES, bool SMALLC>
 static void launch_conv(const zp_conv_args& a, int gx, int gy, hipStream_t st) {
-  hipLaunchKernelGGL((k_conv<T, WC, 4, NWP, SMALLC>), dim3(gx, gy, a.nsub), dim3(128 * NWP), 0, st, a);
+  hipLaunchKernelGGL((k_conv<T, WC, 4, NWP, STAGES, SMALLC>), dim3(gx, gy, a.nsub), dim3(128 * NWP), 0, st,
+                     a);
 }
 
 static int conv_tc(int cout) { return cout > 64 ? 128 : (cout > 32 ? 64 : 32); }
 
-// pixel tile: 256 (8 waves) when that still gives >= 1024 workgroups, else 128 (4 waves)
+// Tuning overrides for sweeps (read once): ZP_CONV_TP=128|256 forces the pixel tile,
+// ZP_CONV_STAGES=2|3 forces the LDS ring depth.  0 = heuristic.
+static int env_int(const char* name) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : 0;
+}
+static int conv_tp_override() {
+  static const int v = env_int("ZP_CONV_TP");
+  return v;
+}
+static int conv_stages_override() {
+  static const int v = env_int("ZP_CONV_STAGES");
+  return v;
+}
+
+// pixel tile: 256 (8 waves) whenever the cout tile allows it.  Measured on MI355X (R34 bs32,
+// profiles/r01_conv_sweep.md): the 8-wave 3-stage tile beats the 4-wave tiles even on the
+// 32x32 layers where it leaves part of the chip idle (fewer workgroups, but 2x the MFMA work
+// per LDS byte and deeper prefetch)
 static int conv_tp(const zp_conv_args& a) {
-  long M = (long)a.N * a.GH * a.GW;
   int tc = a.Cout > 64 ? 128 : (a.Cout > 32 ? 64 : 32);
-  if (tc == 32) return 128;
-  long blocks256 = (long)ceil_div(M, 256) * ceil_div(a.Cout, tc) * a.nsub;
-  return blocks256 >= 1024 ? 256 : 128;
+  if (tc == 32) return 128;  // 32 + 256 rows do not split over 8 waves in 8-row groups
+  const int ov = conv_tp_override();
+  if (ov == 128 || ov == 256) return ov;
+  return 256;
+}
+
+// LDS ring depth: 3 (measured faster than 2 for both tile shapes; 2 is kept for sweeps)
+static int conv_stages(int nwp) {
+  (void)nwp;
+  const int ov = conv_stages_override();
+  if (ov == 2 || ov == 3) return ov;
+  return 3;
 }
 
 extern "C" int zp_conv2d_grid(const zp_conv_args* a) {
@@ -581,9 +617,12 @@ extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
   const int gx = zp_conv2d_grid(&a), gy = ceil_div(a.Cout, tc);
   hipStream_t st = (hipStream_t)stream;
   const int nwp = conv_tp(a) / 64;
+  const int stages = conv_stages(nwp);
+#define ZP_DISPATCH_ST(T, WC, NWP, ST)                                   \
+  if (smallc) launch_conv<T, WC, NWP, ST, true>(a, gx, gy, st);          \
+  else launch_conv<T, WC, NWP, ST, false>(a, gx, gy, st);
 #define ZP_DISPATCH_NWP(T, WC, NWP)                                      \
-  if (smallc) launch_conv<T, WC, NWP, true>(a, gx, gy, st);              \
-  else launch_conv<T, WC, NWP, false>(a, gx, gy, st);
+  if (stages == 3) { ZP_DISPATCH_ST(T, WC, NWP, 3) } else { ZP_DISPATCH_ST(T, WC, NWP, 2) }
 #define ZP_DISPATCH(T)                                                   \
   if (tc == 128) {                                                       \
     if (nwp == 4) { ZP_DISPATCH_NWP(T, 4, 4) } else { ZP_DISPATCH_NWP(T, 4, 2) } \
@@ -597,6 +636,7 @@ extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
   } else {
     ZP_DISPATCH(float)
   }
+#undef ZP_DISPATCH_ST
 #undef ZP_DISPATCH_NWP
 #undef ZP_DISPATCH
   ZP_LAUNCH_CHECK("zp_conv2d");

@@ -23,6 +23,7 @@ input's gradient buffer).
 from __future__ import annotations
 
 import ctypes as C
+import os
 import weakref
 
 import torch
@@ -188,10 +189,14 @@ class Engine:
             wc = 4 if cout > 64 else (2 if cout > 32 else 1)
             nwp = 4 if L.lib.zp_conv2d_stat_parts(C.byref(a)) == 4 * L.lib.zp_conv2d_grid(C.byref(a)) * a.nsub \
                 else 2
-            # rocprofv3 name: k_conv<T, WC, WP=4, NWP, smallC>
+            # rocprofv3 name: k_conv<T, WC, WP=4, NWP, STAGES, smallC> (stage rule: zp_conv.hip conv_stages)
+            st_ov = int(os.environ.get("ZP_CONV_STAGES", "0") or 0)
+            stages = st_ov if st_ov in (2, 3) else 3
             kname = (f"k_conv<{'bf16' if self.dt == L.ZP_BF16 else 'f32'},WC={wc},WP=4,NWP={nwp},"
-                     f"smallC={int(x.C < _KE[self.dt])}>")
-            self.timing.append((label, e0, e1, flops, kname))
+                     f"ST={stages},smallC={int(x.C < _KE[self.dt])}>")
+            geo = (f"{label}:{x.C}->{cout} taps{max(len(sb.taps) for sb in plan.subs)} "
+                   f"{x.H}x{x.W}->{plan.GH}x{plan.GW}x{a.nsub}")
+            self.timing.append((geo, e0, e1, flops, kname))
         else:
             L.check(L.lib.zp_conv2d(C.byref(a), st), "zp_conv2d")
         return stats, parts
