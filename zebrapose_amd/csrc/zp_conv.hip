@@ -48,6 +48,37 @@ __device__ __forceinline__ void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// Per-launch tap grids, derived on the host from the subs' tap lists (every plan of
+// geometry.py enumerates taps as a (tap row) x (tap column) grid, rows outer:
+// ty = ty0 + q * dty, tx = tx0 + r * dtx for tap q * nx + r), plus the byte extents of the
+// activation / weight buffers for the buffer-load range check.
+struct conv_taps {
+  int ny[ZP_MAX_SUB], nx[ZP_MAX_SUB], ty0[ZP_MAX_SUB], dty[ZP_MAX_SUB], tx0[ZP_MAX_SUB], dtx[ZP_MAX_SUB];
+  unsigned x_bytes, w_bytes[ZP_MAX_SUB];
+};
+
+// LDS byte address of a __shared__ pointer
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+// ds_read_b128 with an immediate offset; the caller waits lgkmcnt itself
+template <int OFF>
+__device__ __forceinline__ uint4 ds_read16(unsigned addr) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset range");
+  uint4 r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF) : "memory");
+  return r;
+}
+
+template <int N, typename F, int I = 0>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<N, F, I + 1>(static_cast<F&&>(f));
+  }
+}
+
 // Staging: every K step moves TC weight rows + TP activation rows of 128 B each straight
 // from global memory into LDS with global_load_lds_dwordx4 (one wave-instruction = 8 rows x
 // 128 B, lane-linear in LDS).  The 16 B chunk swizzle (chunk ^ (row & 7), conflict-free
@@ -56,7 +87,7 @@ __device__ __forceinline__ void vm_wait() {
 // in flight while step k's MFMAs run; each step ends with a counted vmcnt wait (only the
 // oldest step's loads) and a raw s_barrier.
 template <typename T, int WC, int WP, int NWP, int STAGES, bool SMALLC>
-__global__ void __launch_bounds__(128 * NWP) k_conv(const zp_conv_args A) {
+__global__ void __launch_bounds__(128 * NWP) k_conv(const zp_conv_args A, const conv_taps TG, const int flags) {
   static_assert(STAGES == 2 || STAGES == 3, "2- or 3-deep LDS ring");
   constexpr int E = MfmaTraits<T>::E;
   constexpr int KE = 8 * E;  // elements per K step (128 B)
@@ -81,7 +112,20 @@ __global__ void __launch_bounds__(128 * NWP) k_conv(const zp_conv_args A) {
   const int wc = wid / NWP, wp = wid % NWP;
   const int GHW = A.GH * A.GW;
   const int M = A.N * GHW;
-  const int p0 = blockIdx.x * TP, c0 = blockIdx.y * TC;
+  // XCD-aware tile order (flags & 2): workgroups are dispatched round-robin over the
+  // 8 XCDs, so consecutive linear ids land on different L2s.  Remap so that each XCD walks a
+  // contiguous run of (pixel tile, cout tile) pairs, cout tiles fastest: the cout tiles of one
+  // pixel tile (same activations) and neighbouring pixel tiles (shared halo rows) then meet in
+  // the same L2.
+  int bx = blockIdx.x, by = blockIdx.y;
+  if (flags & 2) {
+    const int total = gridDim.x * gridDim.y;
+    const int bid = blockIdx.x + gridDim.x * blockIdx.y;
+    const int lin = (total & 7) ? bid : (bid & 7) * (total >> 3) + (bid >> 3);
+    bx = lin / gridDim.y;
+    by = lin - bx * gridDim.y;
+  }
+  const int p0 = bx * TP, c0 = by * TC;
   const int lrow = lane >> 3;                  // row within the 8-row group
   const int csrc = (lane & 7) ^ lrow;          // source chunk (swizzle on the source side)
 
@@ -105,55 +149,111 @@ __global__ void __launch_bounds__(128 * NWP) k_conv(const zp_conv_args A) {
   const int CB = SMALLC ? 1 : A.Cin / KE;
   const int nK = SMALLC ? A.k_pad / KE : S.ntaps * CB;
 
+  // ---- staging addresses (Cin >= 64 B-chunk path): buffer loads with per-lane 32-bit byte
+  // offsets.  The tap walk (ty, tx, channel chunk) is scalar state advanced by one K step per
+  // issue; per lane only the pixel's base offset and two validity bit masks (input row / column
+  // in range, one bit per tap row / column) are kept.  Invalid taps use an offset past the
+  // buffer's end, which the buffer unit returns as zeros: no address clamp, no select of a
+  // zero page, no multiplies in the loop.
+  const int tb = blockIdx.z;
+  const int ny = TG.ny[tb], nx = TG.nx[tb], dty = TG.dty[tb], dtx = TG.dtx[tb];
+  unsigned abase[GPW], ymask[GPW], xmask[GPW];
+#pragma unroll
+  for (int i = 0; i < GPW; ++i) {
+    const int y0 = gpix_y[i], x0 = gpix_x[i];
+    abase[i] = (unsigned)(((((long)gpix_n[i] * A.IH + y0) * A.IW + x0) * A.ldx + A.cx0 + csrc * E) * sizeof(T));
+    unsigned ym = 0, xm = 0;
+    for (int q = 0; q < ny; ++q) ym |= (unsigned)((unsigned)(y0 + TG.ty0[tb] + q * dty) < (unsigned)A.IH) << q;
+    for (int q = 0; q < nx; ++q) xm |= (unsigned)((unsigned)(x0 + TG.tx0[tb] + q * dtx) < (unsigned)A.IW) << q;
+    ymask[i] = gvalid[i] ? ym : 0u;
+    xmask[i] = xm;
+  }
+  const unsigned wbase = (unsigned)(((size_t)(c0 + wid * 8 + lrow) * A.k_pad + csrc * E) * sizeof(T));
+  // scalar tap walk: the next K step to issue is (tap row tyi, tap column txi, chunk cb) with
+  // act_off = ((ty * IW + tx) * ldx + cb * KE) * sizeof(T)
+  int w_tyi = 0, w_txi = 0, w_cb = 0;
+  int act_off = ((TG.ty0[tb] * A.IW + TG.tx0[tb]) * A.ldx) * (int)sizeof(T);
+  const int step_x = dtx * A.ldx * (int)sizeof(T), step_y = dty * A.IW * A.ldx * (int)sizeof(T);
+  const int chunk_b = KE * (int)sizeof(T);
+#if defined(__HIP_DEVICE_COMPILE__)
+  const __amdgpu_buffer_rsrc_t xrsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)TG.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)Wt, (short)0, (int)TG.w_bytes[tb], 0x00020000);
+#endif
+
   auto issue = [&](int ks, uint4* dst) {
-    int ty, tx, cc;
-    bool tok;
-    if (SMALLC) {
+    if constexpr (SMALLC) {
+      // small Cin (stem): one K step mixes taps, per-lane tap decode
+      const int kw_off = ks * KE;
       int k = ks * KE + csrc * E;
       int t = k / A.Cin;
-      cc = k - t * A.Cin;
-      tok = t < S.ntaps;
+      const int cc = k - t * A.Cin;
+      const bool tok = t < S.ntaps;
       int kyy = t / S.kw;
-      ty = kyy * S.dil - S.pad;
-      tx = (t - kyy * S.kw) * S.dil - S.pad;
-    } else {
-      int t = ks / CB;
-      cc = (ks - t * CB) * KE + csrc * E;
-      // tap offsets through scalar dword loads (s_load, counted by lgkmcnt): a byte load would be
-      // a vector load, and waiting for it would also drain the in-flight LDS-DMA ring (vmcnt)
-      const int wy = ((const int*)S.ty)[t >> 2], wx = ((const int*)S.tx)[t >> 2];
-      const int sh = 24 - 8 * (t & 3);
-      ty = (wy << sh) >> 24;
-      tx = (wx << sh) >> 24;
-      tok = true;
-    }
-    // all source addresses first (distinct registers), then the DMA issues back to back: hipcc
-    // waits vmcnt(0) before it rewrites the address VGPRs of an in-flight global_load_lds
-    const void* srcs[GPW];
+      const int ty = kyy * S.dil - S.pad;
+      const int tx = (t - kyy * S.kw) * S.dil - S.pad;
+      const void* srcs[GPW];
 #pragma unroll
-    for (int i = 0; i < GPW; ++i) {
-      const int g = wid + NW * i;
-      const int r = g * 8 + lrow;
-      const void* src;
-      if (g * 8 < TC) {  // wave-uniform: groups never straddle the weight / activation boundary
-        src = Wt + (size_t)(c0 + r) * A.k_pad + (size_t)ks * KE + csrc * E;
-      } else {
-        int iy = gpix_y[i] + ty, ix = gpix_x[i] + tx;
-        bool ok = tok && gvalid[i] && (unsigned)iy < (unsigned)A.IH && (unsigned)ix < (unsigned)A.IW;
-        // branch-free: address of a clamped (always valid) pixel, then a pointer select
-        int iyc = min(max(iy, 0), A.IH - 1), ixc = min(max(ix, 0), A.IW - 1);
-        const T* pv = X + (((size_t)gpix_n[i] * A.IH + iyc) * A.IW + ixc) * A.ldx + A.cx0 + cc;
-        src = ok ? (const void*)pv : (const void*)&g_zero_page[lane & 7];
+      for (int i = 0; i < GPW; ++i) {
+        const int g = wid + NW * i;
+        const int r = g * 8 + lrow;
+        const void* src;
+        if (g * 8 < TC) {
+          src = Wt + (size_t)(c0 + r) * A.k_pad + kw_off + csrc * E;
+        } else {
+          int iy = gpix_y[i] + ty, ix = gpix_x[i] + tx;
+          bool ok = tok && gvalid[i] && (unsigned)iy < (unsigned)A.IH && (unsigned)ix < (unsigned)A.IW;
+          int iyc = min(max(iy, 0), A.IH - 1), ixc = min(max(ix, 0), A.IW - 1);
+          const T* pv = X + (((size_t)gpix_n[i] * A.IH + iyc) * A.IW + ixc) * A.ldx + A.cx0 + cc;
+          src = ok ? (const void*)pv : (const void*)&g_zero_page[lane & 7];
+        }
+        srcs[i] = src;
       }
-      srcs[i] = src;
-    }
 #if defined(__HIP_DEVICE_COMPILE__)  // device-only builtin: the host pass would silently drop the kernel stubs
 #pragma unroll
-    for (int i = 0; i < GPW; ++i) {
-      const int g = wid + NW * i;
-      __builtin_amdgcn_global_load_lds(srcs[i], (__attribute__((address_space(3))) void*)&dst[g * 64], 16, 0, 0);
-    }
+      for (int i = 0; i < GPW; ++i) {
+        const int g = wid + NW * i;
+        __builtin_amdgcn_global_load_lds(srcs[i], (__attribute__((address_space(3))) void*)&dst[g * 64], 16, 0, 0);
+      }
 #endif
+    } else {
+      // all offsets first (distinct registers), then the DMA issues back to back: hipcc waits
+      // vmcnt(0) before it rewrites the address VGPRs of an in-flight LDS-DMA
+      unsigned voff[GPW];
+#pragma unroll
+      for (int i = 0; i < GPW; ++i) {
+        const int g = wid + NW * i;
+        if (g * 8 < TC) {  // wave-uniform: groups never straddle the weight / activation boundary
+          voff[i] = wbase + (unsigned)(NW * i * 8) * (unsigned)(A.k_pad * sizeof(T));
+        } else {
+          const bool ok = (ymask[i] >> w_tyi) & (xmask[i] >> w_txi) & 1u;
+          voff[i] = ok ? abase[i] + (unsigned)act_off : 0x80000000u;
+        }
+      }
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+      for (int i = 0; i < GPW; ++i) {
+        const int g = wid + NW * i;
+        auto* d = (__attribute__((address_space(3))) void*)&dst[g * 64];
+        if (g * 8 < TC)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(wrsrc, d, 16, voff[i], ks * chunk_b, 0, 0);
+        else
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(xrsrc, d, 16, voff[i], 0, 0, 0);
+      }
+#endif
+      // advance the scalar tap walk to step ks + 1 (tap-major: chunks fastest)
+      act_off += chunk_b;
+      if (++w_cb == CB) {
+        w_cb = 0;
+        act_off += step_x - CB * chunk_b;
+        if (++w_txi == nx) {
+          w_txi = 0;
+          act_off += step_y - nx * step_x;
+          ++w_tyi;
+        }
+      }
+    }
   };
 
   f32x4 acc[WC][WP];
@@ -168,28 +268,56 @@ __global__ void __launch_bounds__(128 * NWP) k_conv(const zp_conv_args A) {
   // vmcnt(0) would drain the ring.  Buffer indices are compile-time (loop unrolled by 3) and the
   // three buffers are distinct LDS objects, so hipcc can prove a ds_read never aliases an
   // in-flight global_load_lds and inserts no vmcnt wait in front of it.
+  const bool pingpong = NW == 8 && !SMALLC && (flags & 8);
+  // per-lane byte offsets of the MFMA fragments inside a stage buffer: row (lane & 15) of the
+  // wave's first 16-row tile, 16 B chunk (s * 4 + lane / 16) swizzled by (row & 7) = (lane & 7);
+  // tile i / j adds i * 16 rows = i * 2048 B (an immediate of the ds_read)
+  unsigned aoff[2], boff[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    const unsigned chunk = (unsigned)(((s2 * 4 + (lane >> 4)) ^ (lane & 7)) * 16);
+    aoff[s2] = (unsigned)(wc * 16 * WC + (lane & 15)) * 128u + chunk;
+    boff[s2] = (unsigned)(TC + wp * 16 * WP + (lane & 15)) * 128u + chunk;
+  }
   auto step = [&](auto cur_c, auto nxt_c, int ks) {
-    const uint4* cur = bufp(cur_c);
+    const bool more = ks + (STAGES - 1) < nK;
+    // next stage's DMA first (its tap offsets come from scalar loads, whose lgkmcnt wait must
+    // not also wait for this step's fragment reads)
+    if (more) issue(ks + (STAGES - 1), bufp(nxt_c));
+    // fragment reads as inline asm: hipcc's waitcnt pass cannot prove across the loop back-edge
+    // that they miss the in-flight LDS-DMA buffers and would put a vmcnt(0) in front of them
+    const unsigned cb = lds_addr(bufp(cur_c));
     uint4 af[2][WC], bfr[2][WP];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int ch = s * 4 + (lane >> 4);
-#pragma unroll
-      for (int i = 0; i < WC; ++i) af[s][i] = cur[swz(wc * 16 * WC + i * 16 + (lane & 15), ch)];
-#pragma unroll
-      for (int j = 0; j < WP; ++j) bfr[s][j] = cur[swz(TC + wp * 16 * WP + j * 16 + (lane & 15), ch)];
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const unsigned pa = cb + aoff[s2], pb = cb + boff[s2];
+      static_for<WC>([&](auto i) { af[s2][i] = ds_read16<i * 2048>(pa); });
+      static_for<WP>([&](auto j) { bfr[s2][j] = ds_read16<j * 2048>(pb); });
     }
-    const bool more = ks + (STAGES - 1) < nK;
-    if (more) issue(ks + (STAGES - 1), bufp(nxt_c));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (pingpong) {
+      // end of the read section: fragments in registers (the other group may refill this
+      // buffer after the barrier) and every load but the newest step's retired, so the next
+      // step's buffer is complete once all waves have passed the barrier
+      if (more) vm_wait<GPW * (STAGES - 2)>();
+      else vm_wait<0>();
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (flags & 4) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+    for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
       for (int i = 0; i < WC; ++i)
 #pragma unroll
-        for (int j = 0; j < WP; ++j) MfmaTraits<T>::mma(acc[i][j], af[s][i], bfr[s][j]);
+        for (int j = 0; j < WP; ++j) MfmaTraits<T>::mma(acc[i][j], af[s2][i], bfr[s2][j]);
     __builtin_amdgcn_sched_barrier(0);  // keep the MFMAs in front of the wait + barrier
-    if (more) vm_wait<GPW * (STAGES - 2)>();
-    else vm_wait<0>();
+    if (flags & 4) __builtin_amdgcn_s_setprio(0);
+    if (!pingpong) {
+      if (more) vm_wait<GPW * (STAGES - 2)>();
+      else vm_wait<0>();
+    }
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
   };
@@ -205,6 +333,10 @@ __global__ void __launch_bounds__(128 * NWP) k_conv(const zp_conv_args A) {
   }
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
+  // Ping-pong (flags & 8, 8-wave tiles): every step is a read section (fragments + next DMA)
+  // and an MFMA section, each closed by a barrier; waves 4-7 start one barrier late, so on
+  // every SIMD (waves w and w+4 share one) one wave's MFMAs overlap the other's LDS reads.
+  if (pingpong && wid >= 4) __builtin_amdgcn_s_barrier();
   if constexpr (STAGES == 3) {
     for (int ks = 0; ks < nK; ks += 3) {
       step(I0{}, I2{}, ks);
@@ -221,15 +353,112 @@ __global__ void __launch_bounds__(128 * NWP) k_conv(const zp_conv_args A) {
     }
   }
 
+  if (pingpong && wid < 4) __builtin_amdgcn_s_barrier();  // same barrier count for both groups
+
   // ---------------- epilogue ----------------
+  // output pixel of (lane, j): one division for j = 0, then +16 pixels per j
+  int pn[WP], poy[WP], pox[WP];
+  bool pok[WP];
+  {
+    const int pw0 = p0 + wp * 16 * WP + (lane & 15);
+    int n = pw0 / GHW, rr = pw0 - n * GHW;
+    int gy = rr / A.GW, gx = rr - gy * A.GW;
+    const bool fast = A.GW % 16 == 0;
+#pragma unroll
+    for (int j = 0; j < WP; ++j) {
+      const int p = pw0 + j * 16;
+      pok[j] = p < M;
+      if (j > 0) {
+        if (fast) {
+          gx += 16;
+          if (gx >= A.GW) {
+            gx -= A.GW;
+            if (++gy == A.GH) {
+              gy = 0;
+              ++n;
+            }
+          }
+        } else {
+          n = p / GHW;
+          rr = p - n * GHW;
+          gy = rr / A.GW;
+          gx = rr - gy * A.GW;
+        }
+      }
+      pn[j] = n;
+      poy[j] = gy * S.oys + S.oyo;
+      pox[j] = gx * S.oxs + S.oxo;
+    }
+  }
+  bool stored = false;
+  if constexpr (sizeof(T) == 2 && WC % 2 == 0) {
+    // bf16 NHWC fast path: v_permlane16_swap pairs lane groups (g, g + 1) so that each lane
+    // holds 8 consecutive output channels of one pixel (tiles i and i + 1 exchange halves):
+    // 16 B stores (and residual loads), half the store instructions
+    if (A.out_mode == ZP_OUT_NHWC && A.Cout % 8 == 0 && S.ldy % 8 == 0 && S.cy0 % 8 == 0 &&
+        (!A.res || (A.ldr % 8 == 0 && A.cr0 % 8 == 0))) {
+      stored = true;
+      const int g = lane >> 4;
+#pragma unroll
+      for (int i = 0; i < WC; i += 2) {
+        const int cs = c0 + wc * 16 * WC + (i + (g & 1)) * 16 + (g >> 1) * 8;
+        const bool cok = cs < A.Cout;
+        float sc[8], sh[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          sc[r] = 1.f;
+          sh[r] = 0.f;
+        }
+        if (cok && S.scale) {
+          const float4 s0 = *(const float4*)(S.scale + cs), s1 = *(const float4*)(S.scale + cs + 4);
+          sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w;
+          sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
+        }
+        if (cok && S.shift) {
+          const float4 s0 = *(const float4*)(S.shift + cs), s1 = *(const float4*)(S.shift + cs + 4);
+          sh[0] = s0.x; sh[1] = s0.y; sh[2] = s0.z; sh[3] = s0.w;
+          sh[4] = s1.x; sh[5] = s1.y; sh[6] = s1.z; sh[7] = s1.w;
+        }
+#pragma unroll
+        for (int j = 0; j < WP; ++j) {
+          float v[8];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {  // all lanes active here (cross-lane op)
+            const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][j][r]),
+                                                             __float_as_uint(acc[i + 1][j][r]), false, false);
+            v[r] = __uint_as_float(sw[0]);
+            v[r + 4] = __uint_as_float(sw[1]);
+          }
+          if (!pok[j] || !cok) continue;
+          const size_t pix = ((size_t)pn[j] * S.OH + poy[j]) * S.OW + pox[j];
+#pragma unroll
+          for (int r = 0; r < 8; ++r) v[r] = v[r] * sc[r] + sh[r];
+          if (A.res) {
+            const uint4 rv = *(const uint4*)((const bf16_t*)A.res + pix * A.ldr + A.cr0 + cs);
+            const uint32_t rw[4] = {rv.x, rv.y, rv.z, rv.w};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              v[2 * r] += __uint_as_float(rw[r] << 16);
+              v[2 * r + 1] += __uint_as_float(rw[r] & 0xffff0000u);
+            }
+          }
+          if (A.relu) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) v[r] = fmaxf(v[r], 0.f);
+          }
+          uint32_t o[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = (uint32_t)f2bf(v[2 * r]) | ((uint32_t)f2bf(v[2 * r + 1]) << 16);
+          *(uint4*)((bf16_t*)S.y + pix * S.ldy + S.cy0 + cs) = make_uint4(o[0], o[1], o[2], o[3]);
+        }
+      }
+    }
+  }
   const int cbase = c0 + wc * 16 * WC + (lane >> 4) * 4;
 #pragma unroll
-  for (int j = 0; j < WP; ++j) {
-    const int p = p0 + wp * 16 * WP + j * 16 + (lane & 15);
-    if (p >= M) continue;
-    int n = p / GHW, rr = p - n * GHW;
-    int gy = rr / A.GW, gx = rr - gy * A.GW;
-    int oy = gy * S.oys + S.oyo, ox = gx * S.oxs + S.oxo;
+  for (int j = 0; j < WP && !stored; ++j) {
+    if (!pok[j]) continue;
+    const int n = pn[j], oy = poy[j], ox = pox[j];
     size_t pix = ((size_t)n * S.OH + oy) * S.OW + ox;
 #pragma unroll
     for (int i = 0; i < WC; ++i) {
@@ -298,7 +527,7 @@ __global__ void __launch_bounds__(128 * NWP) k_conv(const zp_conv_args A) {
     // (count, mean, M2) with M2 centred on the local mean (two passes over the registers, no
     // E[x^2] - E[x]^2 cancellation); zp_bn_train_finalize merges the parts (Chan et al.).
     const int parts = gridDim.x * gridDim.z * NWP;
-    const int part = (blockIdx.z * gridDim.x + blockIdx.x) * NWP + wp;
+    const int part = (blockIdx.z * gridDim.x + bx) * NWP + wp;
     float cnt = 0.f;
 #pragma unroll
     for (int j = 0; j < WP; ++j) cnt += (p0 + wp * 16 * WP + j * 16 + (lane & 15) < M) ? 1.f : 0.f;
@@ -530,10 +759,12 @@ __global__ void k_wgrad_reduce(const zp_wgrad_args A, const float* __restrict__ 
 using namespace zp;
 
 // ------------------------------------------------------------------------------------ host
+static int conv_flags();
+
 template <typename T, int WC, int NWP, int STAGES, bool SMALLC>
-static void launch_conv(const zp_conv_args& a, int gx, int gy, hipStream_t st) {
+static void launch_conv(const zp_conv_args& a, const conv_taps& tg, int gx, int gy, hipStream_t st) {
   hipLaunchKernelGGL((k_conv<T, WC, 4, NWP, STAGES, SMALLC>), dim3(gx, gy, a.nsub), dim3(128 * NWP), 0, st,
-                     a);
+                     a, tg, conv_flags());
 }
 
 static int conv_tc(int cout) { return cout > 64 ? 128 : (cout > 32 ? 64 : 32); }
@@ -550,6 +781,14 @@ static int conv_tp_override() {
 }
 static int conv_stages_override() {
   static const int v = env_int("ZP_CONV_STAGES");
+  return v;
+}
+
+// k_conv schedule switches: bit 1 XCD-aware tile order, bit 2 s_setprio(1) around the MFMA
+// cluster, bit 3 ping-pong (staggered wave groups).  Default (measured, profiles/r01_conv_sweep.md):
+// setprio + ping-pong.  ZP_CONV_FLAGS overrides for sweeps.
+static int conv_flags() {
+  static const int v = getenv("ZP_CONV_FLAGS") ? env_int("ZP_CONV_FLAGS") : 12;
   return v;
 }
 
@@ -613,14 +852,41 @@ extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
     }
   }
   if (a.res) ZP_CHECK_ARG(a.ldr >= a.cr0 + a.Cout && a.cr0 % 4 == 0, "zp_conv2d: bad residual ld");
+  conv_taps tg{};
+  {
+    const long long xb = (long long)a.N * a.IH * a.IW * a.ldx * (E == 8 ? 2 : 4);
+    const long long wb = (long long)a.w_rows * a.k_pad * (E == 8 ? 2 : 4);
+    ZP_CHECK_ARG(xb < (1ll << 31) && wb < (1ll << 31),
+                 "zp_conv2d: input (%lld B) / weights (%lld B) must stay below 2 GiB per launch (split the batch)",
+                 xb, wb);
+    tg.x_bytes = (unsigned)xb;
+    for (int s = 0; s < a.nsub; ++s) {
+      const zp_conv_sub& S = a.sub[s];
+      tg.w_bytes[s] = (unsigned)wb;
+      int nx = 1;
+      while (nx < S.ntaps && S.ty[nx] == S.ty[0]) ++nx;
+      const int ny = S.ntaps / nx;
+      tg.ny[s] = ny;
+      tg.nx[s] = nx;
+      tg.ty0[s] = S.ty[0];
+      tg.tx0[s] = S.tx[0];
+      tg.dty[s] = ny > 1 ? S.ty[nx] - S.ty[0] : 0;
+      tg.dtx[s] = nx > 1 ? S.tx[1] - S.tx[0] : 0;
+      if (smallc) continue;  // the small-Cin path decodes (kw, dil, pad) per lane instead
+      bool grid = ny * nx == S.ntaps && ny <= 32 && nx <= 32;
+      for (int t = 0; grid && t < S.ntaps; ++t)
+        grid = S.ty[t] == tg.ty0[s] + (t / nx) * tg.dty[s] && S.tx[t] == tg.tx0[s] + (t % nx) * tg.dtx[s];
+      ZP_CHECK_ARG(grid, "zp_conv2d: sub %d taps must form a (row x column) grid of at most 32 x 32, rows outer", s);
+    }
+  }
   const int tc = conv_tc(a.Cout);
   const int gx = zp_conv2d_grid(&a), gy = ceil_div(a.Cout, tc);
   hipStream_t st = (hipStream_t)stream;
   const int nwp = conv_tp(a) / 64;
   const int stages = conv_stages(nwp);
 #define ZP_DISPATCH_ST(T, WC, NWP, ST)                                   \
-  if (smallc) launch_conv<T, WC, NWP, ST, true>(a, gx, gy, st);          \
-  else launch_conv<T, WC, NWP, ST, false>(a, gx, gy, st);
+  if (smallc) launch_conv<T, WC, NWP, ST, true>(a, tg, gx, gy, st);      \
+  else launch_conv<T, WC, NWP, ST, false>(a, tg, gx, gy, st);
 #define ZP_DISPATCH_NWP(T, WC, NWP)                                      \
   if (stages == 3) { ZP_DISPATCH_ST(T, WC, NWP, 3) } else { ZP_DISPATCH_ST(T, WC, NWP, 2) }
 #define ZP_DISPATCH(T)                                                   \
