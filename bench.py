@@ -18,6 +18,7 @@ rank 0, N = 1, bounded sample).
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import sys
@@ -168,12 +169,12 @@ def main():
     kname, (fl, tsec, nl) = dom
     achieved = fl / tsec / 1e12
     traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
-    if os.path.exists(pmc_path):
-        try:
-            traffic = json.load(open(pmc_path)).get(kname)
-        except Exception:
-            traffic = None
+    # HBM bytes per launch of this kernel instance from the committed PMC passes (rocprofv3 cannot
+    # run inside this process): tools/prof_round.sh + tools/prof_summary.py -> profiles/<tag>_pmc_traffic.json
+    pmc = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    if pmc:
+        with open(pmc[-1]) as fh:
+            traffic = json.load(fh).get("by_label", {}).get(kname)
     all_conv_flops = sum(v[0] for v in per.values())
     all_conv_time = sum(v[1] for v in per.values())
     roofline = {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 2), "peak": PEAK[args.precision],

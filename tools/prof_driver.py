@@ -1,0 +1,74 @@
+#!/usr/bin/env python3
+"""Kernel-level profiling driver for rocprofv3 (run on the GPU box by tools/prof_round.sh).
+
+--mode train: K training steps (configs[2]: R34 bs=32 bf16, hist-weighted BCE + mask loss,
+backward, Adam).  --mode infer: K eval forwards + decode (configs[1]) with NO train-mode BN
+calibration pass, so every dispatch of a kernel in the trace belongs to an identical eval step
+(the PMC per-launch averages in profiles/ are taken over exactly those).  Prints ms/step."""
+import argparse
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ.setdefault("ZP_QUIET", "1")
+
+from bench import calibrate_bn, synthetic_crops  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--precision", default="bf16")
+    ap.add_argument("--mode", default="train", choices=["train", "infer"])
+    a = ap.parse_args()
+    from zebrapose_amd.model.BinaryCodeNet import BinaryCodeNet_Deeplab
+    from zebrapose_amd.train import TrainStep
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(1234)
+    net = BinaryCodeNet_Deeplab(34, 16, 2, concat=True, output_kernel_size=1, precision=a.precision).to(dev)
+    x = synthetic_crops(a.batch, 256, dev, seed=100)
+    if a.mode == "infer":
+        from bench import synthetic_lut
+        from zebrapose_amd.decode import Decoder
+        import numpy as np
+        net.eval()
+        dec = Decoder(synthetic_lut(), device=dev)
+        bb = np.array([[10, 20, 128, 128]] * a.batch)
+
+        def step():
+            with torch.no_grad():
+                m, c = net(x)
+                return dec(m, c, bb, bbox_size=128)
+        for _ in range(a.warmup):
+            step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            step()
+        torch.cuda.synchronize()
+        print(f"infer ms/step {(time.perf_counter() - t0) / a.steps * 1e3:.3f}")
+        return
+    calibrate_bn(net, x)
+    net.train()
+    ts = TrainStep(net, learning_rate=2e-4)
+    g = torch.Generator(device="cpu").manual_seed(7)
+    gt_code = (torch.rand((a.batch, 16, 128, 128), generator=g) < 0.5).to(torch.uint8).to(dev)
+    gt_mask = (torch.rand((a.batch, 128, 128), generator=g) < 0.7).float().to(dev)
+    for _ in range(a.warmup):
+        ts(x, gt_code, gt_mask)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        ts(x, gt_code, gt_mask)
+    torch.cuda.synchronize()
+    print(f"train ms/step {(time.perf_counter() - t0) / a.steps * 1e3:.3f}")
+
+
+if __name__ == "__main__":
+    main()

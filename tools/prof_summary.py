@@ -1,0 +1,89 @@
+#!/usr/bin/env python3
+"""Summarises a tools/prof_round.sh run (gpurun_out/prof_<tag>/) into profiles/:
+
+  profiles/<tag>_infer_kernel_stats.csv   rocprofv3 --kernel-trace --stats, inference (bench.py)
+  profiles/<tag>_train_kernel_stats.csv   same, training step (tools/prof_driver.py --mode train)
+  profiles/<tag>_pmc_traffic.json         HBM bytes per launch per kernel instantiation, from two
+                                          separate --pmc passes (FETCH_SIZE, WRITE_SIZE) over eval
+                                          inference steps, corrected as MI355X_MICROARCH.md §HBM
+                                          prescribes: FETCH_SIZE and WRITE_SIZE are KiB; on gfx950
+                                          FETCH_SIZE counts half the bytes of a wide coalesced read,
+                                          so reads = 2 x FETCH_SIZE x 1024, writes = WRITE_SIZE x 1024.
+
+bench.py reads the json's "by_label" map (keyed by its own kernel labels) for roofline.traffic.
+"""
+import csv
+import glob
+import json
+import os
+import re
+import shutil
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def bench_label(name):
+    """'void zp::k_conv<unsigned short, 4, 4, 4, 3, false>(zp_conv_args)' ->
+    'k_conv<bf16,WC=4,WP=4,NWP=4,ST=3,smallC=0>' (the label bench.py / engine.py use)."""
+    m = re.search(r"k_conv<(unsigned short|float), (\d+), (\d+), (\d+), (\d+), (true|false)>", name)
+    if not m:
+        return None
+    t = "bf16" if m.group(1) == "unsigned short" else "f32"
+    return (f"k_conv<{t},WC={m.group(2)},WP={m.group(3)},NWP={m.group(4)},ST={m.group(5)},"
+            f"smallC={int(m.group(6) == 'true')}>")
+
+
+def one(pattern):
+    f = sorted(glob.glob(pattern, recursive=True))
+    return f[0] if f else None
+
+
+def counters(path, counter):
+    per = defaultdict(list)
+    with open(path) as fh:
+        for r in csv.DictReader(fh):
+            if r["Counter_Name"] != counter:
+                continue
+            per[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+    return per
+
+
+def main(tag="r01"):
+    src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
+    dst = os.path.join(ROOT, "profiles")
+    os.makedirs(dst, exist_ok=True)
+    for leg in ("infer", "train"):
+        f = one(os.path.join(src, leg, "**", "*kernel_stats.csv"))
+        if f:
+            shutil.copy(f, os.path.join(dst, f"{tag}_{leg}_kernel_stats.csv"))
+            print("copied", f)
+    ff = one(os.path.join(src, "pmc_fetch", "**", "*counter_collection.csv"))
+    fw = one(os.path.join(src, "pmc_write", "**", "*counter_collection.csv"))
+    if not (ff and fw):
+        print("no PMC passes found")
+        return
+    fetch, write = counters(ff, "FETCH_SIZE"), counters(fw, "WRITE_SIZE")
+    out = {"source": "tools/prof_round.sh: rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate runs) over "
+                     "tools/prof_driver.py --mode infer --steps 3 --warmup 1 (R34 bs=32 bf16 eval + decode)",
+           "correction": "bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024 (FETCH_SIZE halves wide coalesced "
+                         "reads on gfx950, MI355X_MICROARCH.md HBM section)",
+           "kernels": {}, "by_label": {}}
+    for k in sorted(set(fetch) & set(write)):
+        f, w = fetch[k], write[k]
+        rd = 2.0 * 1024.0 * sum(f) / len(f)
+        wr = 1024.0 * sum(w) / len(w)
+        out["kernels"][k] = {"launches": len(f), "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
+                             "hbm_bytes_per_launch": rd + wr}
+        lab = bench_label(k)
+        if lab:
+            out["by_label"][lab] = round(rd + wr)
+    with open(os.path.join(dst, f"{tag}_pmc_traffic.json"), "w") as fh:
+        json.dump(out, fh, indent=1)
+    for k, v in sorted(out["kernels"].items(), key=lambda kv: -kv[1]["hbm_bytes_per_launch"] * kv[1]["launches"])[:12]:
+        print(f"{v['launches']:5d} {v['hbm_bytes_per_launch'] / 1e6:10.2f} MB/launch  {k[:100]}")
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
