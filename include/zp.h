@@ -147,8 +147,9 @@ int zp_bn_fold(const float* gamma, const float* beta, const float* mean, const f
                const float* conv_bias, float eps, int C, float* scale, float* shift, void* stream);
 /* train: merge the [3][parts][C] partial statistics of zp_conv2d(stats) (count = P, checked),
  * update running stats (momentum, unbiased var; the conv bias, if any, is added to the mean)
- * and emit scale/shift for the apply pass, plus save[2][C] = (mean, invstd) of the raw values. */
-int zp_bn_train_finalize(const float* partials, int parts, int C, long long count, float eps,
+ * and emit scale/shift for the apply pass, plus save[2][C] = (mean, invstd) of the raw values.
+ * partials is scratch: a first merge level overwrites it in place (every 64th part). */
+int zp_bn_train_finalize(float* partials, int parts, int C, long long count, float eps,
                          float momentum, const float* gamma, const float* beta, const float* conv_bias,
                          float* running_mean, float* running_var, int64_t* num_batches_tracked,
                          float* scale, float* shift, float* save, void* stream);

@@ -6,6 +6,7 @@ backward, Adam).  --mode infer: K eval forwards + decode (configs[1]) with NO tr
 calibration pass, so every dispatch of a kernel in the trace belongs to an identical eval step
 (the PMC per-launch averages in profiles/ are taken over exactly those).  Prints ms/step."""
 import argparse
+import json
 import os
 import sys
 import time
@@ -25,6 +26,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--precision", default="bf16")
+    ap.add_argument("--layer-report", default=None)
     ap.add_argument("--mode", default="train", choices=["train", "infer"])
     a = ap.parse_args()
     from zebrapose_amd.model.BinaryCodeNet import BinaryCodeNet_Deeplab
@@ -63,6 +65,23 @@ def main():
     for _ in range(a.warmup):
         ts(x, gt_code, gt_mask)
     torch.cuda.synchronize()
+    if a.layer_report:
+        eng = net.net._engine
+        eng.timing = []
+        ts(x, gt_code, gt_mask)
+        torch.cuda.synchronize()
+        lay = {}
+        for label, e0, e1, flops, kname in eng.timing:
+            d = lay.setdefault(label, [kname, 0.0, 0.0, 0])
+            d[1] += e0.elapsed_time(e1) * 1e3
+            d[2] += flops
+            d[3] += 1
+        eng.timing = None
+        rows = sorted(({"label": k, "kernel": v[0], "n": v[3], "us_total": round(v[1], 1),
+                        "tflops": round(v[2] / v[1] * 1e-6, 1)} for k, v in lay.items()), key=lambda r: -r["us_total"])
+        with open(a.layer_report, "w") as f:
+            json.dump(rows, f, indent=0)
+        print(f"conv+wgrad total {sum(r['us_total'] for r in rows) / 1e3:.2f} ms")
     t0 = time.perf_counter()
     for _ in range(a.steps):
         ts(x, gt_code, gt_mask)

@@ -734,6 +734,285 @@ __global__ void __launch_bounds__(256) k_wgrad(const zp_wgrad_args A, float* __r
     }
 }
 
+// ------------------------------------------------------------------------------------
+// bf16 weight gradient, LDS-DMA version.  Same product and workspace layout as k_wgrad.
+//
+// A workgroup of 8 waves owns a (64*NA output channels) x (64*NB columns) tile; wave
+// (a, b) = (w / NB, w % NB) computes a 64 x 64 block with 4 x 4 v_mfma_f32_16x16x32_bf16.
+// Every K step covers KP consecutive grid points (pixels).  The stage image is NA + NB
+// "panels" of [KP pixel rows][64 channels] (128 B rows): panels 0..NA-1 hold dy channels,
+// panels NA.. hold x columns (tap, channel).  They are filled straight from global memory by
+// buffer_load ... lds (one wave-instruction = 8 rows), STAGES-deep ring, counted vmcnt + raw
+// barrier per step, exactly as k_conv does.
+//
+// The MFMA reduces over pixels, so both operands are read transposed with
+// ds_read_b64_tr_b16: lane 4q+p of 16-lane group g supplies row (8g + q) and columns
+// 4p..4p+3 of a 16-column block and receives one column (4 consecutive pixels).  Chunk
+// swizzle: the 16 B chunk c of row R sits at chunk c ^ s(R), s(R) = 2 * (bit1(R) | bit3(R) << 1)
+// (even, so the chunk pair of a 16-column block stays adjacent): the 8 rows a 32-lane half
+// reads (two groups, rows 8g+q, q < 4) then cover all 64 banks once -- conflict-free.  The
+// LDS-DMA writes are lane-linear, so the swizzle is applied on the per-lane SOURCE chunk.
+//
+// The tap walk is per lane: each lane always loads the same pixel row R of the tile (the
+// instruction -> row-block map is wave-constant), so the grid point (n, gy, gx) advances
+// incrementally by KP per issued step -- no divisions in the loop.
+// ------------------------------------------------------------------------------------
+struct wg_bounds {
+  unsigned x_bytes, dy_bytes[ZP_MAX_SUB];
+};
+
+__device__ __forceinline__ int wg_swz(int r) { return (((r >> 1) & 1) | (((r >> 3) & 1) << 1)) << 1; }
+
+template <int OFF>
+__device__ __forceinline__ uint2 ds_read_tr8(unsigned addr) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset range");
+  uint2 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF) : "memory");
+  return r;
+}
+
+template <int KP, int NA, int NB, int STAGES>
+__global__ void __launch_bounds__(512) k_wgrad_lds(const zp_wgrad_args A, float* __restrict__ ws, int pix_per_split,
+                                                   int col_tiles, int tiles_per_sub, int cols_max,
+                                                   const wg_bounds WB) {
+  static_assert(NA * NB == 8, "8 waves of 64 x 64");
+  static_assert(KP == 32 || KP == 64, "K step");
+  static_assert(STAGES == 2 || STAGES == 3, "ring depth");
+  constexpr int NP = NA + NB;            // panels per stage
+  constexpr int PB = KP * 128;           // panel bytes
+  constexpr int SB = NP * PB;            // stage bytes
+  constexpr int IPP = KP / 8;            // wave-instructions per panel
+  constexpr int NI = NP * IPP;           // wave-instructions per stage
+  constexpr int JPW = (NI + 7) / 8;      // per wave (the last may be idle)
+  static_assert(SB * STAGES <= 160 * 1024, "LDS");
+  __shared__ uint4 lds0[SB / 16];
+  __shared__ uint4 lds1[SB / 16];
+  __shared__ uint4 lds2[STAGES == 3 ? SB / 16 : 1];
+  auto bufp = [&](auto i_c) -> uint4* {
+    constexpr int i = decltype(i_c)::value;
+    if constexpr (i == 0) return lds0;
+    else if constexpr (i == 1) return lds1;
+    else return lds2;
+  };
+
+  // 1-D grid, XCD-aware: workgroups are dispatched round-robin over the 8 XCDs (separate L2s);
+  // remap so that each XCD walks a contiguous range of (split, sub, tile) with the tiles
+  // fastest -- every tile of one split reads the same dy / x pixel rows, which then meet in one
+  // L2 instead of being fetched by all eight.
+  const int total = gridDim.x;
+  const int bid = blockIdx.x;
+  const int lin = (total & 7) ? bid : (bid & 7) * (total >> 3) + (bid >> 3);
+  const int tiles = tiles_per_sub;
+  const int tile = lin % tiles;
+  const int rest = lin / tiles;
+  const int sub = rest % A.nsub;
+  const int split = rest / A.nsub;
+  const auto& S = A.sub[sub];
+  const int cols = S.ntaps * A.Cin;
+  const int ct = tile % col_tiles, cot = tile / col_tiles;
+  const int col0 = ct * 64 * NB, co0 = cot * 64 * NA;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wa = wid / NB, wb = wid % NB;
+  const int GHW = A.GH * A.GW;
+  const int M = A.N * GHW;
+  const int pbeg = split * pix_per_split;
+  const int pend = min(M, pbeg + pix_per_split);
+  const int nK = pend > pbeg ? (pend - pbeg + KP - 1) / KP : 0;
+
+  // ---- staging state of this lane: pixel row R, source chunk of every panel
+  const int rowblk = (KP == 64) ? wid : (wid & 3);
+  // panel of this wave's j-th wave-instruction (instruction q = wid + 8 j, IPP per panel)
+  auto panel_of = [&](int j) { return KP == 64 ? j : 2 * j + ((wid >> 2) & 1); };
+  const int R = rowblk * 8 + (lane >> 3);
+  const int lchunk = (lane & 7) ^ wg_swz(R);
+  const int cout8 = (A.Cout + 7) & ~7;
+  int poff[NP];        // per-panel lane offset (bytes; x panels: relative to the pixel base)
+  int pty[NP], ptx[NP];
+  bool pok[NP];
+#pragma unroll
+  for (int P = 0; P < NP; ++P) {
+    if (P < NA) {
+      const int ch = co0 + 64 * P + 8 * lchunk;
+      pok[P] = ch < cout8;
+      poff[P] = (S.cdy0 + ch) * 2;
+      pty[P] = ptx[P] = 0;
+    } else {
+      const int col = col0 + 64 * (P - NA) + 8 * lchunk;
+      pok[P] = col < cols;
+      const int t = pok[P] ? col / A.Cin : 0;
+      const int ci = col - t * A.Cin;
+      pty[P] = S.ty[t];
+      ptx[P] = S.tx[t];
+      poff[P] = ((pty[P] * A.IW + ptx[P]) * A.ldx + A.cx0 + ci) * 2;
+    }
+  }
+  // grid point of the next step to issue
+  int pn, pgy, pgx;
+  {
+    const int p = min(pbeg + R, M - 1);
+    pn = p / GHW;
+    const int rr = p - pn * GHW;
+    pgy = rr / A.GW;
+    pgx = rr - pgy * A.GW;
+  }
+  int pnext = pbeg + R;
+#if defined(__HIP_DEVICE_COMPILE__)
+  const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)A.x, (short)0, (int)WB.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t drsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)S.dy, (short)0, (int)WB.dy_bytes[sub], 0x00020000);
+#endif
+
+  auto issue = [&](uint4* dst) {
+    const bool pv = pnext < pend;
+    const unsigned dbase =
+        (unsigned)((((pn * S.OH + pgy * S.oys + S.oyo) * S.OW + pgx * S.oxs + S.oxo) * S.lddy) * 2);
+    const int iy0 = pgy * A.sy, ix0 = pgx * A.sx;
+    const int xbase = (((pn * A.IH + iy0) * A.IW + ix0) * A.ldx) * 2;
+    unsigned voff[JPW];
+#pragma unroll
+    for (int j = 0; j < JPW; ++j) {
+      const int P = panel_of(j);  // wave-uniform (compile-time for KP 64)
+      voff[j] = 0x80000000u;
+      if (P < NA) {
+        if (pv && pok[P]) voff[j] = dbase + (unsigned)poff[P];
+      } else if (P < NP) {
+        const int iy = iy0 + pty[P], ix = ix0 + ptx[P];
+        if (pv && pok[P] && (unsigned)iy < (unsigned)A.IH && (unsigned)ix < (unsigned)A.IW)
+          voff[j] = (unsigned)(xbase + poff[P]);
+      }
+    }
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+    for (int j = 0; j < JPW; ++j) {
+      const int P = panel_of(j);
+      if (P >= NP) continue;
+      auto* d = (__attribute__((address_space(3))) void*)((unsigned char*)dst + P * PB + rowblk * 1024);
+      if (P < NA) __builtin_amdgcn_raw_ptr_buffer_load_lds(drsrc, d, 16, voff[j], 0, 0, 0);
+      else __builtin_amdgcn_raw_ptr_buffer_load_lds(xrsrc, d, 16, voff[j], 0, 0, 0);
+    }
+#endif
+    pnext += KP;
+    if (A.GW >= 16) {  // at most KP / 16 row wraps per step: predicated, no loop
+      pgx += KP;
+#pragma unroll
+      for (int it = 0; it < KP / 16; ++it) {
+        if (pgx >= A.GW) {
+          pgx -= A.GW;
+          if (++pgy == A.GH) {
+            pgy = 0;
+            ++pn;
+          }
+        }
+      }
+    } else {  // tiny grids (1x1 image-pool branch): divide
+      const int p = min(pnext, M - 1);
+      pn = p / GHW;
+      const int rr = p - pn * GHW;
+      pgy = rr / A.GW;
+      pgx = rr - pgy * A.GW;
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // fragment read addresses: lane (g, 4q+p) -> row 8g + q, byte 8p of the 16-column block,
+  // 16-column block ii at chunk pair 2*(ii ^ s'), s' = s(R) / 2 (independent of the +4 / +32
+  // row offsets, which are immediates)
+  const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+  const int sh = (((q4 >> 1) & 1) | ((g & 1) << 1));
+  unsigned ra[4], rb[4];
+#pragma unroll
+  for (int ii = 0; ii < 4; ++ii) {
+    const unsigned in_panel = (unsigned)(128 * (8 * g + q4) + 8 * p4 + 32 * (ii ^ sh));
+    ra[ii] = (unsigned)(wa * PB) + in_panel;
+    rb[ii] = (unsigned)((NA + wb) * PB) + in_panel;
+  }
+
+  auto step = [&](auto cur_c, auto nxt_c, int ks) {
+    const bool more = ks + (STAGES - 1) < nK;
+    if (more) issue(bufp(nxt_c));
+    const unsigned cb = lds_addr(bufp(cur_c));
+    unsigned pa[4], pb[4];
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) {
+      pa[ii] = cb + ra[ii];
+      pb[ii] = cb + rb[ii];
+    }
+    static_for<KP / 32>([&](auto s2) {
+      uint4 af[4], bfr[4];
+      static_for<4>([&](auto ii) {
+        const uint2 a0 = ds_read_tr8<s2 * 4096>(pa[ii]);
+        const uint2 a1 = ds_read_tr8<s2 * 4096 + 512>(pa[ii]);
+        const uint2 b0 = ds_read_tr8<s2 * 4096>(pb[ii]);
+        const uint2 b1 = ds_read_tr8<s2 * 4096 + 512>(pb[ii]);
+        af[ii] = make_uint4(a0.x, a0.y, a1.x, a1.y);
+        bfr[ii] = make_uint4(b0.x, b0.y, b1.x, b1.y);
+      });
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) MfmaTraits<bf16_t>::mma(acc[i][j], af[i], bfr[j]);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(0);
+    });
+    if (more) vm_wait<JPW * (STAGES - 2)>();
+    else vm_wait<0>();
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  if (nK > 0) {
+    issue(lds0);
+    if (STAGES == 3 && nK > 1) {
+      issue(lds1);
+      vm_wait<JPW * (STAGES - 2)>();
+    } else {
+      vm_wait<0>();
+    }
+  }
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  if constexpr (STAGES == 3) {
+    for (int ks = 0; ks < nK; ks += 3) {
+      step(I0{}, I2{}, ks);
+      if (ks + 1 >= nK) break;
+      step(I1{}, I0{}, ks + 1);
+      if (ks + 2 >= nK) break;
+      step(I2{}, I1{}, ks + 2);
+    }
+  } else {
+    for (int ks = 0; ks < nK; ks += 2) {
+      step(I0{}, I1{}, ks);
+      if (ks + 1 >= nK) break;
+      step(I1{}, I0{}, ks + 1);
+    }
+  }
+  // partial tile -> ws[((split*nsub + sub)*Cout + co)*cols_max + col]
+  float* W = ws + ((size_t)split * A.nsub + sub) * (size_t)A.Cout * cols_max;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = col0 + wb * 64 + j * 16 + (lane & 15);
+      if (col >= cols) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + wa * 64 + i * 16 + g * 4 + r;
+        if (co < A.Cout) W[(size_t)co * cols_max + col] = acc[i][j][r];
+      }
+    }
+}
+
 // ws (summed over splits) -> dw in the weight's own layout
 __global__ void k_wgrad_reduce(const zp_wgrad_args A, const float* __restrict__ ws, int splits, int cols_max) {
   const int sub = blockIdx.y;
@@ -931,10 +1210,43 @@ static void wgrad_plan(const zp_wgrad_args& a, int* splits, int* col_tiles, int*
   *pix_per = (int)pp;
 }
 
+// bf16: the LDS-DMA kernel (k_wgrad_lds).  Tile 128 co x 256 col (KP 64), or 64 x 512 (KP 32)
+// when Cout <= 64.  One workgroup per CU (144 / 108 KB LDS): aim for ~2 workgroups per CU
+// over the launch, each with >= 16 K steps.  ZP_WGRAD=0 selects the register-staged k_wgrad.
+static bool wgrad_lds(const zp_wgrad_args& a) {
+  static const int v = getenv("ZP_WGRAD") ? env_int("ZP_WGRAD") : 1;
+  return a.dtype == ZP_BF16 && v != 0;
+}
+static void wgrad_plan_lds(const zp_wgrad_args& a, int* splits, int* col_tiles, int* cols_max, int* pix_per) {
+  long M = (long)a.N * a.GH * a.GW;
+  int cm = 0;
+  for (int s = 0; s < a.nsub; ++s) cm = cm > a.sub[s].ntaps * a.Cin ? cm : a.sub[s].ntaps * a.Cin;
+  const bool narrow = a.Cout <= 64;
+  const int tco = narrow ? 64 : 128, tcol = narrow ? 512 : 256, KP = narrow ? 32 : 64;
+  int ct = ceil_div(cm, tcol);
+  int tiles = ct * ceil_div(a.Cout, tco) * a.nsub;
+  long sp = (512 + tiles - 1) / tiles;
+  long maxsp = M / (8 * KP);
+  if (maxsp < 1) maxsp = 1;
+  if (sp > maxsp) sp = maxsp;
+  if (sp > 256) sp = 256;
+  long pp = (M + sp - 1) / sp;
+  pp = (pp + KP - 1) / KP * KP;
+  sp = (M + pp - 1) / pp;
+  // pad the split count so the launch is a multiple of 8 workgroups (the XCD-aware order
+  // needs it); padding splits have an empty pixel range and write zero partials
+  while ((sp * tiles) % 8) ++sp;
+  *splits = (int)sp;
+  *col_tiles = ct;
+  *cols_max = cm;
+  *pix_per = (int)pp;
+}
+
 extern "C" long long zp_conv2d_wgrad_ws_bytes(const zp_wgrad_args* a) {
   if (!a || a->nsub < 1 || a->nsub > ZP_MAX_SUB) return -1;
   int sp, ct, cm, pp;
-  wgrad_plan(*a, &sp, &ct, &cm, &pp);
+  if (wgrad_lds(*a)) wgrad_plan_lds(*a, &sp, &ct, &cm, &pp);
+  else wgrad_plan(*a, &sp, &ct, &cm, &pp);
   return (long long)sp * a->nsub * a->Cout * (long long)cm * 4;
 }
 
@@ -953,13 +1265,35 @@ extern "C" int zp_conv2d_wgrad(const zp_wgrad_args* ap, void* ws, void* stream) 
                  "zp_conv2d_wgrad: dy ld must cover Cout rounded to %d", E);
   }
   int sp, ct, cm, pp;
-  wgrad_plan(a, &sp, &ct, &cm, &pp);
   hipStream_t st = (hipStream_t)stream;
-  dim3 grid(sp, ct * ceil_div(a.Cout, WG_TILE), a.nsub);
-  if (a.dtype == ZP_BF16)
-    hipLaunchKernelGGL(k_wgrad<bf16_t>, grid, dim3(256), 0, st, a, (float*)ws, pp, ct, cm);
-  else
-    hipLaunchKernelGGL(k_wgrad<float>, grid, dim3(256), 0, st, a, (float*)ws, pp, ct, cm);
+  if (wgrad_lds(a)) {
+    wgrad_plan_lds(a, &sp, &ct, &cm, &pp);
+    wg_bounds wb{};
+    const long long xb = (long long)a.N * a.IH * a.IW * a.ldx * 2;
+    ZP_CHECK_ARG(xb < (1ll << 31), "zp_conv2d_wgrad: input %lld B must stay below 2 GiB (split the batch)", xb);
+    wb.x_bytes = (unsigned)xb;
+    for (int s = 0; s < a.nsub; ++s) {
+      const long long db = (long long)a.N * a.sub[s].OH * a.sub[s].OW * a.sub[s].lddy * 2;
+      ZP_CHECK_ARG(db < (1ll << 31), "zp_conv2d_wgrad: dy %lld B must stay below 2 GiB", db);
+      wb.dy_bytes[s] = (unsigned)db;
+    }
+    if (a.Cout <= 64) {
+      const int tiles = ct * ceil_div(a.Cout, 64);
+      hipLaunchKernelGGL((k_wgrad_lds<32, 1, 8, 3>), dim3(sp * a.nsub * tiles), dim3(512), 0, st, a, (float*)ws, pp,
+                         ct, tiles, cm, wb);
+    } else {
+      const int tiles = ct * ceil_div(a.Cout, 128);
+      hipLaunchKernelGGL((k_wgrad_lds<64, 2, 4, 3>), dim3(sp * a.nsub * tiles), dim3(512), 0, st, a, (float*)ws, pp,
+                         ct, tiles, cm, wb);
+    }
+  } else {
+    wgrad_plan(a, &sp, &ct, &cm, &pp);
+    dim3 grid(sp, ct * ceil_div(a.Cout, WG_TILE), a.nsub);
+    if (a.dtype == ZP_BF16)
+      hipLaunchKernelGGL(k_wgrad<bf16_t>, grid, dim3(256), 0, st, a, (float*)ws, pp, ct, cm);
+    else
+      hipLaunchKernelGGL(k_wgrad<float>, grid, dim3(256), 0, st, a, (float*)ws, pp, ct, cm);
+  }
   ZP_LAUNCH_CHECK("zp_conv2d_wgrad");
   long tot = (long)a.Cout * cm;
   int rb = (int)((tot + 255) / 256);

@@ -92,18 +92,20 @@ __global__ void k_bn_fold(const float* g, const float* b, const float* m, const 
   shift[c] = sh;
 }
 
-// block = 32 channels x 8 part lanes
-__global__ void k_bn_train_finalize(const float* __restrict__ part, int parts, int C, long long count, float eps,
-                                    float mom, const float* gamma, const float* beta, const float* bias, float* rm,
-                                    float* rv, int64_t* nbt, float* scale, float* shift, float* save) {
-  // partials: [0] count, [1] mean, [2] M2 (centred) per part; merged with Chan's formula in f64:
-  // n = sum n_k, mean = sum n_k mean_k / n, M2 = sum M2_k + sum n_k (mean_k - mean)^2
+// Level 1 of the statistics merge: block (channel group, j) merges parts [j*R, (j+1)*R) with
+// Chan's formula (f64 inside the block) and writes the merged (count, mean, M2) back in place into
+// part j*R -- only this block reads that range, so the in-place write is race-free.  Level 2
+// (k_bn_train_finalize) then reads every R-th part.  Two levels keep both kernels short: the
+// conv epilogue emits one part per wave-half (8192 parts at 128x128, bs 32).
+constexpr int BN_MERGE_R = 64;
+__global__ void k_bn_stat_merge(float* __restrict__ part, int parts, int C) {
   __shared__ double sh[3][8][33];
   const int cl = threadIdx.x & 31, pl = threadIdx.x >> 5;
   const int c = blockIdx.x * 32 + cl;
+  const int k0 = blockIdx.y * BN_MERGE_R, k1 = min(parts, k0 + BN_MERGE_R);
   double n = 0, s = 0;
   if (c < C)
-    for (int k = pl; k < parts; k += 8) {
+    for (int k = k0 + pl; k < k1; k += 8) {
       double nk = part[(size_t)k * C + c];
       n += nk;
       s += nk * (double)part[((size_t)parts + k) * C + c];
@@ -119,7 +121,48 @@ __global__ void k_bn_train_finalize(const float* __restrict__ part, int parts, i
   const double mean = ntot > 0 ? stot / ntot : 0.0;
   double q = 0;
   if (c < C)
-    for (int k = pl; k < parts; k += 8) {
+    for (int k = k0 + pl; k < k1; k += 8) {
+      double nk = part[(size_t)k * C + c];
+      double dm = (double)part[((size_t)parts + k) * C + c] - mean;
+      q += (double)part[((size_t)2 * parts + k) * C + c] + nk * dm * dm;
+    }
+  sh[2][pl][cl] = q;
+  __syncthreads();  // every read of this range precedes the write-back below
+  if (pl != 0 || c >= C) return;
+  for (int k = 1; k < 8; ++k) q += sh[2][k][cl];
+  part[(size_t)k0 * C + c] = (float)ntot;
+  part[((size_t)parts + k0) * C + c] = (float)mean;
+  part[((size_t)2 * parts + k0) * C + c] = (float)q;
+}
+
+// block = 32 channels x 8 part lanes; reads parts 0, R, 2R, ... (R = stride)
+__global__ void k_bn_train_finalize(const float* __restrict__ part, int parts, int stride, int C, long long count,
+                                    float eps, float mom, const float* gamma, const float* beta, const float* bias,
+                                    float* rm, float* rv, int64_t* nbt, float* scale, float* shift, float* save) {
+  // partials: [0] count, [1] mean, [2] M2 (centred) per part; merged with Chan's formula in f64:
+  // n = sum n_k, mean = sum n_k mean_k / n, M2 = sum M2_k + sum n_k (mean_k - mean)^2
+  __shared__ double sh[3][8][33];
+  const int cl = threadIdx.x & 31, pl = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cl;
+  double n = 0, s = 0;
+  if (c < C)
+    for (int k = pl * stride; k < parts; k += 8 * stride) {
+      double nk = part[(size_t)k * C + c];
+      n += nk;
+      s += nk * (double)part[((size_t)parts + k) * C + c];
+    }
+  sh[0][pl][cl] = n;
+  sh[1][pl][cl] = s;
+  __syncthreads();
+  double ntot = 0, stot = 0;
+  for (int k = 0; k < 8; ++k) {
+    ntot += sh[0][k][cl];
+    stot += sh[1][k][cl];
+  }
+  const double mean = ntot > 0 ? stot / ntot : 0.0;
+  double q = 0;
+  if (c < C)
+    for (int k = pl * stride; k < parts; k += 8 * stride) {
       double nk = part[(size_t)k * C + c];
       double dm = (double)part[((size_t)parts + k) * C + c] - mean;
       q += (double)part[((size_t)2 * parts + k) * C + c] + nk * dm * dm;
@@ -567,15 +610,24 @@ extern "C" int zp_bn_fold(const float* g, const float* b, const float* m, const 
   return ZP_OK;
 }
 
-extern "C" int zp_bn_train_finalize(const float* partials, int parts, int C, long long count, float eps, float momentum,
+extern "C" int zp_bn_train_finalize(float* partials, int parts, int C, long long count, float eps, float momentum,
                                     const float* gamma, const float* beta, const float* conv_bias, float* running_mean,
                                     float* running_var, int64_t* nbt, float* scale, float* shift, float* save,
                                     void* stream) {
   ZP_CHECK_ARG(partials && gamma && beta && running_mean && running_var && scale && shift && save && parts > 0 &&
                    C > 0 && count > 0,
                "zp_bn_train_finalize: bad args");
-  hipLaunchKernelGGL(k_bn_train_finalize, dim3((C + 31) / 32), dim3(256), 0, (hipStream_t)stream, partials, parts, C,
-                     count, eps, momentum, gamma, beta, conv_bias, running_mean, running_var, nbt, scale, shift, save);
+  // the partials buffer is the caller's scratch (zp_conv2d stats): level 1 merges in place
+  int stride = 1;
+  if (parts > 2 * BN_MERGE_R) {
+    hipLaunchKernelGGL(k_bn_stat_merge, dim3((C + 31) / 32, (parts + BN_MERGE_R - 1) / BN_MERGE_R), dim3(256), 0,
+                       (hipStream_t)stream, partials, parts, C);
+    ZP_LAUNCH_CHECK("zp_bn_train_finalize merge");
+    stride = BN_MERGE_R;
+  }
+  hipLaunchKernelGGL(k_bn_train_finalize, dim3((C + 31) / 32), dim3(256), 0, (hipStream_t)stream, partials, parts,
+                     stride, C, count, eps, momentum, gamma, beta, conv_bias, running_mean, running_var, nbt, scale,
+                     shift, save);
   ZP_LAUNCH_CHECK("zp_bn_train_finalize");
   return ZP_OK;
 }

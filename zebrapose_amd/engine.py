@@ -313,6 +313,17 @@ class Engine:
         a.accumulate = 0
         nbytes = L.lib.zp_conv2d_wgrad_ws_bytes(C.byref(a))
         ws = torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=dw.device)
+        if self.timing is not None:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            L.check(L.lib.zp_conv2d_wgrad(C.byref(a), ws.data_ptr(), L.stream_ptr()), "zp_conv2d_wgrad")
+            e1.record()
+            flops = 2.0 * x.B * plan.GH * plan.GW * sum(len(sb.taps) for sb in plan.subs) * x.C * unit.cout
+            geo = (f"wgrad:{x.C}->{unit.cout} taps{max(len(sb.taps) for sb in plan.subs)} "
+                   f"{x.H}x{x.W}->{plan.GH}x{plan.GW}x{a.nsub}")
+            self.timing.append((geo, e0, e1, flops, "k_wgrad+reduce"))
+            return
         L.check(L.lib.zp_conv2d_wgrad(C.byref(a), ws.data_ptr(), L.stream_ptr()), "zp_conv2d_wgrad")
 
     def _dgrad(self, unit, gy: Act, gx: Act):
