@@ -252,6 +252,11 @@ int zp_lut_coarsen(const double* lut64, int old_bits, int new_bits, float* out, 
 /* torch.optim.Adam (no weight decay, amsgrad off) over one flat f32 buffer; step >= 1 */
 int zp_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long long n,
             double lr, double beta1, double beta2, double eps, long long step, void* stream);
+/* the same update for `count` tensors in ceil(count / 40) launches (host arrays of device
+ * pointers; every tensor at the same step), bitwise identical to zp_adam per tensor */
+int zp_adam_multi(int count, float* const* params, const float* const* grads, float* const* exp_avg,
+                  float* const* exp_avg_sq, const long long* numel, double lr, double beta1, double beta2,
+                  double eps, long long step, void* stream);
 
 #ifdef __cplusplus
 }

@@ -219,6 +219,31 @@ def test_fused_adam_matches_torch():
                                rtol=1e-5, atol=1e-7)
 
 
+def test_fused_adam_multi_tensor_matches_torch():
+    """45 tensors (two zp_adam_multi launches), sizes around the 4096-element block chunk,
+    one tensor without a gradient; same op order as torch's single-tensor Adam."""
+    from zebrapose_amd.optim import FusedAdam
+    torch.manual_seed(1)
+    sizes = [1, 7, 4095, 4096, 4097, 12289, 65536 + 3] * 6 + [300, 2, 9]
+    ref = [torch.randn(n, dtype=torch.float32, requires_grad=True) for n in sizes]
+    dev = [r.detach().clone().cuda().requires_grad_(True) for r in ref]
+    o_ref = torch.optim.Adam(ref, lr=3e-4)
+    o = FusedAdam(dev, lr=3e-4)
+    for s in range(3):
+        for i, (r, d) in enumerate(zip(ref, dev)):
+            if i == 5:
+                r.grad, d.grad = None, None
+                continue
+            g = torch.randn(r.shape) * (s + 1)
+            r.grad = g.clone()
+            d.grad = g.cuda()
+        o_ref.step()
+        o.step()
+    torch.cuda.synchronize()
+    for r, d in zip(ref, dev):
+        np.testing.assert_allclose(d.detach().cpu().numpy(), r.detach().numpy(), rtol=1e-6, atol=1e-8)
+
+
 def test_binary_code_helper_dropins(golden):
     """Reference-signature helpers (host arrays in/out, device decode inside)."""
     from zebrapose_amd.binary_code_helper.CNN_output_to_pose import decode_correspondences

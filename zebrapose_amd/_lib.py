@@ -95,6 +95,7 @@ _SIGS = {
     "zp_decode": (i32, [vp, vp, i32, i32, i32, i32, i32, vp, vp, vp, i32, vp, vp, vp, vp, vp, vp]),
     "zp_lut_coarsen": (i32, [vp, i32, i32, vp, vp]),
     "zp_adam": (i32, [vp, vp, vp, vp, i64, f64, f64, f64, f64, i64, vp]),
+    "zp_adam_multi": (i32, [i32, vp, vp, vp, vp, vp, f64, f64, f64, f64, i64, vp]),
 }
 
 

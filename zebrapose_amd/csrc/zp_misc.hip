@@ -237,21 +237,43 @@ __global__ void k_bn_bwd_reduce(const T* __restrict__ dy, int lddy, int cdy0, co
     inv[i] = (x && c < C) ? save[C + c + i] : 0.f;
   }
   if (row < R && c < C) {
-    for (long p = p0 + row; p < p1; p += R) {
+    // U pixels per iteration with all 3U loads issued before any use: the loop is otherwise
+    // latency-bound (one dependent HBM round trip per pixel row)
+    constexpr int U = 4;
+    auto body = [&](long p, const uint4& gd, const uint4& yd, const uint4& xd) {
       float g[N], yy[N], xx[N];
-      V16<T>::load(dy + p * lddy + cdy0 + c, g);
+      V16<T>::load((const T*)&gd, g);
       if (relu) {
-        V16<T>::load(y + p * ldy + cy0 + c, yy);
+        V16<T>::load((const T*)&yd, yy);
 #pragma unroll
         for (int i = 0; i < N; ++i) g[i] = yy[i] > 0.f ? g[i] : 0.f;
       }
       if (x) {
-        V16<T>::load(x + p * C + c, xx);
+        V16<T>::load((const T*)&xd, xx);
 #pragma unroll
         for (int i = 0; i < N; ++i) sgx[i] += g[i] * (xx[i] - mean[i]) * inv[i];
       }
 #pragma unroll
       for (int i = 0; i < N; ++i) sg[i] += g[i];
+    };
+    long p = p0 + row;
+    for (; p + (U - 1) * R < p1; p += U * R) {
+      uint4 gd[U], yd[U], xd[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long pp = p + u * R;
+        gd[u] = *(const uint4*)(dy + pp * lddy + cdy0 + c);
+        yd[u] = relu ? *(const uint4*)(y + pp * ldy + cy0 + c) : make_uint4(0, 0, 0, 0);
+        xd[u] = x ? *(const uint4*)(x + pp * C + c) : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) body(p + u * R, gd[u], yd[u], xd[u]);
+    }
+    for (; p < p1; p += R) {
+      const uint4 gd = *(const uint4*)(dy + p * lddy + cdy0 + c);
+      const uint4 yd = relu ? *(const uint4*)(y + p * ldy + cy0 + c) : make_uint4(0, 0, 0, 0);
+      const uint4 xd = x ? *(const uint4*)(x + p * C + c) : make_uint4(0, 0, 0, 0);
+      body(p, gd, yd, xd);
     }
   }
 #pragma unroll
@@ -277,13 +299,15 @@ __global__ void k_bn_bwd_reduce(const T* __restrict__ dy, int lddy, int cdy0, co
 }
 
 // totals over parts -> part[0][parts][c], part[1][parts][c]; dgamma / dbeta
-__global__ void k_bn_bwd_totals(float* __restrict__ part, int parts, int C, float* dgamma, float* dbeta, int accumulate) {
-  __shared__ double sh[2][8][33];
+// block = 32 channels x 32 part lanes (1024 threads)
+__global__ void __launch_bounds__(1024) k_bn_bwd_totals(float* __restrict__ part, int parts, int C, float* dgamma,
+                                                        float* dbeta, int accumulate) {
+  __shared__ double sh[2][32][33];
   const int cl = threadIdx.x & 31, pl = threadIdx.x >> 5;
   const int c = blockIdx.x * 32 + cl;
   double s = 0, q = 0;
   if (c < C)
-    for (int k = pl; k < parts; k += 8) {
+    for (int k = pl; k < parts; k += 32) {
       s += part[(size_t)k * C + c];
       q += part[((size_t)parts + 1 + k) * C + c];
     }
@@ -291,7 +315,7 @@ __global__ void k_bn_bwd_totals(float* __restrict__ part, int parts, int C, floa
   sh[1][pl][cl] = q;
   __syncthreads();
   if (pl != 0 || c >= C) return;
-  for (int k = 1; k < 8; ++k) {
+  for (int k = 1; k < 32; ++k) {
     s += sh[0][k][cl];
     q += sh[1][k][cl];
   }
@@ -563,6 +587,50 @@ __global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float
   }
 }
 
+// multi-tensor Adam: one launch updates up to ADAM_MT tensors; the tensor of a block comes from
+// the prefix sums of per-tensor block counts (ADAM_CHUNK elements per block)
+constexpr int ADAM_MT = 40;
+constexpr int ADAM_CHUNK = 4096;
+struct AdamTable {
+  float* p[ADAM_MT];
+  const float* g[ADAM_MT];
+  float* m[ADAM_MT];
+  float* v[ADAM_MT];
+  long long n[ADAM_MT];
+  int blk0[ADAM_MT + 1];
+  int count;
+};
+
+__global__ void __launch_bounds__(256) k_adam_multi(const AdamTable T, float lr_bc1, float w1, float b2, float w2,
+                                                    float bc2_sqrt, float eps) {
+  const int b = blockIdx.x;
+  int lo = 0, hi = T.count - 1;  // last t with blk0[t] <= b
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (T.blk0[mid] <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  const int t = lo;
+  const long long e0 = (long long)(b - T.blk0[t]) * ADAM_CHUNK;
+  const long long e1 = min(T.n[t], e0 + ADAM_CHUNK);
+  float* __restrict__ p = T.p[t];
+  const float* __restrict__ g = T.g[t];
+  float* __restrict__ m = T.m[t];
+  float* __restrict__ v = T.v[t];
+  for (long long e = e0 + threadIdx.x; e < e1; e += 256) {
+    // identical op sequence to k_adam (torch.optim.Adam single-tensor order)
+    const float gg = g[e];
+    float mm = m[e];
+    mm = fmaf(w1, __fsub_rn(gg, mm), mm);
+    float vv = __fmul_rn(v[e], b2);
+    vv = __fadd_rn(vv, __fmul_rn(__fmul_rn(w2, gg), gg));
+    m[e] = mm;
+    v[e] = vv;
+    const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(vv), bc2_sqrt), eps);
+    p[e] = __fadd_rn(p[e], __fmul_rn(-lr_bc1, __fdiv_rn(mm, denom)));
+  }
+}
+
 }  // namespace zp
 
 using namespace zp;
@@ -674,7 +742,7 @@ extern "C" int zp_bn_bwd_reduce(const void* dy, int lddy, int cdy0, const void* 
     hipLaunchKernelGGL(k_bn_bwd_reduce<float>, grid, dim3(256), 0, st, (const float*)dy, lddy, cdy0, (const float*)y,
                        ldy, cy0, (const float*)x, (long)P, C, save, relu, partials, parts, cgroups);
   ZP_LAUNCH_CHECK("zp_bn_bwd_reduce");
-  hipLaunchKernelGGL(k_bn_bwd_totals, dim3((C + 31) / 32), dim3(256), 0, st, partials, parts, C, dgamma, dbeta,
+  hipLaunchKernelGGL(k_bn_bwd_totals, dim3((C + 31) / 32), dim3(1024), 0, st, partials, parts, C, dgamma, dbeta,
                      accumulate);
   ZP_LAUNCH_CHECK("zp_bn_bwd_reduce totals");
   return ZP_OK;
@@ -842,5 +910,40 @@ extern "C" int zp_adam(float* param, const float* grad, float* exp_avg, float* e
                      exp_avg_sq, (long)n, (float)(lr / bc1), (float)(1.0 - beta1), (float)beta2,
                      (float)(1.0 - beta2), (float)sqrt(bc2), (float)eps);
   ZP_LAUNCH_CHECK("zp_adam");
+  return ZP_OK;
+}
+
+extern "C" int zp_adam_multi(int count, float* const* params, const float* const* grads, float* const* exp_avg,
+                             float* const* exp_avg_sq, const long long* numel, double lr, double beta1, double beta2,
+                             double eps, long long step, void* stream) {
+  ZP_CHECK_ARG(count >= 0 && (count == 0 || (params && grads && exp_avg && exp_avg_sq && numel)) && step >= 1,
+               "zp_adam_multi: bad args");
+  const double bc1 = 1.0 - pow(beta1, (double)step);
+  const double bc2 = 1.0 - pow(beta2, (double)step);
+  for (int t0 = 0; t0 < count; t0 += ADAM_MT) {
+    AdamTable T{};
+    int nb = 0;
+    T.count = 0;
+    for (int t = t0; t < count && T.count < ADAM_MT; ++t) {
+      ZP_CHECK_ARG(params[t] && grads[t] && exp_avg[t] && exp_avg_sq[t] && numel[t] >= 0,
+                   "zp_adam_multi: tensor %d", t);
+      if (numel[t] == 0) continue;
+      const int k = T.count++;
+      T.p[k] = params[t];
+      T.g[k] = grads[t];
+      T.m[k] = exp_avg[t];
+      T.v[k] = exp_avg_sq[t];
+      T.n[k] = numel[t];
+      T.blk0[k] = nb;
+      const long long blocks = (numel[t] + ADAM_CHUNK - 1) / ADAM_CHUNK;
+      ZP_CHECK_ARG(nb + blocks < (1ll << 30), "zp_adam_multi: too many elements");
+      nb += (int)blocks;
+    }
+    T.blk0[T.count] = nb;
+    if (nb == 0) continue;
+    hipLaunchKernelGGL(k_adam_multi, dim3(nb), dim3(256), 0, (hipStream_t)stream, T, (float)(lr / bc1),
+                       (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)sqrt(bc2), (float)eps);
+    ZP_LAUNCH_CHECK("zp_adam_multi");
+  }
   return ZP_OK;
 }

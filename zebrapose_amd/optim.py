@@ -5,6 +5,8 @@ State dict layout matches torch.optim.Adam ('step', 'exp_avg', 'exp_avg_sq' per 
 checkpoints stay interchangeable (utils_v2.py:15-23)."""
 from __future__ import annotations
 
+import ctypes as C
+
 import torch
 
 from . import _lib as L
@@ -18,10 +20,13 @@ class FusedAdam(torch.optim.Optimizer):
 
     @torch.no_grad()
     def step(self, closure=None):
+        """All parameters of a group that share a step count go through one zp_adam_multi call
+        (ceil(n / 40) launches instead of one launch per parameter)."""
         loss = closure() if closure is not None else None
         st = L.stream_ptr()
         for group in self.param_groups:
             b1, b2 = group["betas"]
+            by_step = {}
             for p in group["params"]:
                 if p.grad is None:
                     continue
@@ -33,11 +38,17 @@ class FusedAdam(torch.optim.Optimizer):
                     state["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     state["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                 state["step"] += 1
-                step = int(state["step"].item())
-                L.call("zp_adam", p.data_ptr(), p.grad.data_ptr(), state["exp_avg"].data_ptr(),
-                       state["exp_avg_sq"].data_ptr(), p.numel(), float(group["lr"]), float(b1), float(b2),
+                by_step.setdefault(int(state["step"].item()), []).append(p)
+            for step, ps in by_step.items():
+                n = len(ps)
+                arr = C.c_void_p * n
+                L.call("zp_adam_multi", n, arr(*[p.data_ptr() for p in ps]), arr(*[p.grad.data_ptr() for p in ps]),
+                       arr(*[self.state[p]["exp_avg"].data_ptr() for p in ps]),
+                       arr(*[self.state[p]["exp_avg_sq"].data_ptr() for p in ps]),
+                       (C.c_longlong * n)(*[p.numel() for p in ps]), float(group["lr"]), float(b1), float(b2),
                        float(group["eps"]), step, st)
                 # the kernel wrote p in place behind autograd's back: bump its version counter so
                 # version-keyed caches (packed eval weights in the engine) see the update
-                torch.autograd.graph.increment_version(p)
+                for p in ps:
+                    torch.autograd.graph.increment_version(p)
         return loss
