@@ -116,6 +116,18 @@ int zp_pack_weight(const float* src, int d0, int d1, int kh, int kw, int transpo
                    const int* ky, const int* kx, int cstride, int dtype, void* dst, int rows_pad,
                    int k_pad, void* stream);
 
+/* Many zp_pack_weight jobs in one launch (training repacks every conv's weights once per
+ * optimizer step).  `jobs` and `prefix` are DEVICE arrays: prefix[i] = sum of rows_pad*k_pad of
+ * jobs before i (prefix[n] = total elements).  Same element mapping as zp_pack_weight. */
+typedef struct zp_pack_job {
+  const float* src;
+  void* dst;
+  int d0, d1, kh, kw, transposed, ntaps, cstride, rows_pad, k_pad, dtype;
+  signed char ky[ZP_MAX_TAPS], kx[ZP_MAX_TAPS];
+} zp_pack_job;
+int zp_pack_weight_multi(int n, const zp_pack_job* jobs, const long long* prefix, long long total,
+                         void* stream);
+
 /* ---- weight gradient ------------------------------------------------------------------
  * dw[co][ci][ky][kx] (f32, layout of the conv's own weight; transposed_w=1 for ConvT's
  * [ci][co][kh][kw]) = sum over grid points and taps of dy[out pixel][co] * x[in pixel][ci],

@@ -38,6 +38,7 @@ def test_struct_layout():
     assert ctypes.sizeof(_lib.ConvSub) % 8 == 0
     assert _lib.ConvArgs.sub.offset % 8 == 0
     assert ctypes.sizeof(_lib.ConvArgs) == _lib.ConvArgs.sub.offset + 4 * ctypes.sizeof(_lib.ConvSub)
+    assert ctypes.sizeof(_lib.PackJob) == 16 + 10 * 4 + 2 * 64  # zp_pack_job (include/zp.h)
 
 
 def test_host_side_validation_without_gpu():

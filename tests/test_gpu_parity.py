@@ -239,7 +239,12 @@ def test_fused_adam_multi_tensor_matches_torch():
             d.grad = g.cuda()
         o_ref.step()
         o.step()
+        if s == 1:  # checkpoint round trip mid-run (utils_v2 saves optimizer_state_dict)
+            sd = o.state_dict()
+            o = FusedAdam(dev, lr=3e-4)
+            o.load_state_dict(sd)
     torch.cuda.synchronize()
+    assert float(o.state_dict()["state"][0]["step"]) == 3.0
     for r, d in zip(ref, dev):
         np.testing.assert_allclose(d.detach().cpu().numpy(), r.detach().numpy(), rtol=1e-6, atol=1e-8)
 

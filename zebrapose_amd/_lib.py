@@ -55,6 +55,12 @@ class WgradArgs(C.Structure):
                 ("nsub", i32), ("sub", WgradSub * MAX_SUB), ("dw", vp), ("accumulate", i32)]
 
 
+class PackJob(C.Structure):
+    _fields_ = [("src", vp), ("dst", vp), ("d0", i32), ("d1", i32), ("kh", i32), ("kw", i32),
+                ("transposed", i32), ("ntaps", i32), ("cstride", i32), ("rows_pad", i32), ("k_pad", i32),
+                ("dtype", i32), ("ky", C.c_byte * MAX_TAPS), ("kx", C.c_byte * MAX_TAPS)]
+
+
 # name -> (restype, argtypes)
 _SIGS = {
     "zp_abi_version": (i32, []),
@@ -95,6 +101,7 @@ _SIGS = {
     "zp_decode": (i32, [vp, vp, i32, i32, i32, i32, i32, vp, vp, vp, i32, vp, vp, vp, vp, vp, vp]),
     "zp_lut_coarsen": (i32, [vp, i32, i32, vp, vp]),
     "zp_adam": (i32, [vp, vp, vp, vp, i64, f64, f64, f64, f64, i64, vp]),
+    "zp_pack_weight_multi": (i32, [i32, vp, vp, i64, vp]),
     "zp_adam_multi": (i32, [i32, vp, vp, vp, vp, vp, f64, f64, f64, f64, i64, vp]),
 }
 

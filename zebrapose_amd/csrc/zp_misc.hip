@@ -78,6 +78,35 @@ __global__ void k_pack(const PackArgs a) {
   }
 }
 
+// one launch for many pack jobs: element e -> job by binary search over the element prefix
+__global__ void k_pack_multi(const zp_pack_job* __restrict__ jobs, const long long* __restrict__ prefix, int n,
+                             long long total) {
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (prefix[mid] <= e) lo = mid;
+      else hi = mid - 1;
+    }
+    const zp_pack_job& a = jobs[lo];
+    const long long le = e - prefix[lo];
+    const int r = (int)(le / a.k_pad), k = (int)(le - (long long)r * a.k_pad);
+    const int rows = a.transposed ? a.d1 : a.d0;
+    const int chans = a.transposed ? a.d0 : a.d1;
+    const int t = k / a.cstride, c = k - t * a.cstride;
+    float v = 0.f;
+    if (r < rows && t < a.ntaps && c < chans) {
+      const int ky = a.ky[t], kx = a.kx[t];
+      const size_t idx = a.transposed ? (((size_t)c * a.d1 + r) * a.kh + ky) * a.kw + kx
+                                      : (((size_t)r * a.d1 + c) * a.kh + ky) * a.kw + kx;
+      v = a.src[idx];
+    }
+    if (a.dtype == ZP_BF16) ((bf16_t*)a.dst)[le] = f2bf(v);
+    else ((float*)a.dst)[le] = v;
+  }
+}
+
 // ------------------------------------------------------------------ batch norm
 __global__ void k_bn_fold(const float* g, const float* b, const float* m, const float* v, const float* bias, float eps,
                           int C, float* scale, float* shift) {
@@ -666,6 +695,16 @@ extern "C" int zp_pack_weight(const float* src, int d0, int d1, int kh, int kw, 
   }
   ZP_BY_DTYPE(dtype, k_pack, dim3(grid_for((long)rows_pad * k_pad)), dim3(256), (hipStream_t)stream, a);
   ZP_LAUNCH_CHECK("zp_pack_weight");
+  return ZP_OK;
+}
+
+extern "C" int zp_pack_weight_multi(int n, const zp_pack_job* jobs, const long long* prefix, long long total,
+                                    void* stream) {
+  ZP_CHECK_ARG(n >= 0 && total >= 0 && (n == 0 || (jobs && prefix)), "zp_pack_weight_multi: bad args");
+  if (n == 0 || total == 0) return ZP_OK;
+  hipLaunchKernelGGL(k_pack_multi, dim3(grid_for(total, 256, 16384)), dim3(256), 0, (hipStream_t)stream, jobs, prefix,
+                     n, total);
+  ZP_LAUNCH_CHECK("zp_pack_weight_multi");
   return ZP_OK;
 }
 

@@ -100,6 +100,8 @@ class Engine:
         self.dtype = dtype
         self.dt = L.dtype_code(dtype)
         self._packed = {}
+        self._jobs = []  # (cache key, weight, PackJob) of every cached packing, for _prepack
+        self._job_table = None
         self._folds = {}
         self._fold_epoch = 0
         self.timing = None  # optional list of (label, start_event, end_event) for conv launches
@@ -107,9 +109,13 @@ class Engine:
     # ------------------------------------------------------------------ weight / BN caches
     def invalidate(self):
         self._packed.clear()
+        self._jobs = []
+        self._job_table = None
         self._folds.clear()
 
-    def _pack(self, unit, sub, transposed, cstride, k_pad, rows, tag, cache):
+    def _pack(self, unit, sub, transposed, cstride, k_pad, rows, tag, cache=True):
+        """Packed weights of one (conv, sub-problem, role), cached on the weight's version counter.
+        Every packing is also recorded as a job of the batched repack (_prepack)."""
         w = unit.conv.weight
         key = (id(unit.conv), tag, tuple(sub.taps), cstride, k_pad, self.dt)
         ver = (w._version, w.data_ptr())
@@ -117,14 +123,49 @@ class Engine:
         if hit is not None and hit[0] == ver:
             return hit[1]
         d0, d1 = w.shape[0], w.shape[1]
-        out = torch.empty((rows, k_pad), dtype=self.dtype, device=w.device)
+        out = hit[1] if hit is not None and hit[1].shape == (rows, k_pad) else \
+            torch.empty((rows, k_pad), dtype=self.dtype, device=w.device)
         ky = [t[0] for t in sub.taps]
         kx = [t[1] for t in sub.taps]
         L.call("zp_pack_weight", w.data_ptr(), d0, d1, w.shape[2], w.shape[3], transposed, len(sub.taps),
                _i32arr(ky), _i32arr(kx), cstride, self.dt, out.data_ptr(), rows, k_pad, L.stream_ptr())
         if cache:
+            if key not in self._packed:
+                j = L.PackJob()
+                j.src, j.dst = w.data_ptr(), out.data_ptr()
+                j.d0, j.d1, j.kh, j.kw = d0, d1, w.shape[2], w.shape[3]
+                j.transposed, j.ntaps, j.cstride, j.rows_pad, j.k_pad, j.dtype = \
+                    transposed, len(sub.taps), cstride, rows, k_pad, self.dt
+                for t, (a, b) in enumerate(zip(ky, kx)):
+                    j.ky[t], j.kx[t] = a, b
+                self._jobs.append((key, w, j))
+                self._job_table = None
             self._packed[key] = (ver, out)
         return out
+
+    def _prepack(self, device):
+        """Batched repack (training): once the optimizer has changed the weights, every recorded
+        packing job runs in ONE zp_pack_weight_multi launch and the cache is revalidated, so the
+        forward / backward below hit the cache instead of launching ~110 pack kernels."""
+        if not self._jobs:
+            return
+        if all(self._packed[k][0] == (w._version, w.data_ptr()) for k, w, _ in self._jobs):
+            return
+        if self._job_table is None or any(self._packed[k][1].data_ptr() != j.dst or w.data_ptr() != j.src
+                                          for k, w, j in self._jobs):
+            for k, w, j in self._jobs:
+                j.src, j.dst = w.data_ptr(), self._packed[k][1].data_ptr()
+            n = len(self._jobs)
+            arr = (L.PackJob * n)(*[j for _, _, j in self._jobs])
+            table = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(device)
+            pre = [0]
+            for _, _, j in self._jobs:
+                pre.append(pre[-1] + j.rows_pad * j.k_pad)
+            self._job_table = (table, torch.tensor(pre, dtype=torch.int64).to(device), n, pre[-1])
+        table, prefix, n, total = self._job_table
+        L.call("zp_pack_weight_multi", n, table.data_ptr(), prefix.data_ptr(), total, L.stream_ptr())
+        for key, w, _ in self._jobs:
+            self._packed[key] = ((w._version, w.data_ptr()), self._packed[key][1])
 
     def _fold(self, unit):
         bn, bias = unit.bn, unit.conv.bias
@@ -221,7 +262,7 @@ class Engine:
         OH, OW = unit.out_hw(x.H, x.W)
         assert (out.H, out.W, out.C) == (OH, OW, unit.cout), ((out.H, out.W, out.C), (OH, OW, unit.cout))
         train = tape is not None
-        ws, kp, rows = self._fwd_weights(unit, plan, cache=not train)
+        ws, kp, rows = self._fwd_weights(unit, plan, cache=True)
         small = self._small(unit.cin, unit.k, unit.d, unit.p)
         if not train or unit.bn is None:
             scale, shift = self._fold(unit)
@@ -277,7 +318,7 @@ class Engine:
     def head_fwd(self, unit, x: Act, mask, code, tape):
         plan = unit.fwd_plan(x.H, x.W)
         OH, OW = unit.out_hw(x.H, x.W)
-        ws, kp, rows = self._fwd_weights(unit, plan, cache=tape is None)
+        ws, kp, rows = self._fwd_weights(unit, plan, cache=True)
         outs = [(mask.data_ptr(), 0, 0, OH, OW, None, unit.conv.bias, code.data_ptr())]
         self._conv(x, plan, unit.cout, ws, kp, rows, outs, None, False, out_mode=L.ZP_OUT_HEAD_NCHW,
                    small=self._small(unit.cin, unit.k, unit.d, unit.p), label="head")
@@ -333,7 +374,7 @@ class Engine:
         kp = max(self._kpad(len(sb.taps), cin_l) for sb in plan.subs)
         rows = L.lib.zp_conv_rows_pad(unit.cin)
         tr = 0 if unit.kind == "convT" else 1
-        ws = [self._pack(unit, sb, tr, cin_l, kp, rows, "dgrad", False) for sb in plan.subs]
+        ws = [self._pack(unit, sb, tr, cin_l, kp, rows, "dgrad") for sb in plan.subs]
         outs = [(gx.ptr, gx.ld, gx.c0, gx.H, gx.W, None, None, None)] * len(plan.subs)
         small = self._small(cin_l, unit.k, -unit.d, -unit.p) if unit.kind == "conv" and unit.s == 1 else None
         if cin_l < _KE[self.dt]:
@@ -409,6 +450,7 @@ class Engine:
         def new(h, w, c):
             return Act(torch.empty((B, h, w, c), dtype=dt, device=dev))
 
+        self._prepack(dev)
         st = L.stream_ptr()
         xin = new(H, W, 8)
         L.call("zp_nchw_to_nhwc", x.data_ptr(), B, 3, H, W, 8, self.dt, xin.ptr, st)

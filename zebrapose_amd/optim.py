@@ -18,15 +18,22 @@ class FusedAdam(torch.optim.Optimizer):
             raise NotImplementedError("weight decay is not used by the ZebraPose trainers")
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=0.0))
 
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        self._steps = {}
+
     @torch.no_grad()
     def step(self, closure=None):
         """All parameters of a group that share a step count go through one zp_adam_multi call
-        (ceil(n / 40) launches instead of one launch per parameter)."""
+        (ceil(n / 40) launches instead of one launch per parameter).  The per-parameter 'step'
+        tensors of torch's state layout are advanced with one foreach op; a host-side int mirror
+        (self._steps) avoids a .item() per parameter."""
         loss = closure() if closure is not None else None
         st = L.stream_ptr()
+        steps = self.__dict__.setdefault("_steps", {})
         for group in self.param_groups:
             b1, b2 = group["betas"]
-            by_step = {}
+            live, step_t = [], []
             for p in group["params"]:
                 if p.grad is None:
                     continue
@@ -37,8 +44,18 @@ class FusedAdam(torch.optim.Optimizer):
                     state["step"] = torch.tensor(0.0)
                     state["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     state["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                state["step"] += 1
-                by_step.setdefault(int(state["step"].item()), []).append(p)
+                    steps[p] = 0
+                elif p not in steps:
+                    steps[p] = int(state["step"].item())
+                steps[p] += 1
+                live.append(p)
+                step_t.append(state["step"])
+            if not live:
+                continue
+            torch._foreach_add_(step_t, 1.0)
+            by_step = {}
+            for p in live:
+                by_step.setdefault(steps[p], []).append(p)
             for step, ps in by_step.items():
                 n = len(ps)
                 arr = C.c_void_p * n
