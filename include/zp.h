@@ -106,6 +106,8 @@ int zp_conv_rows_pad(int Cout);
 int zp_conv2d_grid(const zp_conv_args* a);
 /* number of partial-sum slots `stats` needs: 2 * grid_x * nsub */
 int zp_conv2d_stat_parts(const zp_conv_args* a);
+/* launch configuration zp_conv2d picks: cout tile, pixel tile, LDS ring depth */
+int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* stages);
 
 /* Pack an f32 weight tensor src[d0][d1][kh][kw] into dst[rows_pad][k_pad] (dtype), taps
  * (ky[t], kx[t]), t < ntaps:

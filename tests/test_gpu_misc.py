@@ -1,0 +1,51 @@
+"""Memory-bound helper kernels against torch on the same values: global average pool (ASPP image
+branch, aspp.py:94), its backward pieces (per-channel H*W sums, broadcast back over H*W) and the
+NCHW f32 -> NHWC input conversion, in the vectorised (16 B) and scalar (odd channel slice) forms."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("C,ld,c0", [(512, 512, 0), (256, 1280, 1024), (20, 24, 2)])
+def test_avgpool_sum_broadcast(gpu, prec, C, ld, c0):
+    from zebrapose_amd import _lib as L
+    dt = torch.float32 if prec == "fp32" else torch.bfloat16
+    dc = L.dtype_code(dt)
+    torch.manual_seed(0)
+    B, H, W = 3, 17, 32
+    buf = torch.randn(B, H, W, ld).to(dt)
+    x = buf[..., c0:c0 + C].float()
+    d = buf.to(gpu)
+    out = torch.empty(B, C, dtype=dt, device=gpu)
+    L.call("zp_global_avgpool", d.data_ptr(), B, H, W, ld, c0, C, dc, out.data_ptr(), L.stream_ptr())
+    want = x.double().mean(dim=(1, 2)).float().to(dt).float()
+    assert torch.equal(out.float().cpu(), want)
+    L.call("zp_sum_hw", d.data_ptr(), B, H, W, ld, c0, C, dc, out.data_ptr(), L.stream_ptr())
+    want = x.sum(dim=(1, 2))
+    got = out.float().cpu()
+    tol = 1e-5 if prec == "fp32" else 1e-2
+    assert ((got - want).abs() <= tol * (want.abs() + 1)).all()
+    src = torch.randn(B, C).to(dt).to(gpu)
+    y = torch.zeros(B, H, W, ld, dtype=dt, device=gpu)
+    L.call("zp_broadcast_hw", src.data_ptr(), B, C, dc, y.data_ptr(), H, W, ld, c0, L.stream_ptr())
+    yc = y.cpu()
+    assert torch.equal(yc[..., c0:c0 + C], src.cpu()[:, None, None, :].expand(B, H, W, C))
+    assert not yc[..., :c0].any() and not yc[..., c0 + C:].any()
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("cpad", [8, 5])
+def test_nchw_to_nhwc(gpu, prec, cpad):
+    from zebrapose_amd import _lib as L
+    dt = torch.float32 if prec == "fp32" else torch.bfloat16
+    if prec == "bf16" and cpad == 5:
+        pytest.skip("the network pads to a full 16 B vector")
+    torch.manual_seed(1)
+    x = torch.randn(2, 3, 9, 14)
+    y = torch.full((2, 9, 14, cpad), 7.0, dtype=dt, device=gpu)
+    L.call("zp_nchw_to_nhwc", x.to(gpu).data_ptr(), 2, 3, 9, 14, cpad, L.dtype_code(dt), y.data_ptr(), L.stream_ptr())
+    want = torch.zeros(2, 9, 14, cpad)
+    want[..., :3] = x.permute(0, 2, 3, 1)
+    assert torch.equal(y.cpu().float(), want.to(dt).float())

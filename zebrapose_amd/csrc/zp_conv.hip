@@ -96,6 +96,10 @@ __global__ void __launch_bounds__(128 * NWP) k_conv(const zp_conv_args A, const 
   constexpr int G = (TC + TP) / 8;            // 8-row groups per K step
   static_assert(G % NW == 0, "row groups must split evenly over the waves");
   constexpr int GPW = G / NW;                 // groups per wave
+  // the first WPW groups of every wave are weight rows, the rest activation rows (group g = wid + NW*i
+  // is a weight group iff i < WPW): compile-time, so per-pixel state exists only for pixel groups
+  static_assert((TC / 8) % NW == 0, "weight groups must split evenly over the waves");
+  constexpr int WPW = TC / 8 / NW;
   __shared__ uint4 lds0[(TC + TP) * 8];
   __shared__ uint4 lds1[(TC + TP) * 8];
   __shared__ uint4 lds2[STAGES == 3 ? (TC + TP) * 8 : 1];
@@ -134,6 +138,7 @@ __global__ void __launch_bounds__(128 * NWP) k_conv(const zp_conv_args A, const 
   bool gvalid[GPW];
 #pragma unroll
   for (int i = 0; i < GPW; ++i) {
+    if (i < WPW) continue;
     const int r = (wid + NW * i) * 8 + lrow;
     int m = p0 + (r - TC);
     gvalid[i] = r >= TC && m < M;
@@ -160,6 +165,7 @@ __global__ void __launch_bounds__(128 * NWP) k_conv(const zp_conv_args A, const 
   unsigned abase[GPW], ymask[GPW], xmask[GPW];
 #pragma unroll
   for (int i = 0; i < GPW; ++i) {
+    if (i < WPW) continue;
     const int y0 = gpix_y[i], x0 = gpix_x[i];
     abase[i] = (unsigned)(((((long)gpix_n[i] * A.IH + y0) * A.IW + x0) * A.ldx + A.cx0 + csrc * E) * sizeof(T));
     unsigned ym = 0, xm = 0;
@@ -199,7 +205,7 @@ __global__ void __launch_bounds__(128 * NWP) k_conv(const zp_conv_args A, const 
         const int g = wid + NW * i;
         const int r = g * 8 + lrow;
         const void* src;
-        if (g * 8 < TC) {
+        if (i < WPW) {
           src = Wt + (size_t)(c0 + r) * A.k_pad + kw_off + csrc * E;
         } else {
           int iy = gpix_y[i] + ty, ix = gpix_x[i] + tx;
@@ -224,7 +230,7 @@ __global__ void __launch_bounds__(128 * NWP) k_conv(const zp_conv_args A, const 
 #pragma unroll
       for (int i = 0; i < GPW; ++i) {
         const int g = wid + NW * i;
-        if (g * 8 < TC) {  // wave-uniform: groups never straddle the weight / activation boundary
+        if (i < WPW) {  // weight group (compile-time)
           voff[i] = wbase + (unsigned)(NW * i * 8) * (unsigned)(A.k_pad * sizeof(T));
         } else {
           const bool ok = (ymask[i] >> w_tyi) & (xmask[i] >> w_txi) & 1u;
@@ -236,7 +242,7 @@ __global__ void __launch_bounds__(128 * NWP) k_conv(const zp_conv_args A, const 
       for (int i = 0; i < GPW; ++i) {
         const int g = wid + NW * i;
         auto* d = (__attribute__((address_space(3))) void*)&dst[g * 64];
-        if (g * 8 < TC)
+        if (i < WPW)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(wrsrc, d, 16, voff[i], ks * chunk_b, 0, 0);
         else
           __builtin_amdgcn_raw_ptr_buffer_load_lds(xrsrc, d, 16, voff[i], 0, 0, 0);
@@ -1045,14 +1051,42 @@ static void launch_conv(const zp_conv_args& a, const conv_taps& tg, int gx, int 
   hipLaunchKernelGGL((k_conv<T, WC, 4, NWP, STAGES, SMALLC>), dim3(gx, gy, a.nsub), dim3(128 * NWP), 0, st,
                      a, tg, conv_flags());
 }
-
-static int conv_tc(int cout) { return cout > 64 ? 128 : (cout > 32 ? 64 : 32); }
+// 256 x 256 tile (bf16 only): 64 KB per LDS stage, so a 2-deep ring
+template <typename T>
+static void launch_conv_tc256(const zp_conv_args& a, const conv_taps& tg, int gx, int gy, hipStream_t st) {
+  if constexpr (std::is_same<T, bf16_t>::value) launch_conv<T, 8, 4, 2, false>(a, tg, gx, gy, st);
+}
 
 // Tuning overrides for sweeps (read once): ZP_CONV_TP=128|256 forces the pixel tile,
-// ZP_CONV_STAGES=2|3 forces the LDS ring depth.  0 = heuristic.
+// ZP_CONV_STAGES=2|3 forces the LDS ring depth, ZP_CONV_TC256=0 disables the 256-channel tile.
+// 0 = heuristic.
 static int env_int(const char* name) {
   const char* v = getenv(name);
   return v ? atoi(v) : 0;
+}
+static bool conv_tc256_enabled() {
+  static const bool v = getenv("ZP_CONV_TC256") ? env_int("ZP_CONV_TC256") != 0 : true;
+  return v;
+}
+
+// cout tile: 256 (the whole layer: activations are staged once per pixel tile instead of once per
+// 128-channel tile, and 64 MFMAs per wave per LDS step instead of 32) for bf16 layers with
+// Cout % 256 == 0; else 128 / 64 / 32.
+// Measured (R34 bs 32, profiles/r01_conv_sweep.md): a win when the launch still has >= 512
+// workgroups of 256 pixels (64x64 / 128x128 layers, the 64x64 transposed-conv phases: 1.1-1.2x),
+// a loss on 32x32 layers (128 workgroups for 256 CUs) and on the ASPP launch, whose four
+// sub-problems (1 vs 9 taps) are too unbalanced for 512 large tiles.
+static int conv_tc(const zp_conv_args& a) {
+  if (a.dtype == ZP_BF16 && a.Cout % 256 == 0 && a.Cin >= 64 && conv_tc256_enabled()) {
+    const long M = (long)a.N * a.GH * a.GW;
+    int tmin = ZP_MAX_TAPS, tmax = 0;
+    for (int s = 0; s < a.nsub; ++s) {
+      tmin = a.sub[s].ntaps < tmin ? a.sub[s].ntaps : tmin;
+      tmax = a.sub[s].ntaps > tmax ? a.sub[s].ntaps : tmax;
+    }
+    if (ceil_div(M, 256) * (long)a.nsub >= 512 && tmax <= 4 * tmin) return 256;
+  }
+  return a.Cout > 64 ? 128 : (a.Cout > 32 ? 64 : 32);
 }
 static int conv_tp_override() {
   static const int v = env_int("ZP_CONV_TP");
@@ -1110,7 +1144,7 @@ extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
                "zp_conv2d: Cin %d must be a multiple of %d (or < %d and a multiple of %d)", a.Cin, KE, KE, E);
   ZP_CHECK_ARG(a.ldx >= a.cx0 + a.Cin && a.cx0 % E == 0 && a.ldx % E == 0, "zp_conv2d: bad ldx/cx0");
   ZP_CHECK_ARG(a.k_pad % KE == 0, "zp_conv2d: k_pad %d not a multiple of %d", a.k_pad, KE);
-  ZP_CHECK_ARG(a.w_rows % conv_tc(a.Cout) == 0 && a.w_rows >= a.Cout, "zp_conv2d: w_rows %d", a.w_rows);
+  ZP_CHECK_ARG(a.w_rows % conv_tc(a) == 0 && a.w_rows >= a.Cout, "zp_conv2d: w_rows %d", a.w_rows);
   ZP_CHECK_ARG(a.out_mode >= 0 && a.out_mode <= 2, "zp_conv2d: out_mode");
   ZP_CHECK_ARG(!a.stats || (!a.res && !a.relu && a.out_mode != ZP_OUT_HEAD_NCHW && !a.sub[0].scale &&
                             !a.sub[0].shift),
@@ -1158,7 +1192,7 @@ extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
       ZP_CHECK_ARG(grid, "zp_conv2d: sub %d taps must form a (row x column) grid of at most 32 x 32, rows outer", s);
     }
   }
-  const int tc = conv_tc(a.Cout);
+  const int tc = conv_tc(a);
   const int gx = zp_conv2d_grid(&a), gy = ceil_div(a.Cout, tc);
   hipStream_t st = (hipStream_t)stream;
   const int nwp = conv_tp(a) / 64;
@@ -1169,7 +1203,9 @@ extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
 #define ZP_DISPATCH_NWP(T, WC, NWP)                                      \
   if (stages == 3) { ZP_DISPATCH_ST(T, WC, NWP, 3) } else { ZP_DISPATCH_ST(T, WC, NWP, 2) }
 #define ZP_DISPATCH(T)                                                   \
-  if (tc == 128) {                                                       \
+  if (tc == 256) {                                                       \
+    launch_conv_tc256<T>(a, tg, gx, gy, st);                             \
+  } else if (tc == 128) {                                                \
     if (nwp == 4) { ZP_DISPATCH_NWP(T, 4, 4) } else { ZP_DISPATCH_NWP(T, 4, 2) } \
   } else if (tc == 64) {                                                 \
     if (nwp == 4) { ZP_DISPATCH_NWP(T, 2, 4) } else { ZP_DISPATCH_NWP(T, 2, 2) } \
@@ -1306,4 +1342,13 @@ extern "C" int zp_conv2d_wgrad(const zp_wgrad_args* ap, void* ws, void* stream) 
 extern "C" int zp_conv2d_stat_parts(const zp_conv_args* a) {
   if (!a) return 0;
   return (conv_tp(*a) / 64) * zp_conv2d_grid(a) * a->nsub;
+}
+
+/* launch configuration zp_conv2d picks for these args (for kernel labels in reports) */
+extern "C" int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* stages) {
+  ZP_CHECK_ARG(a && tc && tp && stages, "zp_conv2d_config: null args");
+  *tc = conv_tc(*a);
+  *tp = conv_tp(*a);
+  *stages = *tc == 256 ? 2 : conv_stages(*tp / 64);
+  return ZP_OK;
 }

@@ -4,6 +4,7 @@
 #include <stdarg.h>
 #include <stdio.h>
 #include <math.h>
+#include <type_traits>
 #include "zp_common.h"
 
 namespace zp {
@@ -404,11 +405,21 @@ __global__ void k_bn_bwd_apply(const T* __restrict__ dy, int lddy, int cdy0, con
 // ------------------------------------------------------------------ layout / pooling
 template <typename T>
 __global__ void k_nchw_to_nhwc(const float* __restrict__ x, int B, int C, int H, int W, int cpad, T* __restrict__ y) {
+  constexpr int N = V16<T>::N;
   const long HW = (long)H * W, total = (long)B * HW;
   for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
     long b = e / HW, s = e - b * HW;
     T* o = y + e * cpad;
-    for (int c = 0; c < cpad; ++c) o[c] = Elem<T>::cvt(c < C ? x[(b * C + c) * HW + s] : 0.f);
+    if (cpad % N == 0) {  // one 16 B store per N channels (the network's input: 3 -> 8 bf16 = one store)
+      for (int c0 = 0; c0 < cpad; c0 += N) {
+        float v[N];
+#pragma unroll
+        for (int i = 0; i < N; ++i) v[i] = c0 + i < C ? x[(b * C + c0 + i) * HW + s] : 0.f;
+        V16<T>::store(o + c0, v);
+      }
+    } else {
+      for (int c = 0; c < cpad; ++c) o[c] = Elem<T>::cvt(c < C ? x[(b * C + c) * HW + s] : 0.f);
+    }
   }
 }
 
@@ -523,6 +534,60 @@ __device__ __forceinline__ ACC sum_hw_block(const T* __restrict__ x, long HW, in
   return red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
 }
 
+// Vectorised form (C, c0, ld multiples of the 16 B vector width N): block = (image b, 64
+// channels), 256 threads = (64 / N) chunk lanes x (256 N / 64) pixel lanes, 16 B loads; the pixel
+// lanes are combined through LDS in a fixed order (deterministic).  MODE 0: mean over H*W in
+// double, converted to T (CPU adaptive_avg_pool2d accumulates in double); MODE 1: float sum -> T.
+template <typename T, int MODE>
+__global__ void __launch_bounds__(256) k_hw_reduce_vec(const T* __restrict__ x, int H, int W, int ld, int c0, int C,
+                                                       T* __restrict__ y) {
+  constexpr int N = V16<T>::N;
+  constexpr int CL = 64 / N, PL = 256 / CL;
+  using ACC = typename std::conditional<MODE == 0, double, float>::type;
+  __shared__ ACC red[PL][64];
+  const int b = blockIdx.y;
+  const long HW = (long)H * W;
+  const int cl = threadIdx.x % CL, pl = threadIdx.x / CL;
+  const int c = blockIdx.x * 64 + cl * N;
+  ACC s[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) s[i] = 0;
+  if (c < C) {
+    const T* base = x + (size_t)b * HW * ld + c0 + c;
+    long p = pl;
+    for (; p + 3 * PL < HW; p += 4 * PL) {
+      uint4 u[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) u[k] = *(const uint4*)(base + (p + k * PL) * ld);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float v[N];
+        V16<T>::load((const T*)&u[k], v);
+#pragma unroll
+        for (int i = 0; i < N; ++i) s[i] += (ACC)v[i];
+      }
+    }
+    for (; p < HW; p += PL) {
+      float v[N];
+      V16<T>::load(base + p * ld, v);
+#pragma unroll
+      for (int i = 0; i < N; ++i) s[i] += (ACC)v[i];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) red[pl][cl * N + i] = s[i];
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int cc = blockIdx.x * 64 + threadIdx.x;
+    ACC t = 0;
+    for (int k = 0; k < PL; ++k) t += red[k][threadIdx.x];
+    if (cc < C) {
+      if (MODE == 0) y[(size_t)b * C + cc] = Elem<T>::cvt((float)((double)t / (double)HW));
+      else y[(size_t)b * C + cc] = Elem<T>::cvt((float)t);
+    }
+  }
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) k_avgpool(const T* __restrict__ x, int H, int W, int ldx, int cx0, int C,
                                                  T* __restrict__ y) {
@@ -541,6 +606,22 @@ __global__ void __launch_bounds__(256) k_sum_hw(const T* __restrict__ dy, int H,
   float s = sum_hw_block<T, float>(dy, (long)H * W, lddy, cdy0, C, b);
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   if (threadIdx.x < 64 && c < C) out[(size_t)b * C + c] = Elem<T>::cvt(s);
+}
+
+// y[b, p, cy0 + c] = src[b, c] for every pixel, one 16 B store per N channels (C, ldy, cy0
+// multiples of N)
+template <typename T>
+__global__ void k_broadcast_vec(const T* __restrict__ src, int B, int C, T* __restrict__ y, int H, int W, int ldy,
+                                int cy0) {
+  constexpr int N = V16<T>::N;
+  const int CV = C / N;
+  const long HW = (long)H * W, total = (long)B * HW * CV;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const long pix = e / CV;
+    const int c = (int)(e - pix * CV) * N;
+    const long b = pix / HW;
+    *(uint4*)(y + pix * ldy + cy0 + c) = *(const uint4*)(src + b * C + c);
+  }
 }
 
 template <typename T>
@@ -860,7 +941,17 @@ extern "C" int zp_global_avgpool(const void* x, int B, int H, int W, int ldx, in
                                  void* stream) {
   ZP_DTYPE_CHECK("zp_global_avgpool", dtype);
   ZP_CHECK_ARG(x && y && B > 0 && H > 0 && W > 0 && C > 0, "zp_global_avgpool: bad args");
-  ZP_TLAUNCH(dtype, k_avgpool, dim3((C + 63) / 64, B), (hipStream_t)stream, (const T*)x, H, W, ldx, cx0, C, (T*)y);
+  const int N = dtype == ZP_BF16 ? 8 : 4;
+  if (C % N == 0 && cx0 % N == 0 && ldx % N == 0) {
+    if (dtype == ZP_BF16)
+      hipLaunchKernelGGL((k_hw_reduce_vec<bf16_t, 0>), dim3((C + 63) / 64, B), dim3(256), 0, (hipStream_t)stream,
+                         (const bf16_t*)x, H, W, ldx, cx0, C, (bf16_t*)y);
+    else
+      hipLaunchKernelGGL((k_hw_reduce_vec<float, 0>), dim3((C + 63) / 64, B), dim3(256), 0, (hipStream_t)stream,
+                         (const float*)x, H, W, ldx, cx0, C, (float*)y);
+  } else {
+    ZP_TLAUNCH(dtype, k_avgpool, dim3((C + 63) / 64, B), (hipStream_t)stream, (const T*)x, H, W, ldx, cx0, C, (T*)y);
+  }
   ZP_LAUNCH_CHECK("zp_global_avgpool");
   return ZP_OK;
 }
@@ -870,8 +961,14 @@ extern "C" int zp_broadcast_hw(const void* src, int B, int C, int dtype, void* y
   ZP_DTYPE_CHECK("zp_broadcast_hw", dtype);
   ZP_CHECK_ARG(src && y && B > 0 && C > 0, "zp_broadcast_hw: bad args");
   long total = (long)B * H * W * C;
-  ZP_TLAUNCH(dtype, k_broadcast, dim3(grid_for(total)), (hipStream_t)stream, (const T*)src, B, C, 1.f, (T*)y, H, W,
-             ldy, cy0, 0, 0);
+  const int N = dtype == ZP_BF16 ? 8 : 4;
+  if (C % N == 0 && ldy % N == 0 && cy0 % N == 0) {
+    ZP_TLAUNCH(dtype, k_broadcast_vec, dim3(grid_for(total / N)), (hipStream_t)stream, (const T*)src, B, C, (T*)y, H,
+               W, ldy, cy0);
+  } else {
+    ZP_TLAUNCH(dtype, k_broadcast, dim3(grid_for(total)), (hipStream_t)stream, (const T*)src, B, C, 1.f, (T*)y, H, W,
+               ldy, cy0, 0, 0);
+  }
   ZP_LAUNCH_CHECK("zp_broadcast_hw");
   return ZP_OK;
 }
@@ -880,8 +977,18 @@ extern "C" int zp_sum_hw(const void* dy, int B, int H, int W, int lddy, int cdy0
                          void* stream) {
   ZP_DTYPE_CHECK("zp_sum_hw", dtype);
   ZP_CHECK_ARG(dy && out && B > 0 && C > 0, "zp_sum_hw: bad args");
-  ZP_TLAUNCH(dtype, k_sum_hw, dim3((C + 63) / 64, B), (hipStream_t)stream, (const T*)dy, H, W, lddy, cdy0, C,
-             (T*)out);
+  const int N = dtype == ZP_BF16 ? 8 : 4;
+  if (C % N == 0 && cdy0 % N == 0 && lddy % N == 0) {
+    if (dtype == ZP_BF16)
+      hipLaunchKernelGGL((k_hw_reduce_vec<bf16_t, 1>), dim3((C + 63) / 64, B), dim3(256), 0, (hipStream_t)stream,
+                         (const bf16_t*)dy, H, W, lddy, cdy0, C, (bf16_t*)out);
+    else
+      hipLaunchKernelGGL((k_hw_reduce_vec<float, 1>), dim3((C + 63) / 64, B), dim3(256), 0, (hipStream_t)stream,
+                         (const float*)dy, H, W, lddy, cdy0, C, (float*)out);
+  } else {
+    ZP_TLAUNCH(dtype, k_sum_hw, dim3((C + 63) / 64, B), (hipStream_t)stream, (const T*)dy, H, W, lddy, cdy0, C,
+               (T*)out);
+  }
   ZP_LAUNCH_CHECK("zp_sum_hw");
   return ZP_OK;
 }

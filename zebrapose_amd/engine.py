@@ -23,7 +23,6 @@ input's gradient buffer).
 from __future__ import annotations
 
 import ctypes as C
-import os
 import weakref
 
 import torch
@@ -227,14 +226,11 @@ class Engine:
             L.check(L.lib.zp_conv2d(C.byref(a), st), "zp_conv2d")
             e1.record()
             flops = 2.0 * x.B * plan.GH * plan.GW * sum(len(sb.taps) for sb in plan.subs) * x.C * cout
-            wc = 4 if cout > 64 else (2 if cout > 32 else 1)
-            nwp = 4 if L.lib.zp_conv2d_stat_parts(C.byref(a)) == 4 * L.lib.zp_conv2d_grid(C.byref(a)) * a.nsub \
-                else 2
-            # rocprofv3 name: k_conv<T, WC, WP=4, NWP, STAGES, smallC> (stage rule: zp_conv.hip conv_stages)
-            st_ov = int(os.environ.get("ZP_CONV_STAGES", "0") or 0)
-            stages = st_ov if st_ov in (2, 3) else 3
-            kname = (f"k_conv<{'bf16' if self.dt == L.ZP_BF16 else 'f32'},WC={wc},WP=4,NWP={nwp},"
-                     f"ST={stages},smallC={int(x.C < _KE[self.dt])}>")
+            tc, tp, stages = C.c_int(), C.c_int(), C.c_int()
+            L.call("zp_conv2d_config", C.byref(a), C.byref(tc), C.byref(tp), C.byref(stages))
+            # rocprofv3 name: k_conv<T, WC = tc / 32, WP = 4, NWP = tp / 64, STAGES, smallC>
+            kname = (f"k_conv<{'bf16' if self.dt == L.ZP_BF16 else 'f32'},WC={tc.value // 32},WP=4,"
+                     f"NWP={tp.value // 64},ST={stages.value},smallC={int(x.C < _KE[self.dt])}>")
             geo = (f"{label}:{x.C}->{cout} taps{max(len(sb.taps) for sb in plan.subs)} "
                    f"{x.H}x{x.W}->{plan.GH}x{plan.GW}x{a.nsub}")
             self.timing.append((geo, e0, e1, flops, kname))
