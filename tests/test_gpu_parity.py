@@ -57,6 +57,28 @@ def test_forward_fp32_matches_reference(net_and_state, golden, fixture, xkey, mk
         assert amb <= 0.01 * ref.size  # the ambiguous band itself (reported, tiny)
 
 
+def test_r50_forward_fp32_matches_reference(golden):
+    """ResNet50_OS8 + ASPP_50 (340M parameters; Bottleneck stem/layer1/layer2, 1024/2048-channel
+    BasicBlock layer4/5, 2048-channel ASPP, 512-channel up2 input) through the HIP path, fp32 mode,
+    against the reference's own 64x64 forward (oracle/capture_fixtures.py capture_network(50))."""
+    from oracle import ref_cpu
+    from zebrapose_amd.model.BinaryCodeNet import BinaryCodeNet_Deeplab
+    f = golden("r50_fwd64.npz")
+    sd = ref_cpu.synthetic_state(50, 16, 0, dict(golden("r50_bn_buffers.npz")))
+    net = BinaryCodeNet_Deeplab(50, 16, 2, concat=True, output_kernel_size=1, precision="fp32")
+    net.load_state_dict(sd)
+    net = net.cuda().eval()
+    with torch.no_grad():
+        m, c = net(torch.from_numpy(f["fwd64_x"]).cuda())
+    m, c = m.cpu().numpy(), c.cpu().numpy()
+    for got, ref in ((m, f["fwd64_mask"]), (c, f["fwd64_code"])):
+        np.testing.assert_allclose(got, ref, atol=1e-3, rtol=1e-4)
+        bad, amb = _bits_check(got, ref, 1e-3)
+        assert bad == 0 and amb <= 0.01 * ref.size
+    del net
+    torch.cuda.empty_cache()
+
+
 def test_forward_bf16_within_conditioning_band(net_and_state, golden):
     net, _ = net_and_state
     net.set_precision("bf16")

@@ -99,3 +99,20 @@ def test_decode_matches_reference(golden, ignore_bit):
         assert np.array_equal(ids, d[f"ib{ignore_bit}_b{b}_ids"])
         assert np.array_equal(p2d, d[f"ib{ignore_bit}_b{b}_p2d"])
         assert np.array_equal(p3d, d[f"ib{ignore_bit}_b{b}_p3d"])
+
+
+def test_r50_state_spec_and_forward_match_reference(golden):
+    """ResNet50_OS8 + ASPP_50 variant (resnet.py:206-227, aspp.py:117-225):
+    key layout (488 keys, 144 aliases) and 64x64 forward against the captured reference."""
+    import os
+    from tests.conftest import GOLDEN
+    want = open(os.path.join(GOLDEN, "state_keys_r50.txt")).read().splitlines()
+    entries, aliases = ref_cpu.state_spec(50, 16)
+    assert [f"{k} {list(s)}" for k, s, _ in entries] == want
+    assert len(aliases) == 144
+    f = golden("r50_fwd64.npz")
+    sd = ref_cpu.synthetic_state(50, 16, 0, dict(golden("r50_bn_buffers.npz")))
+    with torch.no_grad():
+        m, c = ref_cpu.forward(sd, torch.from_numpy(f["fwd64_x"]), 50)
+    np.testing.assert_allclose(m.numpy(), f["fwd64_mask"], atol=1e-5, rtol=0)
+    np.testing.assert_allclose(c.numpy(), f["fwd64_code"], atol=1e-5, rtol=0)
