@@ -108,6 +108,9 @@ int zp_conv2d_grid(const zp_conv_args* a);
 int zp_conv2d_stat_parts(const zp_conv_args* a);
 /* launch configuration zp_conv2d picks: cout tile, pixel tile, LDS ring depth */
 int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* stages);
+/* runtime tuning knob (tests / sweeps): key 0 = minimum workgroup count for the 256-channel
+ * tile (default 512).  Returns the previous value, -1 for an unknown key. */
+int zp_conv_tuning(int key, int value);
 
 /* Pack an f32 weight tensor src[d0][d1][kh][kw] into dst[rows_pad][k_pad] (dtype), taps
  * (ky[t], kx[t]), t < ntaps:

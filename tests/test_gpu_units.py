@@ -57,10 +57,20 @@ def _ref_unit(kind, conv, bn, x, res, relu, train, s, p, d):
     return y, (xx, w, b, g, be), (rm, rv)
 
 
+@pytest.fixture(params=["tc-auto", "tc256"])
+def tile_mode(request):
+    """'tc256' forces the 256-channel conv tile (normally only for launches of >= 512 workgroups)
+    onto these small cases so that its code path is checked too."""
+    from zebrapose_amd import _lib as L
+    old = L.lib.zp_conv_tuning(0, 0 if request.param == "tc256" else 512)
+    yield request.param
+    L.lib.zp_conv_tuning(0, old)
+
+
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
 @pytest.mark.parametrize("geom", GEOMS, ids=[f"{g[0]}{g[1]}-{g[2]}k{g[3]}s{g[4]}d{g[6]}" for g in GEOMS])
 @pytest.mark.parametrize("train", [False, True])
-def test_unit(gpu, geom, prec, train):
+def test_unit(gpu, geom, prec, train, tile_mode):
     from zebrapose_amd.engine import Engine, Unit, Act, Tape
     kind, cin, cout, k, s, p, d, bias, H = geom
     torch.manual_seed(0)

@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""Single-layer conv timing (forward, eval epilogue) for kernel experiments:
+    python tools/conv_micro.py --cin 256 --cout 256 --hw 128 --batch 32 [--k 3 --d 1] [--iters 20]
+Prints us / launch and TFLOP/s (algorithmic: 2 * pixels * taps * Cin * Cout).  Kernel switches
+come from the environment (ZP_CONV_FLAGS, ZP_CONV_TC256, ZP_CONV_TP, ZP_CONV_STAGES)."""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ.setdefault("ZP_QUIET", "1")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cin", type=int, default=256)
+    ap.add_argument("--cout", type=int, default=256)
+    ap.add_argument("--hw", type=int, default=128)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--k", type=int, default=3)
+    ap.add_argument("--d", type=int, default=1)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--tag", default="")
+    ap.add_argument("--relu-input", action="store_true", help="post-ReLU activations (half zeros)")
+    ap.add_argument("--zero", action="store_true", help="all-zero activations")
+    a = ap.parse_args()
+    from zebrapose_amd.engine import Engine, Unit, Act
+    from zebrapose_amd.model import layers as LY
+    dev = torch.device("cuda", 0)
+    conv = LY.Conv2d(a.cin, a.cout, a.k, 1, a.d * (a.k // 2), a.d, bias=False).to(dev)
+    bn = LY.BatchNorm2d(a.cout).to(dev).eval()
+    unit = Unit(conv, bn, relu=True)
+    eng = Engine(torch.nn.Module(), torch.bfloat16)
+    xt = torch.randn(a.batch, a.hw, a.hw, a.cin, device=dev)
+    if a.relu_input:
+        xt = xt.clamp(min=0)
+    if a.zero:
+        xt.zero_()
+    x = Act(xt.bfloat16())
+    y = Act(torch.empty(a.batch, a.hw, a.hw, a.cout, device=dev, dtype=torch.bfloat16))
+    for _ in range(3):
+        eng.unit_fwd(unit, x, y, None)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(a.iters):
+        eng.unit_fwd(unit, x, y, None)
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / a.iters
+    fl = 2.0 * a.batch * a.hw * a.hw * a.k * a.k * a.cin * a.cout
+    print(f"{a.tag} {a.cin}->{a.cout} k{a.k} d{a.d} {a.hw}x{a.hw} b{a.batch}: {us:8.1f} us  {fl / us * 1e-6:7.1f} TFLOP/s")
+
+
+if __name__ == "__main__":
+    main()

@@ -103,6 +103,7 @@ _SIGS = {
     "zp_adam": (i32, [vp, vp, vp, vp, i64, f64, f64, f64, f64, i64, vp]),
     "zp_pack_weight_multi": (i32, [i32, vp, vp, i64, vp]),
     "zp_conv2d_config": (i32, [vp, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)]),
+    "zp_conv_tuning": (i32, [i32, i32]),
     "zp_adam_multi": (i32, [i32, vp, vp, vp, vp, vp, f64, f64, f64, f64, i64, vp]),
 }
 

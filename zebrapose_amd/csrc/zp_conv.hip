@@ -1068,6 +1068,8 @@ static bool conv_tc256_enabled() {
   static const bool v = getenv("ZP_CONV_TC256") ? env_int("ZP_CONV_TC256") != 0 : true;
   return v;
 }
+// runtime tuning knobs (zp_conv_tuning): minimum workgroup count for the 256-channel tile
+static int g_tc256_min_blocks = 512;
 
 // cout tile: 256 (the whole layer: activations are staged once per pixel tile instead of once per
 // 128-channel tile, and 64 MFMAs per wave per LDS step instead of 32) for bf16 layers with
@@ -1084,7 +1086,7 @@ static int conv_tc(const zp_conv_args& a) {
       tmin = a.sub[s].ntaps < tmin ? a.sub[s].ntaps : tmin;
       tmax = a.sub[s].ntaps > tmax ? a.sub[s].ntaps : tmax;
     }
-    if (ceil_div(M, 256) * (long)a.nsub >= 512 && tmax <= 4 * tmin) return 256;
+    if (ceil_div(M, 256) * (long)a.nsub >= g_tc256_min_blocks && tmax <= 4 * tmin) return 256;
   }
   return a.Cout > 64 ? 128 : (a.Cout > 32 ? 64 : 32);
 }
@@ -1246,8 +1248,8 @@ static void wgrad_plan(const zp_wgrad_args& a, int* splits, int* col_tiles, int*
   *pix_per = (int)pp;
 }
 
-// bf16: the LDS-DMA kernel (k_wgrad_lds).  Tile 128 co x 256 col (KP 64), or 64 x 512 (KP 32)
-// when Cout <= 64.  One workgroup per CU (144 / 108 KB LDS): aim for ~2 workgroups per CU
+// bf16: the LDS-DMA kernel (k_wgrad_lds).  Tile 128 co x 256 col (3 stages), or 64 x 512 (2 stages)
+// when Cout <= 64; KP 64.  One workgroup per CU (144 KB LDS): aim for ~2 workgroups per CU
 // over the launch, each with >= 16 K steps.  ZP_WGRAD=0 selects the register-staged k_wgrad.
 static bool wgrad_lds(const zp_wgrad_args& a) {
   static const int v = getenv("ZP_WGRAD") ? env_int("ZP_WGRAD") : 1;
@@ -1258,7 +1260,7 @@ static void wgrad_plan_lds(const zp_wgrad_args& a, int* splits, int* col_tiles, 
   int cm = 0;
   for (int s = 0; s < a.nsub; ++s) cm = cm > a.sub[s].ntaps * a.Cin ? cm : a.sub[s].ntaps * a.Cin;
   const bool narrow = a.Cout <= 64;
-  const int tco = narrow ? 64 : 128, tcol = narrow ? 512 : 256, KP = narrow ? 32 : 64;
+  const int tco = narrow ? 64 : 128, tcol = narrow ? 512 : 256, KP = 64;
   int ct = ceil_div(cm, tcol);
   int tiles = ct * ceil_div(a.Cout, tco) * a.nsub;
   long sp = (512 + tiles - 1) / tiles;
@@ -1315,7 +1317,7 @@ extern "C" int zp_conv2d_wgrad(const zp_wgrad_args* ap, void* ws, void* stream) 
     }
     if (a.Cout <= 64) {
       const int tiles = ct * ceil_div(a.Cout, 64);
-      hipLaunchKernelGGL((k_wgrad_lds<32, 1, 8, 3>), dim3(sp * a.nsub * tiles), dim3(512), 0, st, a, (float*)ws, pp,
+      hipLaunchKernelGGL((k_wgrad_lds<64, 1, 8, 2>), dim3(sp * a.nsub * tiles), dim3(512), 0, st, a, (float*)ws, pp,
                          ct, tiles, cm, wb);
     } else {
       const int tiles = ct * ceil_div(a.Cout, 128);
@@ -1351,4 +1353,15 @@ extern "C" int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* st
   *tp = conv_tp(*a);
   *stages = *tc == 256 ? 2 : conv_stages(*tp / 64);
   return ZP_OK;
+}
+
+/* runtime tuning knobs (tests / sweeps).  key 0: minimum workgroups for the 256-channel conv tile
+ * (default 512).  Returns the previous value. */
+extern "C" int zp_conv_tuning(int key, int value) {
+  if (key == 0) {
+    const int old = g_tc256_min_blocks;
+    g_tc256_min_blocks = value;
+    return old;
+  }
+  return -1;
 }
