@@ -14,6 +14,12 @@
 #include <type_traits>
 #include "zp_common.h"
 
+// Diagnostic ablation builds only (tools/build_ablation.sh -> libzp_abl<N>.so; wrong results):
+// ZP_ABL 1 = k_conv issues no LDS-DMA, 2 = k_conv runs no MFMA.  The product build is ZP_ABL 0.
+#ifndef ZP_ABL
+#define ZP_ABL 0
+#endif
+
 namespace zp {
 
 template <typename T> struct MfmaTraits;
@@ -289,7 +295,9 @@ __global__ void __launch_bounds__(128 * NWP) k_conv(const zp_conv_args A, const 
     const bool more = ks + (STAGES - 1) < nK;
     // next stage's DMA first (its tap offsets come from scalar loads, whose lgkmcnt wait must
     // not also wait for this step's fragment reads)
-    if (more) issue(ks + (STAGES - 1), bufp(nxt_c));
+    if constexpr (ZP_ABL != 1) {
+      if (more) issue(ks + (STAGES - 1), bufp(nxt_c));
+    }
     // fragment reads as inline asm: hipcc's waitcnt pass cannot prove across the loop back-edge
     // that they miss the in-flight LDS-DMA buffers and would put a vmcnt(0) in front of them
     const unsigned cb = lds_addr(bufp(cur_c));
@@ -312,12 +320,19 @@ __global__ void __launch_bounds__(128 * NWP) k_conv(const zp_conv_args A, const 
       __builtin_amdgcn_sched_barrier(0);
     }
     if (flags & 4) __builtin_amdgcn_s_setprio(1);
+    if constexpr (ZP_ABL != 2) {
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
+      for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-      for (int i = 0; i < WC; ++i)
+        for (int i = 0; i < WC; ++i)
 #pragma unroll
-        for (int j = 0; j < WP; ++j) MfmaTraits<T>::mma(acc[i][j], af[s2][i], bfr[s2][j]);
+          for (int j = 0; j < WP; ++j) MfmaTraits<T>::mma(acc[i][j], af[s2][i], bfr[s2][j]);
+    } else {
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int i = 0; i < WC; ++i) acc[i][0][0] += __uint_as_float(af[s2][i].x ^ bfr[s2][0].y);
+    }
     __builtin_amdgcn_sched_barrier(0);  // keep the MFMAs in front of the wait + barrier
     if (flags & 4) __builtin_amdgcn_s_setprio(0);
     if (!pingpong) {
