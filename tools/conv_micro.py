@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--tag", default="")
     ap.add_argument("--relu-input", action="store_true", help="post-ReLU activations (half zeros)")
     ap.add_argument("--zero", action="store_true", help="all-zero activations")
+    ap.add_argument("--wgrad", action="store_true", help="time the weight gradient instead")
     a = ap.parse_args()
     from zebrapose_amd.engine import Engine, Unit, Act
     from zebrapose_amd.model import layers as LY
@@ -40,18 +41,28 @@ def main():
         xt.zero_()
     x = Act(xt.bfloat16())
     y = Act(torch.empty(a.batch, a.hw, a.hw, a.cout, device=dev, dtype=torch.bfloat16))
+    dw = torch.empty_like(conv.weight)
+    plan = unit.fwd_plan(a.hw, a.hw)
+
+    def run():
+        if a.wgrad:
+            eng._wgrad(unit, x, plan, y, dw)
+        else:
+            eng.unit_fwd(unit, x, y, None)
+    if a.wgrad:
+        y.buf.copy_(torch.randn_like(y.buf, dtype=torch.float32).clamp(min=0).bfloat16())
     for _ in range(3):
-        eng.unit_fwd(unit, x, y, None)
+        run()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(a.iters):
-        eng.unit_fwd(unit, x, y, None)
+        run()
     e1.record()
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / a.iters
     fl = 2.0 * a.batch * a.hw * a.hw * a.k * a.k * a.cin * a.cout
-    print(f"{a.tag} {a.cin}->{a.cout} k{a.k} d{a.d} {a.hw}x{a.hw} b{a.batch}: {us:8.1f} us  {fl / us * 1e-6:7.1f} TFLOP/s")
+    print(f"{a.tag} {'wgrad ' if a.wgrad else ''}{a.cin}->{a.cout} k{a.k} d{a.d} {a.hw}x{a.hw} b{a.batch}: {us:8.1f} us  {fl / us * 1e-6:7.1f} TFLOP/s")
 
 
 if __name__ == "__main__":

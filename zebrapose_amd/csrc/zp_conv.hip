@@ -15,7 +15,8 @@
 #include "zp_common.h"
 
 // Diagnostic ablation builds only (tools/build_ablation.sh -> libzp_abl<N>.so; wrong results):
-// ZP_ABL 1 = k_conv issues no LDS-DMA, 2 = k_conv runs no MFMA.  The product build is ZP_ABL 0.
+// ZP_ABL 1 = k_conv / k_wgrad_lds issue no LDS-DMA, 2 = they run no MFMA.  The product build is
+// ZP_ABL 0.
 #ifndef ZP_ABL
 #define ZP_ABL 0
 #endif
@@ -792,11 +793,12 @@ __device__ __forceinline__ uint2 ds_read_tr8(unsigned addr) {
   return r;
 }
 
-template <int KP, int NA, int NB, int STAGES>
+template <int KP, int NA, int NB, int STAGES, int WN>
 __global__ void __launch_bounds__(512) k_wgrad_lds(const zp_wgrad_args A, float* __restrict__ ws, int pix_per_split,
                                                    int col_tiles, int tiles_per_sub, int cols_max,
                                                    const wg_bounds WB) {
-  static_assert(NA * NB == 8, "8 waves of 64 x 64");
+  static_assert(NA * NB == 8 * WN, "8 waves of 64 x (64 WN)");
+  constexpr int NBW = NB / WN;           // wave columns
   static_assert(KP == 32 || KP == 64, "K step");
   static_assert(STAGES == 2 || STAGES == 3, "ring depth");
   constexpr int NP = NA + NB;            // panels per stage
@@ -834,7 +836,7 @@ __global__ void __launch_bounds__(512) k_wgrad_lds(const zp_wgrad_args A, float*
   const int col0 = ct * 64 * NB, co0 = cot * 64 * NA;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wa = wid / NB, wb = wid % NB;
+  const int wa = wid / NBW, wb = wid % NBW;  // wave (co panel, group of WN column panels)
   const int GHW = A.GH * A.GW;
   const int M = A.N * GHW;
   const int pbeg = split * pix_per_split;
@@ -935,52 +937,58 @@ __global__ void __launch_bounds__(512) k_wgrad_lds(const zp_wgrad_args A, float*
     }
   };
 
-  f32x4 acc[4][4];
+  f32x4 acc[4][4 * WN];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 4 * WN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   // fragment read addresses: lane (g, 4q+p) -> row 8g + q, byte 8p of the 16-column block,
   // 16-column block ii at chunk pair 2*(ii ^ s'), s' = s(R) / 2 (independent of the +4 / +32
   // row offsets, which are immediates)
   const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
   const int sh = (((q4 >> 1) & 1) | ((g & 1) << 1));
-  unsigned ra[4], rb[4];
+  unsigned ra[4];
 #pragma unroll
-  for (int ii = 0; ii < 4; ++ii) {
-    const unsigned in_panel = (unsigned)(128 * (8 * g + q4) + 8 * p4 + 32 * (ii ^ sh));
-    ra[ii] = (unsigned)(wa * PB) + in_panel;
-    rb[ii] = (unsigned)((NA + wb) * PB) + in_panel;
-  }
+  for (int ii = 0; ii < 4; ++ii) ra[ii] = (unsigned)(wa * PB) + (unsigned)(128 * (8 * g + q4) + 8 * p4 + 32 * (ii ^ sh));
+  // column panel w of this wave = panel NA + wb * WN + w: an immediate offset w * PB
 
   auto step = [&](auto cur_c, auto nxt_c, int ks) {
     const bool more = ks + (STAGES - 1) < nK;
-    if (more) issue(bufp(nxt_c));
+    if constexpr (ZP_ABL != 1) {
+      if (more) issue(bufp(nxt_c));
+    }
     const unsigned cb = lds_addr(bufp(cur_c));
     unsigned pa[4], pb[4];
 #pragma unroll
     for (int ii = 0; ii < 4; ++ii) {
       pa[ii] = cb + ra[ii];
-      pb[ii] = cb + rb[ii];
+      pb[ii] = pa[ii] + (unsigned)((NA + wb * WN - wa) * PB);
     }
     static_for<KP / 32>([&](auto s2) {
-      uint4 af[4], bfr[4];
+      uint4 af[4], bfr[4 * WN];
       static_for<4>([&](auto ii) {
         const uint2 a0 = ds_read_tr8<s2 * 4096>(pa[ii]);
         const uint2 a1 = ds_read_tr8<s2 * 4096 + 512>(pa[ii]);
-        const uint2 b0 = ds_read_tr8<s2 * 4096>(pb[ii]);
-        const uint2 b1 = ds_read_tr8<s2 * 4096 + 512>(pb[ii]);
         af[ii] = make_uint4(a0.x, a0.y, a1.x, a1.y);
-        bfr[ii] = make_uint4(b0.x, b0.y, b1.x, b1.y);
+        static_for<WN>([&](auto w) {
+          const uint2 b0 = ds_read_tr8<w * PB + s2 * 4096>(pb[ii]);
+          const uint2 b1 = ds_read_tr8<w * PB + s2 * 4096 + 512>(pb[ii]);
+          bfr[w * 4 + ii] = make_uint4(b0.x, b0.y, b1.x, b1.y);
+        });
       });
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_setprio(1);
+      if constexpr (ZP_ABL != 2) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) MfmaTraits<bf16_t>::mma(acc[i][j], af[i], bfr[j]);
+          for (int j = 0; j < 4 * WN; ++j) MfmaTraits<bf16_t>::mma(acc[i][j], af[i], bfr[j]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i][0][0] += __uint_as_float(af[i].x ^ bfr[i].y);
+      }
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_setprio(0);
     });
@@ -1023,8 +1031,8 @@ __global__ void __launch_bounds__(512) k_wgrad_lds(const zp_wgrad_args A, float*
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int col = col0 + wb * 64 + j * 16 + (lane & 15);
+    for (int j = 0; j < 4 * WN; ++j) {
+      const int col = col0 + wb * WN * 64 + j * 16 + (lane & 15);
       if (col >= cols) continue;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -1045,8 +1053,20 @@ __global__ void k_wgrad_reduce(const zp_wgrad_args A, const float* __restrict__ 
     const int t = col / A.Cin, ci = col - t * A.Cin;
     const int ky = S.ky[t], kx = S.kx[t];
     if (ci >= A.Cw || ky < 0) continue;  // padded input channels / padding taps
-    float s = 0.f;
-    for (int k = 0; k < splits; ++k) s += ws[(((size_t)k * A.nsub + sub) * A.Cout + co) * cols_max + col];
+    // 8 independent partial sums (loads in flight together; fixed order -> deterministic)
+    const size_t stride = (size_t)A.nsub * A.Cout * cols_max;
+    const float* p = ws + ((size_t)sub * A.Cout + co) * cols_max + col;
+    float q[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int k = 0;
+    for (; k + 8 <= splits; k += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = p[(size_t)(k + u) * stride];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) q[u] += v[u];
+    }
+    for (; k < splits; ++k) q[0] += p[(size_t)k * stride];
+    const float s = ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
     size_t idx = A.transposed_w ? (((size_t)ci * A.Cout + co) * A.kh + ky) * A.kw + kx
                                 : (((size_t)co * A.Cw + ci) * A.kh + ky) * A.kw + kx;
     if (A.accumulate) A.dw[idx] += s;
@@ -1270,16 +1290,24 @@ static bool wgrad_lds(const zp_wgrad_args& a) {
   static const int v = getenv("ZP_WGRAD") ? env_int("ZP_WGRAD") : 1;
   return a.dtype == ZP_BF16 && v != 0;
 }
+// tile: 0 = 64 co x 512 col (Cout <= 64), 1 = 128 x 256, 2 = 256 x 256 (Cout >= 256: fewer staged
+// bytes per FLOP -- the L2 -> LDS stream, not the MFMA, bounds this kernel)
+static int wgrad_cfg(const zp_wgrad_args& a) {
+  static const int big = getenv("ZP_WGRAD_BIG") ? env_int("ZP_WGRAD_BIG") : 1;
+  if (a.Cout <= 64) return 0;
+  if (a.Cout >= 256 && big) return 2;
+  return 1;
+}
 static void wgrad_plan_lds(const zp_wgrad_args& a, int* splits, int* col_tiles, int* cols_max, int* pix_per) {
   long M = (long)a.N * a.GH * a.GW;
   int cm = 0;
   for (int s = 0; s < a.nsub; ++s) cm = cm > a.sub[s].ntaps * a.Cin ? cm : a.sub[s].ntaps * a.Cin;
-  const bool narrow = a.Cout <= 64;
-  const int tco = narrow ? 64 : 128, tcol = narrow ? 512 : 256, KP = 64;
+  const int cfg = wgrad_cfg(a);
+  const int tco = cfg == 0 ? 64 : (cfg == 1 ? 128 : 256), tcol = cfg == 0 ? 512 : 256, KP = 64;
   int ct = ceil_div(cm, tcol);
   int tiles = ct * ceil_div(a.Cout, tco) * a.nsub;
   long sp = (512 + tiles - 1) / tiles;
-  long maxsp = M / (8 * KP);
+  long maxsp = M / (16 * KP);
   if (maxsp < 1) maxsp = 1;
   if (sp > maxsp) sp = maxsp;
   if (sp > 256) sp = 256;
@@ -1330,14 +1358,19 @@ extern "C" int zp_conv2d_wgrad(const zp_wgrad_args* ap, void* ws, void* stream) 
       ZP_CHECK_ARG(db < (1ll << 31), "zp_conv2d_wgrad: dy %lld B must stay below 2 GiB", db);
       wb.dy_bytes[s] = (unsigned)db;
     }
-    if (a.Cout <= 64) {
+    const int cfg = wgrad_cfg(a);
+    if (cfg == 0) {
       const int tiles = ct * ceil_div(a.Cout, 64);
-      hipLaunchKernelGGL((k_wgrad_lds<64, 1, 8, 2>), dim3(sp * a.nsub * tiles), dim3(512), 0, st, a, (float*)ws, pp,
-                         ct, tiles, cm, wb);
-    } else {
+      hipLaunchKernelGGL((k_wgrad_lds<64, 1, 8, 2, 1>), dim3(sp * a.nsub * tiles), dim3(512), 0, st, a, (float*)ws,
+                         pp, ct, tiles, cm, wb);
+    } else if (cfg == 1) {
       const int tiles = ct * ceil_div(a.Cout, 128);
-      hipLaunchKernelGGL((k_wgrad_lds<64, 2, 4, 3>), dim3(sp * a.nsub * tiles), dim3(512), 0, st, a, (float*)ws, pp,
-                         ct, tiles, cm, wb);
+      hipLaunchKernelGGL((k_wgrad_lds<64, 2, 4, 3, 1>), dim3(sp * a.nsub * tiles), dim3(512), 0, st, a, (float*)ws,
+                         pp, ct, tiles, cm, wb);
+    } else {
+      const int tiles = ct * ceil_div(a.Cout, 256);
+      hipLaunchKernelGGL((k_wgrad_lds<64, 4, 4, 2, 2>), dim3(sp * a.nsub * tiles), dim3(512), 0, st, a, (float*)ws,
+                         pp, ct, tiles, cm, wb);
     }
   } else {
     wgrad_plan(a, &sp, &ct, &cm, &pp);
