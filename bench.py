@@ -183,6 +183,24 @@ def main():
                 "all_conv_tflops": round(all_conv_flops / all_conv_time / 1e12, 2),
                 "whole_step_tflops": round(FWD_GFLOP_PER_CROP * 1e9 * B / (ms_per_step * 1e-3) / 1e12, 2)}
 
+    # ------------------------------------------------------------------ on-device PnP (extra, §8f rank 1)
+    # RANSAC-EPnP (150 iterations, 2 px) over the last step's decoded correspondences; the random
+    # network gives random correspondences, i.e. the worst case (no early RANSAC termination)
+    from zebrapose_amd.pnp import PnP
+    pnp = PnP()
+    counts, xy, xyz = out
+    pnp(counts, xy, xyz)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(5):
+        pnp(counts, xy, xyz)
+    e1.record()
+    torch.cuda.synchronize()
+    pnp_ms = e0.elapsed_time(e1) / 5
+    pnp_res = {"ms_per_batch": round(pnp_ms, 3), "crops_per_s": round(B / (pnp_ms * 1e-3), 1), "iterations": 150,
+               "correspondences_per_crop": round(n_corr / B)}
+
     # ------------------------------------------------------------------ training step (extra)
     train = None
     if not args.no_train:
@@ -251,7 +269,7 @@ def main():
                            "model": "BinaryCodeNet_Deeplab(34, 16, 2, concat=True)", "global_batch": world * B,
                            "per_gpu_batch": B, "input": f"{S}x{S}", "parallelism": f"replicas{world}",
                            "correspondences_last_step": n_corr},
-                "roofline": roofline, "cpu_baseline": cpu, "train": train}
+                "roofline": roofline, "cpu_baseline": cpu, "train": train, "pnp": pnp_res}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -265,6 +265,17 @@ int zp_decode(const float* mask_logits, const float* code_logits, int B, int H, 
 /* out[n][3] (f32) = mean over the 2^(old-new) children of lut64 (f64, summed in order) */
 int zp_lut_coarsen(const double* lut64, int old_bits, int new_bits, float* out, void* stream);
 
+/* ---- pose ---------------------------------------------------------
+ * Batched RANSAC-EPnP, replacing cv2.solvePnPRansac(P3D, P2D, K, None, reprojectionError,
+ * iterationsCount, flags=SOLVEPNP_EPNP) at binary_code_helper/CNN_output_to_pose.py:152-156.
+ * Inputs are zp_decode's outputs: counts[B], xy int32 [B][HW][2] (original-image pixels),
+ * xyz f32 [B][HW][3]; K f64 [B][4] = (fx, fy, cx, cy).  Outputs R f64 [B][9] (row-major),
+ * T f64 [B][3], success[B] (RANSAC found a model), inliers[B].  ws: zp_pnp_ws_bytes(B, iters). */
+long long zp_pnp_ws_bytes(int B, int iters);
+int zp_pnp_ransac(int B, int HW, const int* counts, const int* xy, const float* xyz, const double* K,
+                  int iters, double reproj_err, double confidence, double* R, double* T, int* success,
+                  int* inliers, void* ws, void* stream);
+
 /* ---- optimizer ----------------------------------------------------------------------- */
 /* torch.optim.Adam (no weight decay, amsgrad off) over one flat f32 buffer; step >= 1 */
 int zp_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long long n,

@@ -5,7 +5,9 @@ the ``zp_decode`` HIP kernel: these functions take the reference's host arrays, 
 decode and return the reference's host arrays.  For batched inference use
 ``zebrapose_amd.decode.Decoder`` directly on the network's device outputs.
 
-PnP (:132-158) stays with OpenCV / pyprogressivex as in the reference (out of scope: SURVEY §8f).
+PnP (:132-158): the reference's default RANSAC-EPnP runs on the device (``zebrapose_amd.pnp``,
+``zp_pnp_ransac``); Progressive-X stays with pyprogressivex when that module is installed, as in
+the reference.
 """
 from __future__ import annotations
 
@@ -95,9 +97,17 @@ def CNN_outputs_to_object_pose(mask_image, class_code_image, Bbox, Bbox_Size, cl
             else:
                 rot, tvecs, success = np.zeros((3, 3)), np.zeros((3, 1)), False
         else:
-            import cv2  # OpenCV is the reference's default PnP (not part of this package)
-            _, rvecs, tvecs, _ = cv2.solvePnPRansac(coord_3d, coord_2d, intrinsic_matrix, distCoeffs=None,
-                                                    reprojectionError=2, iterationsCount=150,
-                                                    flags=cv2.SOLVEPNP_EPNP)
-            rot, _ = cv2.Rodrigues(rvecs, jacobian=None)
+            # the reference's default, cv2.solvePnPRansac(EPNP, 2 px, 150 iterations) + Rodrigues
+            # (:152-158), runs on the device: zp_pnp_ransac (csrc/zp_pnp.hip)
+            rot, tvecs = _device_pnp(p2d, p3d, intrinsic_matrix)
     return rot, tvecs, success
+
+
+def _device_pnp(p2d, p3d, intrinsic_matrix, device="cuda"):
+    from ..pnp import PnP
+    n = len(p2d)
+    counts = torch.tensor([n], dtype=torch.int32, device=device)
+    xy = torch.from_numpy(np.ascontiguousarray(p2d.astype(np.int32))[None]).to(device)
+    xyz = torch.from_numpy(np.ascontiguousarray(p3d.astype(np.float32))[None]).to(device)
+    R, t, _, _ = PnP()(counts, xy, xyz, np.asarray(intrinsic_matrix, dtype=np.float64))
+    return R[0].cpu().numpy(), t[0].cpu().numpy().reshape(3, 1)

@@ -1151,6 +1151,11 @@ static int conv_tp(const zp_conv_args& a) {
   if (tc == 32) return 128;  // 32 + 256 rows do not split over 8 waves in 8-row groups
   const int ov = conv_tp_override();
   if (ov == 128 || ov == 256) return ov;
+  // Cout <= 128 (one cout tile): 128-pixel tiles double the workgroup count of the 32x32 / 64x64
+  // layers (tools/conv_micro.py: 128->128 @32x32 36 -> 24 us, 64->64 @64x64 28.6 -> 26.3 us);
+  // the small-Cin stem keeps 256
+  const int E = a.dtype == ZP_BF16 ? 8 : 4;
+  if (a.Cout <= 128 && a.Cin >= 8 * E) return 128;
   return 256;
 }
 
