@@ -276,6 +276,16 @@ int zp_pnp_ransac(int B, int HW, const int* counts, const int* xy, const float* 
                   int iters, double reproj_err, double confidence, double* R, double* T, int* success,
                   int* inliers, void* ws, void* stream);
 
+/* ---- pose error ----------------------------------------------------
+ * ADD / ADI of B pose pairs over one model's points pts f32 [n][3], replacing
+ * metric.py:8-18 (bop_toolkit pose_error.add / adi; lib/pysixd/pose_error.py:297-336).
+ * R f64 [B][9] row-major, t f64 [B][3]; out f64 [B].  ADI is an exact nearest-neighbour search. */
+#define ZP_METRIC_ADD 0
+#define ZP_METRIC_ADI 1
+long long zp_pose_error_ws_bytes(int B, int n, int mode);
+int zp_pose_error(int B, const float* pts, int n, const double* R_est, const double* t_est,
+                  const double* R_gt, const double* t_gt, int mode, double* out, void* ws, void* stream);
+
 /* ---- optimizer ----------------------------------------------------------------------- */
 /* torch.optim.Adam (no weight decay, amsgrad off) over one flat f32 buffer; step >= 1 */
 int zp_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long long n,
