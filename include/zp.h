@@ -106,8 +106,9 @@ int zp_conv_rows_pad(int Cout);
 int zp_conv2d_grid(const zp_conv_args* a);
 /* number of partial-sum slots `stats` needs: 2 * grid_x * nsub */
 int zp_conv2d_stat_parts(const zp_conv_args* a);
-/* launch configuration zp_conv2d picks: cout tile, pixel tile, LDS ring depth */
-int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* stages);
+/* launch configuration zp_conv2d picks: cout tile, pixel tile, LDS ring depth, kernel variant
+ * (0 = k_conv, 1 = k_conv_strip: 3x3 stride-1 convs with activation-strip reuse) */
+int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* stages, int* variant);
 /* runtime tuning knob (tests / sweeps): key 0 = minimum workgroup count for the 256-channel
  * tile (default 512).  Returns the previous value, -1 for an unknown key. */
 int zp_conv_tuning(int key, int value);

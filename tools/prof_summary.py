@@ -27,6 +27,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def bench_label(name):
     """'void zp::k_conv<unsigned short, 4, 4, 4, 3, false>(zp_conv_args)' ->
     'k_conv<bf16,WC=4,WP=4,NWP=4,ST=3,smallC=0>' (the label bench.py / engine.py use)."""
+    m = re.search(r"k_conv_strip<(\d+), (\d+), (\d+)>", name)
+    if m:
+        return f"k_conv_strip<bf16,WC={m.group(1)},ST={m.group(2)}>"
     m = re.search(r"k_conv<(unsigned short|float), (\d+), (\d+), (\d+), (\d+), (true|false)>", name)
     if not m:
         return None

@@ -102,7 +102,7 @@ _SIGS = {
     "zp_lut_coarsen": (i32, [vp, i32, i32, vp, vp]),
     "zp_adam": (i32, [vp, vp, vp, vp, i64, f64, f64, f64, f64, i64, vp]),
     "zp_pack_weight_multi": (i32, [i32, vp, vp, i64, vp]),
-    "zp_conv2d_config": (i32, [vp, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)]),
+    "zp_conv2d_config": (i32, [vp, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)]),
     "zp_conv_tuning": (i32, [i32, i32]),
     "zp_pnp_ws_bytes": (i64, [i32, i32]),
     "zp_pnp_ransac": (i32, [i32, i32, vp, vp, vp, vp, i32, f64, f64, vp, vp, vp, vp, vp, vp]),

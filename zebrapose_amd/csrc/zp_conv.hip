@@ -15,8 +15,8 @@
 #include "zp_common.h"
 
 // Diagnostic ablation builds only (tools/build_ablation.sh -> libzp_abl<N>.so; wrong results):
-// ZP_ABL 1 = k_conv / k_wgrad_lds issue no LDS-DMA, 2 = they run no MFMA.  The product build is
-// ZP_ABL 0.
+// ZP_ABL 1 = k_conv / k_wgrad_lds issue no LDS-DMA, 2 = they run no MFMA, 3 = k_conv stages only
+// the weights (no activation DMA).  The product build is ZP_ABL 0.
 #ifndef ZP_ABL
 #define ZP_ABL 0
 #endif
@@ -86,297 +86,12 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
-// Staging: every K step moves TC weight rows + TP activation rows of 128 B each straight
-// from global memory into LDS with global_load_lds_dwordx4 (one wave-instruction = 8 rows x
-// 128 B, lane-linear in LDS).  The 16 B chunk swizzle (chunk ^ (row & 7), conflict-free
-// ds_read_b128 of the MFMA fragments) is applied on the per-lane SOURCE address.  Out-of-
-// image taps read g_zero_page.  STAGES LDS buffers: the loads of steps k+1..k+STAGES-1 are
-// in flight while step k's MFMAs run; each step ends with a counted vmcnt wait (only the
-// oldest step's loads) and a raw s_barrier.
-template <typename T, int WC, int WP, int NWP, int STAGES, bool SMALLC>
-__global__ void __launch_bounds__(128 * NWP) k_conv(const zp_conv_args A, const conv_taps TG, const int flags) {
-  static_assert(STAGES == 2 || STAGES == 3, "2- or 3-deep LDS ring");
-  constexpr int E = MfmaTraits<T>::E;
-  constexpr int KE = 8 * E;  // elements per K step (128 B)
-  constexpr int TC = 32 * WC, TP = 16 * WP * NWP;
-  constexpr int NW = 2 * NWP;                 // waves
-  constexpr int G = (TC + TP) / 8;            // 8-row groups per K step
-  static_assert(G % NW == 0, "row groups must split evenly over the waves");
-  constexpr int GPW = G / NW;                 // groups per wave
-  // the first WPW groups of every wave are weight rows, the rest activation rows (group g = wid + NW*i
-  // is a weight group iff i < WPW): compile-time, so per-pixel state exists only for pixel groups
-  static_assert((TC / 8) % NW == 0, "weight groups must split evenly over the waves");
-  constexpr int WPW = TC / 8 / NW;
-  __shared__ uint4 lds0[(TC + TP) * 8];
-  __shared__ uint4 lds1[(TC + TP) * 8];
-  __shared__ uint4 lds2[STAGES == 3 ? (TC + TP) * 8 : 1];
-  auto bufp = [&](auto i_c) -> uint4* {
-    constexpr int i = decltype(i_c)::value;
-    if constexpr (i == 0) return lds0;
-    else if constexpr (i == 1) return lds1;
-    else return lds2;
-  };
-
-  const zp_conv_sub& S = A.sub[blockIdx.z];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar branches)
-  const int wc = wid / NWP, wp = wid % NWP;
-  const int GHW = A.GH * A.GW;
-  const int M = A.N * GHW;
-  // XCD-aware tile order (flags & 2): workgroups are dispatched round-robin over the
-  // 8 XCDs, so consecutive linear ids land on different L2s.  Remap so that each XCD walks a
-  // contiguous run of (pixel tile, cout tile) pairs, cout tiles fastest: the cout tiles of one
-  // pixel tile (same activations) and neighbouring pixel tiles (shared halo rows) then meet in
-  // the same L2.
-  int bx = blockIdx.x, by = blockIdx.y;
-  if (flags & 2) {
-    const int total = gridDim.x * gridDim.y;
-    const int bid = blockIdx.x + gridDim.x * blockIdx.y;
-    const int lin = (total & 7) ? bid : (bid & 7) * (total >> 3) + (bid >> 3);
-    bx = lin / gridDim.y;
-    by = lin - bx * gridDim.y;
-  }
-  const int p0 = bx * TP, c0 = by * TC;
-  const int lrow = lane >> 3;                  // row within the 8-row group
-  const int csrc = (lane & 7) ^ lrow;          // source chunk (swizzle on the source side)
-
-  // per group: weight row or activation row (pixel) of this lane
-  int gpix_n[GPW], gpix_y[GPW], gpix_x[GPW];
-  bool gvalid[GPW];
-#pragma unroll
-  for (int i = 0; i < GPW; ++i) {
-    if (i < WPW) continue;
-    const int r = (wid + NW * i) * 8 + lrow;
-    int m = p0 + (r - TC);
-    gvalid[i] = r >= TC && m < M;
-    int mm = gvalid[i] ? m : 0;
-    int n = mm / GHW, rr = mm - n * GHW;
-    int gy = rr / A.GW, gx = rr - gy * A.GW;
-    gpix_n[i] = n;
-    gpix_y[i] = gy * A.sy;
-    gpix_x[i] = gx * A.sx;
-  }
-  const T* __restrict__ X = (const T*)A.x;
-  const T* __restrict__ Wt = (const T*)S.w;
-  const int CB = SMALLC ? 1 : A.Cin / KE;
-  const int nK = SMALLC ? A.k_pad / KE : S.ntaps * CB;
-
-  // ---- staging addresses (Cin >= 64 B-chunk path): buffer loads with per-lane 32-bit byte
-  // offsets.  The tap walk (ty, tx, channel chunk) is scalar state advanced by one K step per
-  // issue; per lane only the pixel's base offset and two validity bit masks (input row / column
-  // in range, one bit per tap row / column) are kept.  Invalid taps use an offset past the
-  // buffer's end, which the buffer unit returns as zeros: no address clamp, no select of a
-  // zero page, no multiplies in the loop.
-  const int tb = blockIdx.z;
-  const int ny = TG.ny[tb], nx = TG.nx[tb], dty = TG.dty[tb], dtx = TG.dtx[tb];
-  unsigned abase[GPW], ymask[GPW], xmask[GPW];
-#pragma unroll
-  for (int i = 0; i < GPW; ++i) {
-    if (i < WPW) continue;
-    const int y0 = gpix_y[i], x0 = gpix_x[i];
-    abase[i] = (unsigned)(((((long)gpix_n[i] * A.IH + y0) * A.IW + x0) * A.ldx + A.cx0 + csrc * E) * sizeof(T));
-    unsigned ym = 0, xm = 0;
-    for (int q = 0; q < ny; ++q) ym |= (unsigned)((unsigned)(y0 + TG.ty0[tb] + q * dty) < (unsigned)A.IH) << q;
-    for (int q = 0; q < nx; ++q) xm |= (unsigned)((unsigned)(x0 + TG.tx0[tb] + q * dtx) < (unsigned)A.IW) << q;
-    ymask[i] = gvalid[i] ? ym : 0u;
-    xmask[i] = xm;
-  }
-  const unsigned wbase = (unsigned)(((size_t)(c0 + wid * 8 + lrow) * A.k_pad + csrc * E) * sizeof(T));
-  // scalar tap walk: the next K step to issue is (tap row tyi, tap column txi, chunk cb) with
-  // act_off = ((ty * IW + tx) * ldx + cb * KE) * sizeof(T)
-  int w_tyi = 0, w_txi = 0, w_cb = 0;
-  int act_off = ((TG.ty0[tb] * A.IW + TG.tx0[tb]) * A.ldx) * (int)sizeof(T);
-  const int step_x = dtx * A.ldx * (int)sizeof(T), step_y = dty * A.IW * A.ldx * (int)sizeof(T);
-  const int chunk_b = KE * (int)sizeof(T);
-#if defined(__HIP_DEVICE_COMPILE__)
-  const __amdgpu_buffer_rsrc_t xrsrc =
-      __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)TG.x_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t wrsrc =
-      __builtin_amdgcn_make_buffer_rsrc((void*)Wt, (short)0, (int)TG.w_bytes[tb], 0x00020000);
-#endif
-
-  auto issue = [&](int ks, uint4* dst) {
-    if constexpr (SMALLC) {
-      // small Cin (stem): one K step mixes taps, per-lane tap decode
-      const int kw_off = ks * KE;
-      int k = ks * KE + csrc * E;
-      int t = k / A.Cin;
-      const int cc = k - t * A.Cin;
-      const bool tok = t < S.ntaps;
-      int kyy = t / S.kw;
-      const int ty = kyy * S.dil - S.pad;
-      const int tx = (t - kyy * S.kw) * S.dil - S.pad;
-      const void* srcs[GPW];
-#pragma unroll
-      for (int i = 0; i < GPW; ++i) {
-        const int g = wid + NW * i;
-        const int r = g * 8 + lrow;
-        const void* src;
-        if (i < WPW) {
-          src = Wt + (size_t)(c0 + r) * A.k_pad + kw_off + csrc * E;
-        } else {
-          int iy = gpix_y[i] + ty, ix = gpix_x[i] + tx;
-          bool ok = tok && gvalid[i] && (unsigned)iy < (unsigned)A.IH && (unsigned)ix < (unsigned)A.IW;
-          int iyc = min(max(iy, 0), A.IH - 1), ixc = min(max(ix, 0), A.IW - 1);
-          const T* pv = X + (((size_t)gpix_n[i] * A.IH + iyc) * A.IW + ixc) * A.ldx + A.cx0 + cc;
-          src = ok ? (const void*)pv : (const void*)&g_zero_page[lane & 7];
-        }
-        srcs[i] = src;
-      }
-#if defined(__HIP_DEVICE_COMPILE__)  // device-only builtin: the host pass would silently drop the kernel stubs
-#pragma unroll
-      for (int i = 0; i < GPW; ++i) {
-        const int g = wid + NW * i;
-        __builtin_amdgcn_global_load_lds(srcs[i], (__attribute__((address_space(3))) void*)&dst[g * 64], 16, 0, 0);
-      }
-#endif
-    } else {
-      // all offsets first (distinct registers), then the DMA issues back to back: hipcc waits
-      // vmcnt(0) before it rewrites the address VGPRs of an in-flight LDS-DMA
-      unsigned voff[GPW];
-#pragma unroll
-      for (int i = 0; i < GPW; ++i) {
-        const int g = wid + NW * i;
-        if (i < WPW) {  // weight group (compile-time)
-          voff[i] = wbase + (unsigned)(NW * i * 8) * (unsigned)(A.k_pad * sizeof(T));
-        } else {
-          const bool ok = (ymask[i] >> w_tyi) & (xmask[i] >> w_txi) & 1u;
-          voff[i] = ok ? abase[i] + (unsigned)act_off : 0x80000000u;
-        }
-      }
-#if defined(__HIP_DEVICE_COMPILE__)
-#pragma unroll
-      for (int i = 0; i < GPW; ++i) {
-        const int g = wid + NW * i;
-        auto* d = (__attribute__((address_space(3))) void*)&dst[g * 64];
-        if (i < WPW)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(wrsrc, d, 16, voff[i], ks * chunk_b, 0, 0);
-        else
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(xrsrc, d, 16, voff[i], 0, 0, 0);
-      }
-#endif
-      // advance the scalar tap walk to step ks + 1 (tap-major: chunks fastest)
-      act_off += chunk_b;
-      if (++w_cb == CB) {
-        w_cb = 0;
-        act_off += step_x - CB * chunk_b;
-        if (++w_txi == nx) {
-          w_txi = 0;
-          act_off += step_y - nx * step_x;
-          ++w_tyi;
-        }
-      }
-    }
-  };
-
-  f32x4 acc[WC][WP];
-#pragma unroll
-  for (int i = 0; i < WC; ++i)
-#pragma unroll
-    for (int j = 0; j < WP; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  // Three-stage ring: while step k computes from buffer k%3, the DMA of steps k+1 (issued one
-  // step earlier) and k+2 (issued now) are in flight.  End of step k: counted vmcnt(GPW) (only
-  // step k+2's loads may remain outstanding) + raw s_barrier -- never __syncthreads(), whose
-  // vmcnt(0) would drain the ring.  Buffer indices are compile-time (loop unrolled by 3) and the
-  // three buffers are distinct LDS objects, so hipcc can prove a ds_read never aliases an
-  // in-flight global_load_lds and inserts no vmcnt wait in front of it.
-  const bool pingpong = NW == 8 && !SMALLC && (flags & 8);
-  // per-lane byte offsets of the MFMA fragments inside a stage buffer: row (lane & 15) of the
-  // wave's first 16-row tile, 16 B chunk (s * 4 + lane / 16) swizzled by (row & 7) = (lane & 7);
-  // tile i / j adds i * 16 rows = i * 2048 B (an immediate of the ds_read)
-  unsigned aoff[2], boff[2];
-#pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2) {
-    const unsigned chunk = (unsigned)(((s2 * 4 + (lane >> 4)) ^ (lane & 7)) * 16);
-    aoff[s2] = (unsigned)(wc * 16 * WC + (lane & 15)) * 128u + chunk;
-    boff[s2] = (unsigned)(TC + wp * 16 * WP + (lane & 15)) * 128u + chunk;
-  }
-  auto step = [&](auto cur_c, auto nxt_c, int ks) {
-    const bool more = ks + (STAGES - 1) < nK;
-    // next stage's DMA first (its tap offsets come from scalar loads, whose lgkmcnt wait must
-    // not also wait for this step's fragment reads)
-    if constexpr (ZP_ABL != 1) {
-      if (more) issue(ks + (STAGES - 1), bufp(nxt_c));
-    }
-    // fragment reads as inline asm: hipcc's waitcnt pass cannot prove across the loop back-edge
-    // that they miss the in-flight LDS-DMA buffers and would put a vmcnt(0) in front of them
-    const unsigned cb = lds_addr(bufp(cur_c));
-    uint4 af[2][WC], bfr[2][WP];
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      const unsigned pa = cb + aoff[s2], pb = cb + boff[s2];
-      static_for<WC>([&](auto i) { af[s2][i] = ds_read16<i * 2048>(pa); });
-      static_for<WP>([&](auto j) { bfr[s2][j] = ds_read16<j * 2048>(pb); });
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    if (pingpong) {
-      // end of the read section: fragments in registers (the other group may refill this
-      // buffer after the barrier) and every load but the newest step's retired, so the next
-      // step's buffer is complete once all waves have passed the barrier
-      if (more) vm_wait<GPW * (STAGES - 2)>();
-      else vm_wait<0>();
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (flags & 4) __builtin_amdgcn_s_setprio(1);
-    if constexpr (ZP_ABL != 2) {
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int i = 0; i < WC; ++i)
-#pragma unroll
-          for (int j = 0; j < WP; ++j) MfmaTraits<T>::mma(acc[i][j], af[s2][i], bfr[s2][j]);
-    } else {
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int i = 0; i < WC; ++i) acc[i][0][0] += __uint_as_float(af[s2][i].x ^ bfr[s2][0].y);
-    }
-    __builtin_amdgcn_sched_barrier(0);  // keep the MFMAs in front of the wait + barrier
-    if (flags & 4) __builtin_amdgcn_s_setprio(0);
-    if (!pingpong) {
-      if (more) vm_wait<GPW * (STAGES - 2)>();
-      else vm_wait<0>();
-    }
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  using I2 = std::integral_constant<int, 2>;
-  issue(0, lds0);
-  if (STAGES == 3 && nK > 1) {
-    issue(1, lds1);
-    vm_wait<GPW * (STAGES - 2)>();
-  } else {
-    vm_wait<0>();
-  }
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-  // Ping-pong (flags & 8, 8-wave tiles): every step is a read section (fragments + next DMA)
-  // and an MFMA section, each closed by a barrier; waves 4-7 start one barrier late, so on
-  // every SIMD (waves w and w+4 share one) one wave's MFMAs overlap the other's LDS reads.
-  if (pingpong && wid >= 4) __builtin_amdgcn_s_barrier();
-  if constexpr (STAGES == 3) {
-    for (int ks = 0; ks < nK; ks += 3) {
-      step(I0{}, I2{}, ks);
-      if (ks + 1 >= nK) break;
-      step(I1{}, I0{}, ks + 1);
-      if (ks + 2 >= nK) break;
-      step(I2{}, I1{}, ks + 2);
-    }
-  } else {
-    for (int ks = 0; ks < nK; ks += 2) {
-      step(I0{}, I1{}, ks);
-      if (ks + 1 >= nK) break;
-      step(I1{}, I0{}, ks + 1);
-    }
-  }
-
-  if (pingpong && wid < 4) __builtin_amdgcn_s_barrier();  // same barrier count for both groups
-
+// Conv epilogue shared by k_conv and k_conv_strip: BN scale/shift (+bias), residual, ReLU,
+// NHWC (channel slice) / NCHW-head / f32 stores, or train-mode BN partial statistics.
+template <typename T, int WC, int WP, int NWP>
+__device__ __forceinline__ void conv_epilogue(const zp_conv_args& A, const zp_conv_sub& S, f32x4 (&acc)[WC][WP],
+                                              const int p0, const int c0, const int wc, const int wp, const int lane,
+                                              const int M, const int GHW, const int bx) {
   // ---------------- epilogue ----------------
   // output pixel of (lane, j): one division for j = 0, then +16 pixels per j
   int pn[WP], poy[WP], pox[WP];
@@ -589,6 +304,511 @@ __global__ void __launch_bounds__(128 * NWP) k_conv(const zp_conv_args A, const 
         }
       }
   }
+}
+
+// Staging: every K step moves TC weight rows + TP activation rows of 128 B each straight
+// from global memory into LDS with global_load_lds_dwordx4 (one wave-instruction = 8 rows x
+// 128 B, lane-linear in LDS).  The 16 B chunk swizzle (chunk ^ (row & 7), conflict-free
+// ds_read_b128 of the MFMA fragments) is applied on the per-lane SOURCE address.  Out-of-
+// image taps read g_zero_page.  STAGES LDS buffers: the loads of steps k+1..k+STAGES-1 are
+// in flight while step k's MFMAs run; each step ends with a counted vmcnt wait (only the
+// oldest step's loads) and a raw s_barrier.
+template <typename T, int WC, int WP, int NWP, int STAGES, bool SMALLC>
+__global__ void __launch_bounds__(128 * NWP) k_conv(const zp_conv_args A, const conv_taps TG, const int flags) {
+  static_assert(STAGES == 2 || STAGES == 3, "2- or 3-deep LDS ring");
+  constexpr int E = MfmaTraits<T>::E;
+  constexpr int KE = 8 * E;  // elements per K step (128 B)
+  constexpr int TC = 32 * WC, TP = 16 * WP * NWP;
+  constexpr int NW = 2 * NWP;                 // waves
+  constexpr int G = (TC + TP) / 8;            // 8-row groups per K step
+  static_assert(G % NW == 0, "row groups must split evenly over the waves");
+  constexpr int GPW = G / NW;                 // groups per wave
+  // the first WPW groups of every wave are weight rows, the rest activation rows (group g = wid + NW*i
+  // is a weight group iff i < WPW): compile-time, so per-pixel state exists only for pixel groups
+  static_assert((TC / 8) % NW == 0, "weight groups must split evenly over the waves");
+  constexpr int WPW = TC / 8 / NW;
+  constexpr int LPS = ZP_ABL == 3 ? WPW : GPW;  // LDS-DMA instructions per wave per stage
+  __shared__ uint4 lds0[(TC + TP) * 8];
+  __shared__ uint4 lds1[(TC + TP) * 8];
+  __shared__ uint4 lds2[STAGES == 3 ? (TC + TP) * 8 : 1];
+  auto bufp = [&](auto i_c) -> uint4* {
+    constexpr int i = decltype(i_c)::value;
+    if constexpr (i == 0) return lds0;
+    else if constexpr (i == 1) return lds1;
+    else return lds2;
+  };
+
+  const zp_conv_sub& S = A.sub[blockIdx.z];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar branches)
+  const int wc = wid / NWP, wp = wid % NWP;
+  const int GHW = A.GH * A.GW;
+  const int M = A.N * GHW;
+  // XCD-aware tile order (flags & 2): workgroups are dispatched round-robin over the
+  // 8 XCDs, so consecutive linear ids land on different L2s.  Remap so that each XCD walks a
+  // contiguous run of (pixel tile, cout tile) pairs, cout tiles fastest: the cout tiles of one
+  // pixel tile (same activations) and neighbouring pixel tiles (shared halo rows) then meet in
+  // the same L2.
+  int bx = blockIdx.x, by = blockIdx.y;
+  if (flags & 2) {
+    const int total = gridDim.x * gridDim.y;
+    const int bid = blockIdx.x + gridDim.x * blockIdx.y;
+    const int lin = (total & 7) ? bid : (bid & 7) * (total >> 3) + (bid >> 3);
+    bx = lin / gridDim.y;
+    by = lin - bx * gridDim.y;
+  }
+  const int p0 = bx * TP, c0 = by * TC;
+  const int lrow = lane >> 3;                  // row within the 8-row group
+  const int csrc = (lane & 7) ^ lrow;          // source chunk (swizzle on the source side)
+
+  // per group: weight row or activation row (pixel) of this lane
+  int gpix_n[GPW], gpix_y[GPW], gpix_x[GPW];
+  bool gvalid[GPW];
+#pragma unroll
+  for (int i = 0; i < GPW; ++i) {
+    if (i < WPW) continue;
+    const int r = (wid + NW * i) * 8 + lrow;
+    int m = p0 + (r - TC);
+    gvalid[i] = r >= TC && m < M;
+    int mm = gvalid[i] ? m : 0;
+    int n = mm / GHW, rr = mm - n * GHW;
+    int gy = rr / A.GW, gx = rr - gy * A.GW;
+    gpix_n[i] = n;
+    gpix_y[i] = gy * A.sy;
+    gpix_x[i] = gx * A.sx;
+  }
+  const T* __restrict__ X = (const T*)A.x;
+  const T* __restrict__ Wt = (const T*)S.w;
+  const int CB = SMALLC ? 1 : A.Cin / KE;
+  const int nK = SMALLC ? A.k_pad / KE : S.ntaps * CB;
+
+  // ---- staging addresses (Cin >= 64 B-chunk path): buffer loads with per-lane 32-bit byte
+  // offsets.  The tap walk (ty, tx, channel chunk) is scalar state advanced by one K step per
+  // issue; per lane only the pixel's base offset and two validity bit masks (input row / column
+  // in range, one bit per tap row / column) are kept.  Invalid taps use an offset past the
+  // buffer's end, which the buffer unit returns as zeros: no address clamp, no select of a
+  // zero page, no multiplies in the loop.
+  const int tb = blockIdx.z;
+  const int ny = TG.ny[tb], nx = TG.nx[tb], dty = TG.dty[tb], dtx = TG.dtx[tb];
+  unsigned abase[GPW], ymask[GPW], xmask[GPW];
+#pragma unroll
+  for (int i = 0; i < GPW; ++i) {
+    if (i < WPW) continue;
+    const int y0 = gpix_y[i], x0 = gpix_x[i];
+    abase[i] = (unsigned)(((((long)gpix_n[i] * A.IH + y0) * A.IW + x0) * A.ldx + A.cx0 + csrc * E) * sizeof(T));
+    unsigned ym = 0, xm = 0;
+    for (int q = 0; q < ny; ++q) ym |= (unsigned)((unsigned)(y0 + TG.ty0[tb] + q * dty) < (unsigned)A.IH) << q;
+    for (int q = 0; q < nx; ++q) xm |= (unsigned)((unsigned)(x0 + TG.tx0[tb] + q * dtx) < (unsigned)A.IW) << q;
+    ymask[i] = gvalid[i] ? ym : 0u;
+    xmask[i] = xm;
+  }
+  const unsigned wbase = (unsigned)(((size_t)(c0 + wid * 8 + lrow) * A.k_pad + csrc * E) * sizeof(T));
+  // scalar tap walk: the next K step to issue is (tap row tyi, tap column txi, chunk cb) with
+  // act_off = ((ty * IW + tx) * ldx + cb * KE) * sizeof(T)
+  int w_tyi = 0, w_txi = 0, w_cb = 0;
+  int act_off = ((TG.ty0[tb] * A.IW + TG.tx0[tb]) * A.ldx) * (int)sizeof(T);
+  const int step_x = dtx * A.ldx * (int)sizeof(T), step_y = dty * A.IW * A.ldx * (int)sizeof(T);
+  const int chunk_b = KE * (int)sizeof(T);
+#if defined(__HIP_DEVICE_COMPILE__)
+  const __amdgpu_buffer_rsrc_t xrsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)TG.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)Wt, (short)0, (int)TG.w_bytes[tb], 0x00020000);
+#endif
+
+  auto issue = [&](int ks, uint4* dst) {
+    if constexpr (SMALLC) {
+      // small Cin (stem): one K step mixes taps, per-lane tap decode
+      const int kw_off = ks * KE;
+      int k = ks * KE + csrc * E;
+      int t = k / A.Cin;
+      const int cc = k - t * A.Cin;
+      const bool tok = t < S.ntaps;
+      int kyy = t / S.kw;
+      const int ty = kyy * S.dil - S.pad;
+      const int tx = (t - kyy * S.kw) * S.dil - S.pad;
+      const void* srcs[GPW];
+#pragma unroll
+      for (int i = 0; i < GPW; ++i) {
+        const int g = wid + NW * i;
+        const int r = g * 8 + lrow;
+        const void* src;
+        if (i < WPW) {
+          src = Wt + (size_t)(c0 + r) * A.k_pad + kw_off + csrc * E;
+        } else {
+          int iy = gpix_y[i] + ty, ix = gpix_x[i] + tx;
+          bool ok = tok && gvalid[i] && (unsigned)iy < (unsigned)A.IH && (unsigned)ix < (unsigned)A.IW;
+          int iyc = min(max(iy, 0), A.IH - 1), ixc = min(max(ix, 0), A.IW - 1);
+          const T* pv = X + (((size_t)gpix_n[i] * A.IH + iyc) * A.IW + ixc) * A.ldx + A.cx0 + cc;
+          src = ok ? (const void*)pv : (const void*)&g_zero_page[lane & 7];
+        }
+        srcs[i] = src;
+      }
+#if defined(__HIP_DEVICE_COMPILE__)  // device-only builtin: the host pass would silently drop the kernel stubs
+#pragma unroll
+      for (int i = 0; i < GPW; ++i) {
+        const int g = wid + NW * i;
+        __builtin_amdgcn_global_load_lds(srcs[i], (__attribute__((address_space(3))) void*)&dst[g * 64], 16, 0, 0);
+      }
+#endif
+    } else {
+      // all offsets first (distinct registers), then the DMA issues back to back: hipcc waits
+      // vmcnt(0) before it rewrites the address VGPRs of an in-flight LDS-DMA
+      unsigned voff[GPW];
+#pragma unroll
+      for (int i = 0; i < GPW; ++i) {
+        const int g = wid + NW * i;
+        if (i < WPW) {  // weight group (compile-time)
+          voff[i] = wbase + (unsigned)(NW * i * 8) * (unsigned)(A.k_pad * sizeof(T));
+        } else {
+          const bool ok = (ymask[i] >> w_tyi) & (xmask[i] >> w_txi) & 1u;
+          voff[i] = ok ? abase[i] + (unsigned)act_off : 0x80000000u;
+        }
+      }
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+      for (int i = 0; i < GPW; ++i) {
+        const int g = wid + NW * i;
+        auto* d = (__attribute__((address_space(3))) void*)&dst[g * 64];
+        if (i < WPW)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(wrsrc, d, 16, voff[i], ks * chunk_b, 0, 0);
+        else if (ZP_ABL != 3)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(xrsrc, d, 16, voff[i], 0, 0, 0);
+      }
+#endif
+      // advance the scalar tap walk to step ks + 1 (tap-major: chunks fastest)
+      act_off += chunk_b;
+      if (++w_cb == CB) {
+        w_cb = 0;
+        act_off += step_x - CB * chunk_b;
+        if (++w_txi == nx) {
+          w_txi = 0;
+          act_off += step_y - nx * step_x;
+          ++w_tyi;
+        }
+      }
+    }
+  };
+
+  f32x4 acc[WC][WP];
+#pragma unroll
+  for (int i = 0; i < WC; ++i)
+#pragma unroll
+    for (int j = 0; j < WP; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // Three-stage ring: while step k computes from buffer k%3, the DMA of steps k+1 (issued one
+  // step earlier) and k+2 (issued now) are in flight.  End of step k: counted vmcnt(GPW) (only
+  // step k+2's loads may remain outstanding) + raw s_barrier -- never __syncthreads(), whose
+  // vmcnt(0) would drain the ring.  Buffer indices are compile-time (loop unrolled by 3) and the
+  // three buffers are distinct LDS objects, so hipcc can prove a ds_read never aliases an
+  // in-flight global_load_lds and inserts no vmcnt wait in front of it.
+  const bool pingpong = NW == 8 && !SMALLC && (flags & 8);
+  // per-lane byte offsets of the MFMA fragments inside a stage buffer: row (lane & 15) of the
+  // wave's first 16-row tile, 16 B chunk (s * 4 + lane / 16) swizzled by (row & 7) = (lane & 7);
+  // tile i / j adds i * 16 rows = i * 2048 B (an immediate of the ds_read)
+  unsigned aoff[2], boff[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    const unsigned chunk = (unsigned)(((s2 * 4 + (lane >> 4)) ^ (lane & 7)) * 16);
+    aoff[s2] = (unsigned)(wc * 16 * WC + (lane & 15)) * 128u + chunk;
+    boff[s2] = (unsigned)(TC + wp * 16 * WP + (lane & 15)) * 128u + chunk;
+  }
+  auto step = [&](auto cur_c, auto nxt_c, int ks) {
+    const bool more = ks + (STAGES - 1) < nK;
+    // next stage's DMA first (its tap offsets come from scalar loads, whose lgkmcnt wait must
+    // not also wait for this step's fragment reads)
+    if constexpr (ZP_ABL != 1) {
+      if (more) issue(ks + (STAGES - 1), bufp(nxt_c));
+    }
+    // fragment reads as inline asm: hipcc's waitcnt pass cannot prove across the loop back-edge
+    // that they miss the in-flight LDS-DMA buffers and would put a vmcnt(0) in front of them
+    const unsigned cb = lds_addr(bufp(cur_c));
+    uint4 af[2][WC], bfr[2][WP];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const unsigned pa = cb + aoff[s2], pb = cb + boff[s2];
+      static_for<WC>([&](auto i) { af[s2][i] = ds_read16<i * 2048>(pa); });
+      static_for<WP>([&](auto j) { bfr[s2][j] = ds_read16<j * 2048>(pb); });
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (pingpong) {
+      // end of the read section: fragments in registers (the other group may refill this
+      // buffer after the barrier) and every load but the newest step's retired, so the next
+      // step's buffer is complete once all waves have passed the barrier
+      if (more) vm_wait<LPS * (STAGES - 2)>();
+      else vm_wait<0>();
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (flags & 4) __builtin_amdgcn_s_setprio(1);
+    if constexpr (ZP_ABL != 2) {
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int i = 0; i < WC; ++i)
+#pragma unroll
+          for (int j = 0; j < WP; ++j) MfmaTraits<T>::mma(acc[i][j], af[s2][i], bfr[s2][j]);
+    } else {
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int i = 0; i < WC; ++i) acc[i][0][0] += __uint_as_float(af[s2][i].x ^ bfr[s2][0].y);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // keep the MFMAs in front of the wait + barrier
+    if (flags & 4) __builtin_amdgcn_s_setprio(0);
+    if (!pingpong) {
+      if (more) vm_wait<LPS * (STAGES - 2)>();
+      else vm_wait<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  issue(0, lds0);
+  if (STAGES == 3 && nK > 1) {
+    issue(1, lds1);
+    vm_wait<LPS * (STAGES - 2)>();
+  } else {
+    vm_wait<0>();
+  }
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  // Ping-pong (flags & 8, 8-wave tiles): every step is a read section (fragments + next DMA)
+  // and an MFMA section, each closed by a barrier; waves 4-7 start one barrier late, so on
+  // every SIMD (waves w and w+4 share one) one wave's MFMAs overlap the other's LDS reads.
+  if (pingpong && wid >= 4) __builtin_amdgcn_s_barrier();
+  if constexpr (STAGES == 3) {
+    for (int ks = 0; ks < nK; ks += 3) {
+      step(I0{}, I2{}, ks);
+      if (ks + 1 >= nK) break;
+      step(I1{}, I0{}, ks + 1);
+      if (ks + 2 >= nK) break;
+      step(I2{}, I1{}, ks + 2);
+    }
+  } else {
+    for (int ks = 0; ks < nK; ks += 2) {
+      step(I0{}, I1{}, ks);
+      if (ks + 1 >= nK) break;
+      step(I1{}, I0{}, ks + 1);
+    }
+  }
+
+  if (pingpong && wid < 4) __builtin_amdgcn_s_barrier();  // same barrier count for both groups
+
+  conv_epilogue<T, WC, WP, NWP>(A, S, acc, p0, c0, wc, wp, lane, M, GHW, bx);
+}
+
+// ------------------------------------------------------------------------------------
+// 3x3 stride-1 convolution with activation-strip reuse (bf16).  k_conv stages the activation
+// rows of every tap separately: 9 shifted copies of nearly the same rows per channel chunk, and
+// the L2 -> LDS stream (not the MFMA) bounds it (profiles/r01_conv_sweep.md ablations).  Here a
+// tile is TR full image rows (TP = TR * W = 256 pixels) and, per (tap row, 64-channel chunk), ONE
+// strip of TR x (W + 2d) input pixels is staged and read by the three taps of that row at column
+// offsets 0, d, 2d: 3 strips + 9 weight tiles per chunk instead of 9 + 9 tiles.
+// K steps run (tap row, chunk, tap column), tap column fastest.  Weights: STAGES-deep ring as
+// k_conv; strips: 2-deep ring, each strip issued two steps ahead of its first use.  Every wave
+// issues the same number of LDS-DMA instructions per step (padding rows load zeros), so the
+// counted vmcnt waits stay exact.  Epilogue shared with k_conv.
+// ------------------------------------------------------------------------------------
+struct strip_geo {
+  int W, TR, SW, SR, SPW;       // width, rows per tile, strip width W + 2d, strip rows, DMA instrs / wave
+  int ty0, dty, tx0, dtx, pad;  // tap grid (3 x 3) and the halo width pad = max |offset|
+  unsigned x_bytes, w_bytes;
+};
+
+template <int WC, int STAGES, int SPW>
+__global__ void __launch_bounds__(512) k_conv_strip(const zp_conv_args A, const strip_geo SG, const int flags) {
+  using T = bf16_t;
+  constexpr int WP = 4, NWP = 4, NW = 8;
+  constexpr int TC = 32 * WC, TP = 256;
+  constexpr int WPW = TC / 8 / NW;  // weight DMA instrs per wave per step
+  constexpr int SRP = 64 * SPW;     // strip rows incl. padding (8 waves x SPW instrs x 8 rows)
+  static_assert(STAGES == 2 || STAGES == 3, "weight ring");
+  __shared__ uint4 w0[TC * 8], w1[TC * 8], w2[STAGES == 3 ? TC * 8 : 1];
+  __shared__ uint4 s0[SRP * 8], s1[SRP * 8];
+  auto wbuf = [&](auto i_c) -> uint4* {
+    constexpr int i = decltype(i_c)::value % STAGES;
+    if constexpr (i == 0) return w0;
+    else if constexpr (i == 1) return w1;
+    else return w2;
+  };
+  auto sbuf = [&](auto i_c) -> uint4* {
+    constexpr int i = decltype(i_c)::value % 2;
+    if constexpr (i == 0) return s0;
+    else return s1;
+  };
+  const zp_conv_sub& S = A.sub[0];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wid / NWP, wp = wid % NWP;
+  const int GHW = A.GH * A.GW;
+  const int M = A.N * GHW;
+  const int bx = blockIdx.x, by = blockIdx.y;
+  const int p0 = bx * TP, c0 = by * TC;
+  const int n_img = p0 / GHW, y0 = (p0 - n_img * GHW) / SG.W;
+  const int CB = A.Cin / 64;
+  const int nK = 9 * CB;
+  const int lrow = lane >> 3;
+  const int csrc = (lane & 7) ^ lrow;  // weight rows: swizzle by (row & 7) = lrow
+
+#if defined(__HIP_DEVICE_COMPILE__)
+  const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)A.x, (short)0, (int)SG.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)S.w, (short)0, (int)SG.w_bytes, 0x00020000);
+#endif
+  // weight rows of this lane: row c0 + (wid + NW*i)*8 + lrow
+  const unsigned wbase = (unsigned)(((size_t)(c0 + wid * 8 + lrow) * A.k_pad + csrc * 8) * 2);
+  // strip rows of this lane: s = (wid + 8 i) * 8 + lrow -> (tr, c); input (n, y0 + ty + tr, c - pad)
+  // per strip instruction: the byte offset of the row's (tr, column) with tr packed into the low
+  // 4 bits (offsets are 16-byte multiples; tr < 16), or -1 for padding rows / columns
+  int sbase[SPW];
+  const int rowb = A.IW * A.ldx * 2;  // bytes per input row
+#pragma unroll
+  for (int i = 0; i < SPW; ++i) {
+    const int srow = (wid + 8 * i) * 8 + lrow;
+    const int tr = srow / SG.SW, c = srow - tr * SG.SW;
+    const int ix = c - SG.pad;
+    const bool ok = srow < SG.SR && (unsigned)ix < (unsigned)A.IW;
+    const int sw = (lane & 7) ^ (srow & 7);  // source-side chunk swizzle by the strip row
+    sbase[i] = ok ? ((((n_img * A.IH + y0 + tr) * A.IW + ix) * A.ldx + A.cx0 + sw * 8) * 2) | tr : -1;
+  }
+  auto issue_w = [&](int ks, uint4* dst) {
+    const int g = ks / 3, kx = ks - 3 * g, ky = g / CB, cb = g - ky * CB;
+    const int koff = ((ky * 3 + kx) * A.Cin + cb * 64) * 2;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+    for (int i = 0; i < WPW; ++i) {
+      auto* d = (__attribute__((address_space(3))) void*)&dst[(wid + NW * i) * 64];
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrsrc, d, 16, wbase + (unsigned)(NW * i * 8) * (unsigned)(A.k_pad * 2),
+                                               koff, 0, 0);
+    }
+#endif
+  };
+  auto issue_s = [&](int g, uint4* dst) {
+    const int ky = g / CB, cb = g - ky * CB;
+    const int ty = SG.ty0 + ky * SG.dty;
+    unsigned voff[SPW];
+#pragma unroll
+    for (int i = 0; i < SPW; ++i) {
+      const int tr = sbase[i] & 15;
+      const bool ok = sbase[i] >= 0 && (unsigned)(y0 + ty + tr) < (unsigned)A.IH;
+      voff[i] = ok ? (unsigned)((sbase[i] & ~15) + ty * rowb + cb * 128) : 0x80000000u;
+    }
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+    for (int i = 0; i < SPW; ++i) {
+      auto* d = (__attribute__((address_space(3))) void*)&dst[(wid + 8 * i) * 64];
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrsrc, d, 16, voff[i], 0, 0, 0);
+    }
+#endif
+  };
+
+  f32x4 acc[WC][WP];
+#pragma unroll
+  for (int i = 0; i < WC; ++i)
+#pragma unroll
+    for (int j = 0; j < WP; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // fragment offsets: A (weights) as in k_conv; B from the strip: pixel q = wp*64 + j*16 + (lane&15)
+  // -> strip row tr*SW + x + (tx + pad), chunk swizzled by that row
+  unsigned aoff[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2)
+    aoff[s2] = (unsigned)(wc * 16 * WC + (lane & 15)) * 128u + (unsigned)(((s2 * 4 + (lane >> 4)) ^ (lane & 7)) * 16);
+  // strip row of fragment j = bsrow0 + jdelta(j): the wave's 64 pixels are one image row when
+  // W >= 64, two rows of 32 when W == 32
+  int bsrow0;
+  {
+    const int q0 = wp * 16 * WP;
+    const int tr = q0 / SG.W, x0 = q0 - tr * SG.W;
+    bsrow0 = tr * SG.SW + x0 + (lane & 15) + SG.pad;
+  }
+  const int jrow = SG.W == 32 ? SG.SW - 32 : 0;  // extra offset for fragments 2, 3 when W == 32
+  const bool pingpong = (flags & 8) != 0;
+
+  // step phase PH = ks % 6 (compile-time): weight slot PH % STAGES, strip slot (PH / 3) % 2
+  auto step = [&](auto ph_c, int ks) {
+    constexpr int PH = decltype(ph_c)::value;
+    using WN = std::integral_constant<int, (PH + STAGES - 1) % 6>;
+    using SN = std::integral_constant<int, ((PH + 2) % 6) / 3>;
+    const bool more_w = ks + (STAGES - 1) < nK;
+    const bool strip_next = ((PH + 2) % 3 == 0) && ks + 2 < nK;
+    if (more_w) issue_w(ks + (STAGES - 1), wbuf(WN{}));
+    if (strip_next) issue_s((ks + 2) / 3, sbuf(SN{}));
+    const int g = ks / 3, kx = ks - 3 * g;
+    const int txo = SG.tx0 + kx * SG.dtx;
+    const unsigned cw = lds_addr(wbuf(std::integral_constant<int, PH>{}));
+    const unsigned csb = lds_addr(sbuf(std::integral_constant<int, PH / 3>{}));
+    uint4 af[2][WC], bfr[2][WP];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const unsigned pa = cw + aoff[s2];
+      static_for<WC>([&](auto i) { af[s2][i] = ds_read16<i * 2048>(pa); });
+#pragma unroll
+      for (int j = 0; j < WP; ++j) {
+        const int sr = bsrow0 + txo + 16 * j + (j >= 2 ? jrow : 0);
+        const unsigned pb = csb + (unsigned)sr * 128u + (unsigned)((((s2 * 4 + (lane >> 4)) ^ (sr & 7))) * 16);
+        bfr[s2][j] = ds_read16<0>(pb);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    // loads allowed to stay in flight at the end of this step: the ones issued for later steps
+    constexpr int OUT_S2 = ((PH + 2) % 3 == 0) ? SPW : 0;  // strip issued this step (needed at ks + 2)
+    constexpr int OUT = (STAGES == 3 ? WPW : 0) + OUT_S2;
+    // (a step whose strip slot would have been refilled past the end issued no strip)
+    auto wait_out = [&]() {
+      if (strip_next) vm_wait<OUT>();
+      else if (more_w) vm_wait<OUT - OUT_S2>();
+      else vm_wait<0>();
+    };
+    if (pingpong) {
+      wait_out();
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int i = 0; i < WC; ++i)
+#pragma unroll
+        for (int j = 0; j < WP; ++j) MfmaTraits<T>::mma(acc[i][j], af[s2][i], bfr[s2][j]);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(0);
+    if (!pingpong) wait_out();
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // prologue: strip of group 0, weights of steps 0 .. STAGES-2; the strip of group 1 is issued
+  // at step 1 (two steps ahead of step 3)
+  issue_s(0, s0);
+  issue_w(0, w0);
+  if (STAGES == 3) issue_w(1, w1);
+  if (STAGES == 3) vm_wait<WPW>();  // strip(0) and weights(0) landed; weights(1) may be in flight
+  else vm_wait<0>();
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  if (pingpong && wid >= 4) __builtin_amdgcn_s_barrier();
+  using P0 = std::integral_constant<int, 0>;
+  using P1 = std::integral_constant<int, 1>;
+  using P2 = std::integral_constant<int, 2>;
+  using P3 = std::integral_constant<int, 3>;
+  using P4 = std::integral_constant<int, 4>;
+  using P5 = std::integral_constant<int, 5>;
+  for (int ks = 0; ks < nK; ks += 6) {  // nK = 9 CB is a multiple of 3; stop after any step
+    step(P0{}, ks);
+    step(P1{}, ks + 1);
+    step(P2{}, ks + 2);
+    if (ks + 3 >= nK) break;
+    step(P3{}, ks + 3);
+    step(P4{}, ks + 4);
+    step(P5{}, ks + 5);
+  }
+  if (pingpong && wid < 4) __builtin_amdgcn_s_barrier();
+  conv_epilogue<T, WC, WP, NWP>(A, S, acc, p0, c0, wc, wp, lane, M, GHW, bx);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1113,7 +1333,11 @@ static int g_tc256_min_blocks = 512;
 // workgroups of 256 pixels (64x64 / 128x128 layers, the 64x64 transposed-conv phases: 1.1-1.2x),
 // a loss on 32x32 layers (128 workgroups for 256 CUs) and on the ASPP launch, whose four
 // sub-problems (1 vs 9 taps) are too unbalanced for 512 large tiles.
+static bool strip_eligible(const zp_conv_args& a, strip_geo* sg);
 static int conv_tc(const zp_conv_args& a) {
+  // the strip kernel (128-channel tile) stages fewer bytes per FLOP than the 256-channel k_conv
+  // tile, and its 256-channel form does not fit the register file: it takes precedence
+  if (strip_eligible(a, nullptr)) return 128;
   if (a.dtype == ZP_BF16 && a.Cout % 256 == 0 && a.Cin >= 64 && conv_tc256_enabled()) {
     const long M = (long)a.N * a.GH * a.GW;
     int tmin = ZP_MAX_TAPS, tmax = 0;
@@ -1142,6 +1366,44 @@ static int conv_flags() {
   return v;
 }
 
+// 3x3 stride-1 same-size bf16 convs on full-width tiles (W 32 / 64 / 128) whose strip of
+// TR x (W + 2 pad) pixels fits the 320-row LDS slot run k_conv_strip (256-pixel tiles).
+// ZP_CONV_STRIP=0 disables.
+static bool strip_eligible(const zp_conv_args& a, strip_geo* sg) {
+  static const int en = getenv("ZP_CONV_STRIP") ? env_int("ZP_CONV_STRIP") : 1;
+  if (!en || a.dtype != ZP_BF16 || a.nsub != 1 || a.Cin % 64 != 0 || a.Cout <= 64) return false;
+  if (a.sy != 1 || a.sx != 1 || a.GH != a.IH || a.GW != a.IW) return false;
+  const zp_conv_sub& S = a.sub[0];
+  if (S.ntaps != 9 || S.oys != 1 || S.oxs != 1 || S.oyo != 0 || S.oxo != 0 || S.OH != a.GH || S.OW != a.GW)
+    return false;
+  const int ty0 = S.ty[0], tx0 = S.tx[0], dty = S.ty[3] - S.ty[0], dtx = S.tx[1] - S.tx[0];
+  for (int t = 0; t < 9; ++t)
+    if (S.ty[t] != ty0 + (t / 3) * dty || S.tx[t] != tx0 + (t % 3) * dtx) return false;
+  const int W = a.GW;
+  if (W != 32 && W != 64 && W != 128) return false;
+  if (((long)a.GH * a.GW) % 256 != 0) return false;
+  int pad = 0;
+  for (int k = 0; k < 3; ++k) {
+    pad = max(pad, abs(ty0 + k * dty));
+    pad = max(pad, abs(tx0 + k * dtx));
+  }
+  const int TR = 256 / W, SW = W + 2 * pad, SR = TR * SW;
+  if (SR > 320) return false;
+  if (sg) {
+    sg->W = W;
+    sg->TR = TR;
+    sg->SW = SW;
+    sg->SR = SR;
+    sg->SPW = 5;
+    sg->ty0 = ty0;
+    sg->dty = dty;
+    sg->tx0 = tx0;
+    sg->dtx = dtx;
+    sg->pad = pad;
+  }
+  return true;
+}
+
 // pixel tile: 256 (8 waves) whenever the cout tile allows it.  Measured on MI355X (R34 bs32,
 // profiles/r01_conv_sweep.md): the 8-wave 3-stage tile beats the 4-wave tiles even on the
 // 32x32 layers where it leaves part of the chip idle (fewer workgroups, but 2x the MFMA work
@@ -1149,6 +1411,7 @@ static int conv_flags() {
 static int conv_tp(const zp_conv_args& a) {
   int tc = a.Cout > 64 ? 128 : (a.Cout > 32 ? 64 : 32);
   if (tc == 32) return 128;  // 32 + 256 rows do not split over 8 waves in 8-row groups
+  if (strip_eligible(a, nullptr)) return 256;
   const int ov = conv_tp_override();
   if (ov == 128 || ov == 256) return ov;
   // Cout <= 128 (one cout tile): 128-pixel tiles double the workgroup count of the 32x32 / 64x64
@@ -1237,6 +1500,15 @@ extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
   const int tc = conv_tc(a);
   const int gx = zp_conv2d_grid(&a), gy = ceil_div(a.Cout, tc);
   hipStream_t st = (hipStream_t)stream;
+  strip_geo sg{};
+  if (tc == 128 && strip_eligible(a, &sg)) {
+    sg.x_bytes = tg.x_bytes;
+    sg.w_bytes = tg.w_bytes[0];
+    const int sgx = (int)(((long)a.N * a.GH * a.GW) / 256);
+    hipLaunchKernelGGL((k_conv_strip<4, 3, 5>), dim3(sgx, gy, 1), dim3(512), 0, st, a, sg, conv_flags());
+    ZP_LAUNCH_CHECK("zp_conv2d strip");
+    return ZP_OK;
+  }
   const int nwp = conv_tp(a) / 64;
   const int stages = conv_stages(nwp);
 #define ZP_DISPATCH_ST(T, WC, NWP, ST)                                   \
@@ -1400,11 +1672,12 @@ extern "C" int zp_conv2d_stat_parts(const zp_conv_args* a) {
 }
 
 /* launch configuration zp_conv2d picks for these args (for kernel labels in reports) */
-extern "C" int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* stages) {
-  ZP_CHECK_ARG(a && tc && tp && stages, "zp_conv2d_config: null args");
+extern "C" int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* stages, int* variant) {
+  ZP_CHECK_ARG(a && tc && tp && stages && variant, "zp_conv2d_config: null args");
   *tc = conv_tc(*a);
   *tp = conv_tp(*a);
   *stages = *tc == 256 ? 2 : conv_stages(*tp / 64);
+  *variant = *tc == 128 && strip_eligible(*a, nullptr) ? 1 : 0;
   return ZP_OK;
 }
 

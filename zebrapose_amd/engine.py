@@ -226,11 +226,13 @@ class Engine:
             L.check(L.lib.zp_conv2d(C.byref(a), st), "zp_conv2d")
             e1.record()
             flops = 2.0 * x.B * plan.GH * plan.GW * sum(len(sb.taps) for sb in plan.subs) * x.C * cout
-            tc, tp, stages = C.c_int(), C.c_int(), C.c_int()
-            L.call("zp_conv2d_config", C.byref(a), C.byref(tc), C.byref(tp), C.byref(stages))
-            # rocprofv3 name: k_conv<T, WC = tc / 32, WP = 4, NWP = tp / 64, STAGES, smallC>
-            kname = (f"k_conv<{'bf16' if self.dt == L.ZP_BF16 else 'f32'},WC={tc.value // 32},WP=4,"
-                     f"NWP={tp.value // 64},ST={stages.value},smallC={int(x.C < _KE[self.dt])}>")
+            tc, tp, stages, var = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+            L.call("zp_conv2d_config", C.byref(a), C.byref(tc), C.byref(tp), C.byref(stages), C.byref(var))
+            if var.value == 1:  # rocprofv3 name: k_conv_strip<WC, STAGES, SPW = 5>
+                kname = f"k_conv_strip<bf16,WC={tc.value // 32},ST=3>"
+            else:  # rocprofv3 name: k_conv<T, WC = tc / 32, WP = 4, NWP = tp / 64, STAGES, smallC>
+                kname = (f"k_conv<{'bf16' if self.dt == L.ZP_BF16 else 'f32'},WC={tc.value // 32},WP=4,"
+                         f"NWP={tp.value // 64},ST={stages.value},smallC={int(x.C < _KE[self.dt])}>")
             geo = (f"{label}:{x.C}->{cout} taps{max(len(sb.taps) for sb in plan.subs)} "
                    f"{x.H}x{x.W}->{plan.GH}x{plan.GW}x{a.nsub}")
             self.timing.append((geo, e0, e1, flops, kname))
