@@ -627,19 +627,13 @@ __global__ void __launch_bounds__(512) k_conv_strip(const zp_conv_args A, const 
   constexpr int WPW = TC / 8 / NW;  // weight DMA instrs per wave per step
   constexpr int SRP = 64 * SPW;     // strip rows incl. padding (8 waves x SPW instrs x 8 rows)
   static_assert(STAGES == 2 || STAGES == 3, "weight ring");
-  __shared__ uint4 w0[TC * 8], w1[TC * 8], w2[STAGES == 3 ? TC * 8 : 1];
-  __shared__ uint4 s0[SRP * 8], s1[SRP * 8];
-  auto wbuf = [&](auto i_c) -> uint4* {
-    constexpr int i = decltype(i_c)::value % STAGES;
-    if constexpr (i == 0) return w0;
-    else if constexpr (i == 1) return w1;
-    else return w2;
-  };
-  auto sbuf = [&](auto i_c) -> uint4* {
-    constexpr int i = decltype(i_c)::value % 2;
-    if constexpr (i == 0) return s0;
-    else return s1;
-  };
+  // weight ring and strip ring; slots are runtime indices (ks % STAGES, group & 1): the loop is
+  // unrolled only over the 3 tap columns of a group (compile-time wait counts), which keeps the
+  // 256-channel variant inside the register file
+  __shared__ uint4 wring[STAGES * TC * 8];
+  __shared__ uint4 sring[2 * SRP * 8];
+  auto wbuf = [&](int slot) -> uint4* { return wring + slot * (TC * 8); };
+  auto sbuf = [&](int slot) -> uint4* { return sring + slot * (SRP * 8); };
   const zp_conv_sub& S = A.sub[0];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -728,19 +722,26 @@ __global__ void __launch_bounds__(512) k_conv_strip(const zp_conv_args A, const 
   const int jrow = SG.W == 32 ? SG.SW - 32 : 0;  // extra offset for fragments 2, 3 when W == 32
   const bool pingpong = (flags & 8) != 0;
 
-  // step phase PH = ks % 6 (compile-time): weight slot PH % STAGES, strip slot (PH / 3) % 2
+  // step phase PH = ks % 3 = tap column (compile-time); weight slot ks % STAGES, strip slot g & 1
   auto step = [&](auto ph_c, int ks) {
     constexpr int PH = decltype(ph_c)::value;
-    using WN = std::integral_constant<int, (PH + STAGES - 1) % 6>;
-    using SN = std::integral_constant<int, ((PH + 2) % 6) / 3>;
     const bool more_w = ks + (STAGES - 1) < nK;
     const bool strip_next = ((PH + 2) % 3 == 0) && ks + 2 < nK;
-    if (more_w) issue_w(ks + (STAGES - 1), wbuf(WN{}));
-    if (strip_next) issue_s((ks + 2) / 3, sbuf(SN{}));
-    const int g = ks / 3, kx = ks - 3 * g;
-    const int txo = SG.tx0 + kx * SG.dtx;
-    const unsigned cw = lds_addr(wbuf(std::integral_constant<int, PH>{}));
-    const unsigned csb = lds_addr(sbuf(std::integral_constant<int, PH / 3>{}));
+    if (more_w) issue_w(ks + (STAGES - 1), wbuf((ks + STAGES - 1) % STAGES));
+    if (strip_next) issue_s((ks + 2) / 3, sbuf(((ks + 2) / 3) & 1));
+    const int g = ks / 3;
+    const int txo = SG.tx0 + PH * SG.dtx;
+    const unsigned cw = lds_addr(wbuf(ks % STAGES));
+    const unsigned csb = lds_addr(sbuf(g & 1));
+    // loads allowed to stay in flight at the end of this step: the ones issued for later steps
+    constexpr int OUT_S2 = ((PH + 2) % 3 == 0) ? SPW : 0;  // strip issued this step (needed at ks + 2)
+    constexpr int OUT = (STAGES == 3 ? WPW : 0) + OUT_S2;
+    // (a step whose strip slot would have been refilled past the end issued no strip)
+    auto wait_out = [&]() {
+      if (strip_next) vm_wait<OUT>();
+      else if (more_w) vm_wait<OUT - OUT_S2>();
+      else vm_wait<0>();
+    };
     uint4 af[2][WC], bfr[2][WP];
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
@@ -755,15 +756,6 @@ __global__ void __launch_bounds__(512) k_conv_strip(const zp_conv_args A, const 
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    // loads allowed to stay in flight at the end of this step: the ones issued for later steps
-    constexpr int OUT_S2 = ((PH + 2) % 3 == 0) ? SPW : 0;  // strip issued this step (needed at ks + 2)
-    constexpr int OUT = (STAGES == 3 ? WPW : 0) + OUT_S2;
-    // (a step whose strip slot would have been refilled past the end issued no strip)
-    auto wait_out = [&]() {
-      if (strip_next) vm_wait<OUT>();
-      else if (more_w) vm_wait<OUT - OUT_S2>();
-      else vm_wait<0>();
-    };
     if (pingpong) {
       wait_out();
       __builtin_amdgcn_s_barrier();
@@ -784,9 +776,9 @@ __global__ void __launch_bounds__(512) k_conv_strip(const zp_conv_args A, const 
   };
   // prologue: strip of group 0, weights of steps 0 .. STAGES-2; the strip of group 1 is issued
   // at step 1 (two steps ahead of step 3)
-  issue_s(0, s0);
-  issue_w(0, w0);
-  if (STAGES == 3) issue_w(1, w1);
+  issue_s(0, sbuf(0));
+  issue_w(0, wbuf(0));
+  if (STAGES == 3) issue_w(1, wbuf(1));
   if (STAGES == 3) vm_wait<WPW>();  // strip(0) and weights(0) landed; weights(1) may be in flight
   else vm_wait<0>();
   __builtin_amdgcn_s_barrier();
@@ -795,17 +787,10 @@ __global__ void __launch_bounds__(512) k_conv_strip(const zp_conv_args A, const 
   using P0 = std::integral_constant<int, 0>;
   using P1 = std::integral_constant<int, 1>;
   using P2 = std::integral_constant<int, 2>;
-  using P3 = std::integral_constant<int, 3>;
-  using P4 = std::integral_constant<int, 4>;
-  using P5 = std::integral_constant<int, 5>;
-  for (int ks = 0; ks < nK; ks += 6) {  // nK = 9 CB is a multiple of 3; stop after any step
+  for (int ks = 0; ks < nK; ks += 3) {  // nK = 9 CB: whole groups
     step(P0{}, ks);
     step(P1{}, ks + 1);
     step(P2{}, ks + 2);
-    if (ks + 3 >= nK) break;
-    step(P3{}, ks + 3);
-    step(P4{}, ks + 4);
-    step(P5{}, ks + 5);
   }
   if (pingpong && wid < 4) __builtin_amdgcn_s_barrier();
   conv_epilogue<T, WC, WP, NWP>(A, S, acc, p0, c0, wc, wp, lane, M, GHW, bx);
@@ -1335,8 +1320,9 @@ static int g_tc256_min_blocks = 512;
 // sub-problems (1 vs 9 taps) are too unbalanced for 512 large tiles.
 static bool strip_eligible(const zp_conv_args& a, strip_geo* sg);
 static int conv_tc(const zp_conv_args& a) {
-  // the strip kernel (128-channel tile) stages fewer bytes per FLOP than the 256-channel k_conv
-  // tile, and its 256-channel form does not fit the register file: it takes precedence
+  // strip-eligible layers take k_conv_strip's 128-channel tile: it stages fewer bytes per FLOP than
+  // the 256-channel k_conv tile, and a 256-channel strip tile does not fit the register file
+  // (35 spilled VGPRs)
   if (strip_eligible(a, nullptr)) return 128;
   if (a.dtype == ZP_BF16 && a.Cout % 256 == 0 && a.Cin >= 64 && conv_tc256_enabled()) {
     const long M = (long)a.N * a.GH * a.GW;
