@@ -514,6 +514,78 @@ ZP_HD bool epnp_small(int m, const double (*pw)[3], const double* uu, const doub
   return ok;
 }
 
+// Parallel cyclic Jacobi on the symmetric 12x12 A (LDS), eigenvectors accumulated in V (LDS,
+// columns): threads 0..63 of the block work (6 disjoint rotations per round, circle-method
+// pairing, 11 rounds per sweep), every thread of the block takes part in the barriers.
+__device__ void par_jacobi12(double* A, double* V, double (*cs)[2], int* rotated) {
+  const int lane = threadIdx.x;
+  const bool worker = lane < 64;
+  if (worker)
+    for (int e = lane; e < 144; e += 64) V[e] = (e / 12 == e % 12) ? 1.0 : 0.0;
+  __syncthreads();
+  for (int sweep = 0; sweep < 40; ++sweep) {
+    if (lane == 0) *rotated = 0;
+    __syncthreads();
+    for (int r = 0; r < 11; ++r) {
+      if (lane < 6) {
+        const int p = lane == 0 ? 11 : (r + lane) % 11;
+        const int q = lane == 0 ? r : (r - lane + 11) % 11;
+        const double apq = A[p * 12 + q], app = A[p * 12 + p], aqq = A[q * 12 + q];
+        double c = 1.0, sn = 0.0;
+        if (!(fabs(apq) <= 1e-17 * sqrt(fabs(app * aqq)) || apq == 0.0)) {
+          const double theta = (aqq - app) / (2.0 * apq);
+          const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+          c = 1.0 / sqrt(t * t + 1.0);
+          sn = t * c;
+          *rotated = 1;
+        }
+        cs[lane][0] = c;
+        cs[lane][1] = sn;
+      }
+      __syncthreads();
+      if (worker)
+        for (int job = lane; job < 72; job += 64) {  // rows p, q of the 6 pairs
+          const int k = job / 12, j = job % 12;
+          const int p = k == 0 ? 11 : (r + k) % 11, q = k == 0 ? r : (r - k + 11) % 11;
+          const double c = cs[k][0], sn = cs[k][1];
+          const double ap = A[p * 12 + j], aq = A[q * 12 + j];
+          A[p * 12 + j] = c * ap - sn * aq;
+          A[q * 12 + j] = sn * ap + c * aq;
+        }
+      __syncthreads();
+      if (worker)
+        for (int job = lane; job < 72; job += 64) {  // columns p, q, and V
+          const int k = job / 12, i = job % 12;
+          const int p = k == 0 ? 11 : (r + k) % 11, q = k == 0 ? r : (r - k + 11) % 11;
+          const double c = cs[k][0], sn = cs[k][1];
+          const double ap = A[i * 12 + p], aq = A[i * 12 + q];
+          A[i * 12 + p] = c * ap - sn * aq;
+          A[i * 12 + q] = sn * ap + c * aq;
+          const double vp = V[i * 12 + p], vq = V[i * 12 + q];
+          V[i * 12 + p] = c * vp - sn * vq;
+          V[i * 12 + q] = sn * vp + c * vq;
+        }
+      __syncthreads();
+    }
+    if (!*rotated) break;
+  }
+}
+
+// the 4 eigenvectors of the smallest eigenvalues (diagonal of the rotated A), smallest first
+__device__ void null4(const double* A, const double* V, double* v4) {
+  int ord[12];
+  for (int i = 0; i < 12; ++i) ord[i] = i;
+  for (int i = 0; i < 12; ++i)
+    for (int j = i + 1; j < 12; ++j)
+      if (A[ord[j] * 12 + ord[j]] > A[ord[i] * 12 + ord[i]]) {
+        const int t = ord[i];
+        ord[i] = ord[j];
+        ord[j] = t;
+      }
+  for (int i = 0; i < 4; ++i)
+    for (int k = 0; k < 12; ++k) v4[12 * i + k] = V[k * 12 + ord[11 - i]];
+}
+
 // One wave per hypothesis: lane 0 builds M^T M from the 5-point subset, the 64 lanes run a
 // parallel cyclic Jacobi on it (6 disjoint rotations per round, circle-method pairing, 11 rounds
 // per sweep) with the matrix in LDS, lane 0 finishes EPnP from the 4-vector null space.  (A
@@ -563,66 +635,10 @@ __global__ void __launch_bounds__(64) k_pnp_hyp(const PnpArgs a) {
     if (lane == 0) a.mvalid[mi] = 0;
     return;
   }
-  for (int e = lane; e < 144; e += 64) V[e] = (e / 12 == e % 12) ? 1.0 : 0.0;
-  __syncthreads();
-  for (int sweep = 0; sweep < 40; ++sweep) {
-    if (lane == 0) rotated = 0;
-    __syncthreads();
-    for (int r = 0; r < 11; ++r) {
-      if (lane < 6) {
-        const int p = lane == 0 ? 11 : (r + lane) % 11;
-        const int q = lane == 0 ? r : (r - lane + 11) % 11;
-        const double apq = A[p * 12 + q], app = A[p * 12 + p], aqq = A[q * 12 + q];
-        double c = 1.0, sn = 0.0;
-        if (!(fabs(apq) <= 1e-17 * sqrt(fabs(app * aqq)) || apq == 0.0)) {
-          const double theta = (aqq - app) / (2.0 * apq);
-          const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-          c = 1.0 / sqrt(t * t + 1.0);
-          sn = t * c;
-          rotated = 1;
-        }
-        cs[lane][0] = c;
-        cs[lane][1] = sn;
-      }
-      __syncthreads();
-      for (int job = lane; job < 72; job += 64) {  // rows p, q of the 6 pairs
-        const int k = job / 12, j = job % 12;
-        const int p = k == 0 ? 11 : (r + k) % 11, q = k == 0 ? r : (r - k + 11) % 11;
-        const double c = cs[k][0], sn = cs[k][1];
-        const double ap = A[p * 12 + j], aq = A[q * 12 + j];
-        A[p * 12 + j] = c * ap - sn * aq;
-        A[q * 12 + j] = sn * ap + c * aq;
-      }
-      __syncthreads();
-      for (int job = lane; job < 72; job += 64) {  // columns p, q, and V
-        const int k = job / 12, i = job % 12;
-        const int p = k == 0 ? 11 : (r + k) % 11, q = k == 0 ? r : (r - k + 11) % 11;
-        const double c = cs[k][0], sn = cs[k][1];
-        const double ap = A[i * 12 + p], aq = A[i * 12 + q];
-        A[i * 12 + p] = c * ap - sn * aq;
-        A[i * 12 + q] = sn * ap + c * aq;
-        const double vp = V[i * 12 + p], vq = V[i * 12 + q];
-        V[i * 12 + p] = c * vp - sn * vq;
-        V[i * 12 + q] = sn * vp + c * vq;
-      }
-      __syncthreads();
-    }
-    if (!rotated) break;
-  }
+  par_jacobi12(A, V, cs, &rotated);
   if (lane != 0) return;
-  // the 4 smallest eigenpairs, smallest first (stable selection over the diagonal)
-  int ord[12];
-  for (int i = 0; i < 12; ++i) ord[i] = i;
-  for (int i = 0; i < 12; ++i)
-    for (int j = i + 1; j < 12; ++j)
-      if (A[ord[j] * 12 + ord[j]] > A[ord[i] * 12 + ord[i]]) {
-        const int t = ord[i];
-        ord[i] = ord[j];
-        ord[j] = t;
-      }
   double v4[48], cw[12];
-  for (int i = 0; i < 4; ++i)
-    for (int k = 0; k < 12; ++k) v4[12 * i + k] = V[k * 12 + ord[11 - i]];
+  null4(A, V, v4);
   for (int k = 0; k < 12; ++k) cw[k] = cws[k];
   double ccs[36];
   epnp_betas_null(v4, cw, ccs);
@@ -805,8 +821,17 @@ __global__ void __launch_bounds__(256) k_pnp_refine(const PnpArgs a) {
     }
   }
   block_sum<94>(s3, sh);
+  __shared__ double Aj[144], Vj[144], csj[6][2];
+  __shared__ int rotj;
+  if (threadIdx.x == 0)
+    for (int i = 0; i < 12; ++i)
+      for (int j = i; j < 12; ++j) Aj[i * 12 + j] = Aj[j * 12 + i] = s3[tri_index(i, j)];
+  __syncthreads();
+  par_jacobi12(Aj, Vj, csj, &rotj);
   if (threadIdx.x == 0) {
-    epnp_betas(s3, cws, ccs);
+    double v4[48];
+    null4(Aj, Vj, v4);
+    epnp_betas_null(v4, cws, ccs);
     for (int N = 0; N < 3; ++N) {
       double Rm[9], t[3];
       epnp_pose(ccs + 12 * N, a0, s3 + 82, s3 + 78, mean, cnt, Rm, t);
