@@ -12,7 +12,9 @@ backward, Adam; DDP over RCCL when N > 1), the dominant kernel's roofline (HIP e
 launches over a timed pass), and the CPU baseline (the oracle restatement on the host cores,
 rank 0, N = 1, bounded sample).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-train] [--no-cpu]
+Also the configs[4] leg (rank 0, N = 1): R50 fp16 batched multi-object inference + decode + PnP.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-train] [--no-cpu] [--no-multi]
     torchrun --nproc-per-node N bench.py --gpus N ...
 """
 from __future__ import annotations
@@ -34,6 +36,7 @@ os.environ.setdefault("ZP_QUIET", "1")
 
 PEAK = {"bf16": 2516.6, "fp32": 157.3}  # TFLOP/s dense MFMA (256 CU x 4 SIMD x 2.4 GHz; MI355X_MICROARCH.md)
 FWD_GFLOP_PER_CROP = 109.136  # 2 x 54,568,026,112 MAC per 256x256 crop (R34)
+R50_GFLOP_PER_CROP = 747.68  # ResNet50_OS8 + ASPP_50 forward per crop
 
 
 def parse():
@@ -49,6 +52,9 @@ def parse():
     ap.add_argument("--train-steps", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--layer-report", default=None, help="write per-launch conv timings (JSON) here")
+    ap.add_argument("--no-multi", action="store_true", help="skip the configs[4] multi-object leg")
+    ap.add_argument("--mo-objects", type=int, default=30)
+    ap.add_argument("--mo-crops", type=int, default=8, help="crops per object per step (configs[4] leg)")
     return ap.parse_args()
 
 
@@ -86,6 +92,69 @@ def kernel_name(dt, cout, cin_l):
     wc = 4 if cout > 64 else (2 if cout > 32 else 1)
     small = cin_l < (64 if dt == "bf16" else 32)
     return f"k_conv<{'bf16' if dt == 'bf16' else 'f32'},WC={wc},WP=4,smallC={int(small)}>"
+
+
+def _device_init_(net, seed):
+    """Synthetic weights generated on the device (SURVEY §8d recipe: He-normal convs, BN
+    gamma~U(0.5,1.5), beta~N(0,0.1)); used for the 30 R50 objects of the configs[4] leg, whose
+    f32 masters (41 GB) are never built on the host."""
+    g = torch.Generator(device=next(net.parameters()).device).manual_seed(seed)
+    with torch.no_grad():
+        for m in net.modules():
+            if isinstance(m, (torch.nn.Conv2d, torch.nn.ConvTranspose2d)):
+                w = m.weight
+                fan = (w.shape[1] if isinstance(m, torch.nn.Conv2d) else w.shape[0] / 4.0) * w.shape[2] * w.shape[3]
+                w.normal_(0.0, float(np.sqrt(2.0 / fan)), generator=g)
+                if m.bias is not None:
+                    m.bias.normal_(0.0, 0.01, generator=g)
+            elif isinstance(m, torch.nn.BatchNorm2d):
+                m.weight.uniform_(0.5, 1.5, generator=g)
+                m.bias.normal_(0.0, 0.1, generator=g)
+                m.running_mean.zero_()
+                m.running_var.fill_(1.0)
+                m.num_batches_tracked.zero_()
+
+
+def multi_object_leg(args, dev):
+    """configs[4]: ResNet50 + ASPP_50, fp16 MFMA, batched multi-object inference (T-LESS-style 30
+    objects, one weight set + LUT each) with the code->vertex decode and PnP on the device
+    (zebrapose_amd/multi_object.py).  One step = mo_crops crops of every object, grouped by object,
+    one forward per object, one decode and one PnP launch over the whole batch."""
+    from zebrapose_amd.model.BinaryCodeNet import BinaryCodeNet_Deeplab
+    from zebrapose_amd.multi_object import MultiObjectPose
+    nobj, per = args.mo_objects, args.mo_crops
+    B = nobj * per
+    x = synthetic_crops(B, 256, dev, seed=500)
+    nets = []
+    for o in range(nobj):
+        with torch.device("meta"):
+            n = BinaryCodeNet_Deeplab(50, 16, 2, concat=True, output_kernel_size=1, precision="fp16")
+        n = n.to_empty(device=dev)
+        _device_init_(n, 1000 + o)
+        calibrate_bn(n, x[o * per:(o + 1) * per])
+        nets.append(n)
+    luts = [synthetic_lut(o) for o in range(nobj)]
+    mo = MultiObjectPose(nets, luts, precision="fp16")
+    rng = np.random.default_rng(11)
+    obj = rng.permutation(np.repeat(np.arange(nobj), per))  # crops arrive interleaved
+    side = rng.integers(64, 401, B)
+    bb = np.stack([rng.integers(0, 300, B), rng.integers(0, 200, B), side, side], 1)
+    mo(x, obj, bb)
+    torch.cuda.synchronize()
+    steps = 3
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = mo(x, obj, bb)
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / steps
+    res = {"workload": f"configs[4]: R50+ASPP_50 fp16, {nobj} objects x {per} crops (256x256) per step, "
+                       "grouped forward + one decode + one PnP launch", "crops_per_s": round(B / el, 1),
+           "ms_per_step": round(el * 1e3, 2), "steps": steps, "dtype": "f16",
+           "network_tflops": round(R50_GFLOP_PER_CROP * 1e9 * B / el / 1e12, 1),
+           "pnp_success": int(out["success"].sum().item())}
+    del mo, nets
+    torch.cuda.empty_cache()
+    return res
 
 
 def main():
@@ -234,6 +303,11 @@ def main():
                  "parallelism": f"ddp{world}" if world > 1 else "single"}
         del ts, tnet
 
+    # ------------------------------------------------------------------ configs[4] multi-object leg (extra)
+    multi = None
+    if rank == 0 and world == 1 and not args.no_multi:
+        multi = multi_object_leg(args, dev)
+
     # ------------------------------------------------------------------ CPU baseline (rank 0, N = 1)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -269,7 +343,8 @@ def main():
                            "model": "BinaryCodeNet_Deeplab(34, 16, 2, concat=True)", "global_batch": world * B,
                            "per_gpu_batch": B, "input": f"{S}x{S}", "parallelism": f"replicas{world}",
                            "correspondences_last_step": n_corr},
-                "roofline": roofline, "cpu_baseline": cpu, "train": train, "pnp": pnp_res}
+                "roofline": roofline, "cpu_baseline": cpu, "train": train, "pnp": pnp_res,
+                "multi_object": multi}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -49,6 +49,7 @@ extern "C" {
 /* element types of activations / packed weights */
 #define ZP_F32 0
 #define ZP_BF16 1
+#define ZP_F16 2 /* IEEE fp16 storage + v_mfma_f32_16x16x32_f16; inference (forward) kernels only */
 
 /* zp_conv_args.out_mode */
 #define ZP_OUT_NHWC 0       /* y[n, oy, ox, cy0 + c] (ldy elements per pixel), dtype of the call */
@@ -78,7 +79,7 @@ typedef struct zp_conv_sub {
 } zp_conv_sub;
 
 typedef struct zp_conv_args {
-  int dtype;            /* ZP_F32 (exact-f32 MFMA path) or ZP_BF16 (bf16 MFMA, fp32 accumulate) */
+  int dtype;            /* ZP_F32 (exact-f32 MFMA path), ZP_BF16 or ZP_F16 (16-bit MFMA, fp32 accumulate) */
   const void* x;        /* input NHWC */
   int ldx, cx0, IH, IW, Cin;   /* Cin: multiple of 64 (bf16) / 32 (f32), or 8 (small-Cin path) */
   int N, GH, GW, sy, sx;       /* GEMM grid (pixels) and input stride */

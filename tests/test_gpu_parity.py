@@ -94,6 +94,50 @@ def test_forward_bf16_within_conditioning_band(net_and_state, golden):
         assert agree >= 0.90, agree
 
 
+def test_forward_fp16_within_conditioning_band(net_and_state, golden):
+    """fp16 (configs[4] dtype): as bf16 but with an 11-bit mantissa, so a tighter band."""
+    net, _ = net_and_state
+    net.set_precision("fp16")
+    f = golden("r34_fwd64.npz")
+    with torch.no_grad():
+        m, c = net(torch.from_numpy(f["fwd64_x"]).cuda())
+    net.set_precision("fp32")
+    for got, ref in ((m.cpu().numpy(), f["fwd64_mask"]), (c.cpu().numpy(), f["fwd64_code"])):
+        assert np.isfinite(got).all()
+        rel = np.linalg.norm(got - ref) / np.linalg.norm(ref)
+        print(f"fp16 rel-L2 {rel:.4g}")
+        assert rel <= 0.06, rel
+        out = np.abs(ref) > 0.25
+        agree = ((got > THR) == (ref > THR))[out].mean()
+        assert agree >= 0.97, agree
+
+
+def test_r50_forward_fp16_within_band(golden):
+    """configs[4] network: ResNet50_OS8 + ASPP_50 in fp16 against the reference's 64x64 forward."""
+    from oracle import ref_cpu
+    from zebrapose_amd.model.BinaryCodeNet import BinaryCodeNet_Deeplab
+    f = golden("r50_fwd64.npz")
+    sd = ref_cpu.synthetic_state(50, 16, 0, dict(golden("r50_bn_buffers.npz")))
+    net = BinaryCodeNet_Deeplab(50, 16, 2, concat=True, output_kernel_size=1, precision="fp16")
+    net.load_state_dict(sd)
+    net = net.cuda().eval()
+    with torch.no_grad():
+        m, c = net(torch.from_numpy(f["fwd64_x"]).cuda())
+    for got, ref in ((m.cpu().numpy(), f["fwd64_mask"]), (c.cpu().numpy(), f["fwd64_code"])):
+        assert np.isfinite(got).all()
+        rel = np.linalg.norm(got - ref) / np.linalg.norm(ref)
+        print(f"r50 fp16 rel-L2 {rel:.4g}")
+        assert rel <= 0.06, rel
+        out = np.abs(ref) > 0.25
+        agree = ((got > THR) == (ref > THR))[out].mean()
+        assert agree >= 0.97, agree
+    net.train()
+    with pytest.raises(RuntimeError, match="inference-only"):
+        net(torch.from_numpy(f["fwd64_x"]).cuda())
+    del net
+    torch.cuda.empty_cache()
+
+
 def test_decode_matches_reference_exactly(golden):
     from zebrapose_amd.decode import Decoder
     d = golden("decode.npz")

@@ -145,11 +145,39 @@ def test_unit(gpu, geom, prec, train, tile_mode):
     assert not errs, "; ".join(errs)
 
 
-@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("geom", GEOMS, ids=[f"{g[0]}{g[1]}-{g[2]}k{g[3]}s{g[4]}d{g[6]}" for g in GEOMS])
+def test_unit_fp16_eval(gpu, geom, tile_mode):
+    """fp16 (inference-only dtype, configs[4]): eval-mode conv + folded BN + residual + ReLU, fp16
+    NHWC in / out, v_mfma_f32_16x16x32_f16 -- against the fp32 CPU reference on the same
+    fp16-representable inputs; 11-bit mantissa -> 4e-3 of the output scale."""
+    from zebrapose_amd.engine import Engine, Unit, Act
+    kind, cin, cout, k, s, p, d, bias, H = geom
+    torch.manual_seed(0)
+    B = 2 if H <= 32 else 1
+    conv, bn = _mk(kind, cin, cout, k, s, p, d, bias)
+    x = torch.randn(B, cin, H, H).half().float()
+    unit = Unit(conv, bn, relu=True)
+    OH, OW = unit.out_hw(H, H)
+    use_res = (kind == "conv" and s == 1 and cin == cout)
+    res = torch.randn(B, cout, OH, OW).half().float() if use_res else None
+    y_ref, _, _ = _ref_unit(kind, conv, bn, x, res, True, False, s, p, d)
+    convg, bng = conv.to(gpu).eval(), bn.to(gpu).eval()
+    eng = Engine(torch.nn.Module(), torch.float16)
+    xa = Act(x.permute(0, 2, 3, 1).contiguous().to(gpu, torch.float16))
+    ra = Act(res.permute(0, 2, 3, 1).contiguous().to(gpu, torch.float16)) if res is not None else None
+    oa = Act(torch.empty(B, OH, OW, cout, device=gpu, dtype=torch.float16))
+    eng.unit_fwd(unit, xa, oa, None, res=ra)
+    y = oa.buf.float().permute(0, 3, 1, 2).cpu()
+    scale = y_ref.abs().max().item()
+    err = (y - y_ref.detach()).abs().max().item()
+    assert err <= 4e-3 * max(1.0, scale), f"forward max|d| {err} (scale {scale})"
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16", "fp16"])
 def test_maxpool(gpu, prec):
     from zebrapose_amd import _lib as L
     torch.manual_seed(1)
-    dt = torch.float32 if prec == "fp32" else torch.bfloat16
+    dt = {"fp32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16}[prec]
     x = torch.randn(2, 64, 17, 16).to(dt).float()
     xx = x.clone().requires_grad_(True)
     y = F.max_pool2d(xx, 3, 2, 1)
@@ -161,6 +189,11 @@ def test_maxpool(gpu, prec):
     dc = L.dtype_code(dt)
     L.call("zp_maxpool3s2", xd.data_ptr(), 2, 17, 16, 64, 0, 64, dc, yd.data_ptr(), OH, OW, 64, 0, L.stream_ptr())
     assert torch.equal(yd.float().permute(0, 3, 1, 2).cpu(), y.detach())
+    if prec == "fp16":  # inference-only dtype: the backward entry point refuses it
+        with pytest.raises(RuntimeError, match="inference-only"):
+            L.call("zp_maxpool3s2_bwd", xd.data_ptr(), 64, 0, yd.data_ptr(), 64, 0, 2, 17, 16, 64, OH, OW, dc,
+                   xd.data_ptr(), 64, 0, 1, L.stream_ptr())
+        return
     gd = g.permute(0, 2, 3, 1).contiguous().to(gpu, dt)
     dx = torch.zeros_like(xd)
     L.call("zp_maxpool3s2_bwd", xd.data_ptr(), 64, 0, gd.data_ptr(), 64, 0, 2, 17, 16, 64, OH, OW, dc, dx.data_ptr(), 64,

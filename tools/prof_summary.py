@@ -27,13 +27,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def bench_label(name):
     """'void zp::k_conv<unsigned short, 4, 4, 4, 3, false>(zp_conv_args)' ->
     'k_conv<bf16,WC=4,WP=4,NWP=4,ST=3,smallC=0>' (the label bench.py / engine.py use)."""
-    m = re.search(r"k_conv_strip<(\d+), (\d+), (\d+)>", name)
+    tn = {"unsigned short": "bf16", "_Float16": "f16", "float": "f32"}
+    m = re.search(r"k_conv_strip<(unsigned short|_Float16), (\d+), (\d+), (\d+)>", name)
     if m:
-        return f"k_conv_strip<bf16,WC={m.group(1)},ST={m.group(2)}>"
-    m = re.search(r"k_conv<(unsigned short|float), (\d+), (\d+), (\d+), (\d+), (true|false)>", name)
+        return f"k_conv_strip<{tn[m.group(1)]},WC={m.group(2)},ST={m.group(3)}>"
+    m = re.search(r"k_conv<(unsigned short|_Float16|float), (\d+), (\d+), (\d+), (\d+), (true|false)>", name)
     if not m:
         return None
-    t = "bf16" if m.group(1) == "unsigned short" else "f32"
+    t = tn[m.group(1)]
     return (f"k_conv<{t},WC={m.group(2)},WP={m.group(3)},NWP={m.group(4)},ST={m.group(5)},"
             f"smallC={int(m.group(6) == 'true')}>")
 

@@ -14,7 +14,7 @@ import torch  # noqa: F401  (load torch's HIP runtime first; libzp binds to the 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ZP_LIB", os.path.join(_HERE, "libzp.so"))
 
-ZP_F32, ZP_BF16 = 0, 1
+ZP_F32, ZP_BF16, ZP_F16 = 0, 1, 2
 ZP_OUT_NHWC, ZP_OUT_HEAD_NCHW, ZP_OUT_NHWC_F32 = 0, 1, 2
 MAX_TAPS, MAX_SUB = 64, 4
 
@@ -158,4 +158,6 @@ def dtype_code(dt) -> int:
         return ZP_F32
     if dt == torch.bfloat16:
         return ZP_BF16
+    if dt == torch.float16:
+        return ZP_F16
     raise ValueError(f"unsupported activation dtype {dt}")

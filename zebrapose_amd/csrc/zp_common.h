@@ -7,7 +7,9 @@
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
 typedef unsigned short bf16_t;  // bf16 storage
+typedef _Float16 f16_t;         // IEEE fp16 (inference-only compute dtype ZP_F16)
 
 namespace zp {
 
@@ -44,6 +46,24 @@ template <> struct Elem<float> {
 template <> struct Elem<bf16_t> {
   static __device__ __forceinline__ float ld(const bf16_t* p) { return bf2f(*p); }
   static __device__ __forceinline__ bf16_t cvt(float v) { return f2bf(v); }
+};
+
+template <> struct Elem<f16_t> {
+  static __device__ __forceinline__ float ld(const f16_t* p) { return (float)*p; }
+  static __device__ __forceinline__ f16_t cvt(float v) { return (f16_t)v; }  // RNE
+};
+
+// 16-bit storage formats as raw bits: from(bits) -> f32, to(f32) -> bits.  H16<float> exists only
+// so that runtime-dead 16-bit branches of f32 instantiations compile.
+template <typename T> struct H16 {
+  static __device__ __forceinline__ float from(uint32_t u) { return bf2f((bf16_t)u); }
+  static __device__ __forceinline__ uint32_t to(float v) { return f2bf(v); }
+};
+template <> struct H16<f16_t> {
+  static __device__ __forceinline__ float from(uint32_t u) {
+    return (float)__builtin_bit_cast(f16_t, (unsigned short)u);
+  }
+  static __device__ __forceinline__ uint32_t to(float v) { return __builtin_bit_cast(unsigned short, (f16_t)v); }
 };
 
 inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }

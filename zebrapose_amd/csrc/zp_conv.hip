@@ -31,6 +31,13 @@ template <> struct MfmaTraits<bf16_t> {
                                                   acc, 0, 0, 0);
   }
 };
+template <> struct MfmaTraits<f16_t> {
+  static constexpr int E = 8;
+  static __device__ __forceinline__ void mma(f32x4& acc, const uint4& a, const uint4& b) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b),
+                                                 acc, 0, 0, 0);
+  }
+};
 template <> struct MfmaTraits<float> {
   static constexpr int E = 4;
   // 16 B chunk = 4 consecutive k of one row; element e is k-substep e for every lane
@@ -171,12 +178,12 @@ __device__ __forceinline__ void conv_epilogue(const zp_conv_args& A, const zp_co
 #pragma unroll
           for (int r = 0; r < 8; ++r) v[r] = v[r] * sc[r] + sh[r];
           if (A.res) {
-            const uint4 rv = *(const uint4*)((const bf16_t*)A.res + pix * A.ldr + A.cr0 + cs);
+            const uint4 rv = *(const uint4*)((const unsigned short*)A.res + pix * A.ldr + A.cr0 + cs);
             const uint32_t rw[4] = {rv.x, rv.y, rv.z, rv.w};
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              v[2 * r] += __uint_as_float(rw[r] << 16);
-              v[2 * r + 1] += __uint_as_float(rw[r] & 0xffff0000u);
+              v[2 * r] += H16<T>::from(rw[r] & 0xffffu);
+              v[2 * r + 1] += H16<T>::from(rw[r] >> 16);
             }
           }
           if (A.relu) {
@@ -185,8 +192,8 @@ __device__ __forceinline__ void conv_epilogue(const zp_conv_args& A, const zp_co
           }
           uint32_t o[4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) o[r] = (uint32_t)f2bf(v[2 * r]) | ((uint32_t)f2bf(v[2 * r + 1]) << 16);
-          *(uint4*)((bf16_t*)S.y + pix * S.ldy + S.cy0 + cs) = make_uint4(o[0], o[1], o[2], o[3]);
+          for (int r = 0; r < 4; ++r) o[r] = H16<T>::to(v[2 * r]) | (H16<T>::to(v[2 * r + 1]) << 16);
+          *(uint4*)((unsigned short*)S.y + pix * S.ldy + S.cy0 + cs) = make_uint4(o[0], o[1], o[2], o[3]);
         }
       }
     }
@@ -242,13 +249,13 @@ __device__ __forceinline__ void conv_epilogue(const zp_conv_args& A, const zp_co
             if (cf + r < A.Cout) Y[r] = v[r];
         }
       } else {
-        bf16_t b[4];
+        unsigned short b[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          b[r] = f2bf(v[r]);
-          v[r] = bf2f(b[r]);  // statistics of the stored value
+          b[r] = (unsigned short)H16<T>::to(v[r]);
+          v[r] = H16<T>::from(b[r]);  // statistics of the stored value
         }
-        bf16_t* Y = (bf16_t*)S.y + pix * S.ldy + S.cy0 + cf;
+        unsigned short* Y = (unsigned short*)S.y + pix * S.ldy + S.cy0 + cf;
         if (cf + 3 < A.Cout) {
           *(uint2*)Y = make_uint2((uint32_t)b[0] | ((uint32_t)b[1] << 16), (uint32_t)b[2] | ((uint32_t)b[3] << 16));
         } else {
@@ -280,7 +287,7 @@ __device__ __forceinline__ void conv_epilogue(const zp_conv_args& A, const zp_co
         for (int j = 0; j < WP; ++j) {
           const bool ok = p0 + wp * 16 * WP + j * 16 + (lane & 15) < M;
           float v = acc[i][j][r];
-          if (sizeof(T) == 2 && A.out_mode != ZP_OUT_NHWC_F32) v = bf2f(f2bf(v));  // stored value
+          if (sizeof(T) == 2 && A.out_mode != ZP_OUT_NHWC_F32) v = H16<T>::from(H16<T>::to(v));  // stored value
           vv[j] = ok ? v : 0.f;
           sm += vv[j];
         }
@@ -619,9 +626,8 @@ struct strip_geo {
   unsigned x_bytes, w_bytes;
 };
 
-template <int WC, int STAGES, int SPW>
+template <typename T, int WC, int STAGES, int SPW>
 __global__ void __launch_bounds__(512) k_conv_strip(const zp_conv_args A, const strip_geo SG, const int flags) {
-  using T = bf16_t;
   constexpr int WP = 4, NWP = 4, NW = 8;
   constexpr int TC = 32 * WC, TP = 256;
   constexpr int WPW = TC / 8 / NW;  // weight DMA instrs per wave per step
@@ -1294,7 +1300,7 @@ static void launch_conv(const zp_conv_args& a, const conv_taps& tg, int gx, int 
 // 256 x 256 tile (bf16 only): 64 KB per LDS stage, so a 2-deep ring
 template <typename T>
 static void launch_conv_tc256(const zp_conv_args& a, const conv_taps& tg, int gx, int gy, hipStream_t st) {
-  if constexpr (std::is_same<T, bf16_t>::value) launch_conv<T, 8, 4, 2, false>(a, tg, gx, gy, st);
+  if constexpr (sizeof(T) == 2) launch_conv<T, 8, 4, 2, false>(a, tg, gx, gy, st);
 }
 
 // Tuning overrides for sweeps (read once): ZP_CONV_TP=128|256 forces the pixel tile,
@@ -1324,7 +1330,7 @@ static int conv_tc(const zp_conv_args& a) {
   // the 256-channel k_conv tile, and a 256-channel strip tile does not fit the register file
   // (35 spilled VGPRs)
   if (strip_eligible(a, nullptr)) return 128;
-  if (a.dtype == ZP_BF16 && a.Cout % 256 == 0 && a.Cin >= 64 && conv_tc256_enabled()) {
+  if (a.dtype != ZP_F32 && a.Cout % 256 == 0 && a.Cin >= 64 && conv_tc256_enabled()) {
     const long M = (long)a.N * a.GH * a.GW;
     int tmin = ZP_MAX_TAPS, tmax = 0;
     for (int s = 0; s < a.nsub; ++s) {
@@ -1357,7 +1363,7 @@ static int conv_flags() {
 // ZP_CONV_STRIP=0 disables.
 static bool strip_eligible(const zp_conv_args& a, strip_geo* sg) {
   static const int en = getenv("ZP_CONV_STRIP") ? env_int("ZP_CONV_STRIP") : 1;
-  if (!en || a.dtype != ZP_BF16 || a.nsub != 1 || a.Cin % 64 != 0 || a.Cout <= 64) return false;
+  if (!en || a.dtype == ZP_F32 || a.nsub != 1 || a.Cin % 64 != 0 || a.Cout <= 64) return false;
   if (a.sy != 1 || a.sx != 1 || a.GH != a.IH || a.GW != a.IW) return false;
   const zp_conv_sub& S = a.sub[0];
   if (S.ntaps != 9 || S.oys != 1 || S.oxs != 1 || S.oyo != 0 || S.oxo != 0 || S.OH != a.GH || S.OW != a.GW)
@@ -1403,7 +1409,7 @@ static int conv_tp(const zp_conv_args& a) {
   // Cout <= 128 (one cout tile): 128-pixel tiles double the workgroup count of the 32x32 / 64x64
   // layers (tools/conv_micro.py: 128->128 @32x32 36 -> 24 us, 64->64 @64x64 28.6 -> 26.3 us);
   // the small-Cin stem keeps 256
-  const int E = a.dtype == ZP_BF16 ? 8 : 4;
+  const int E = a.dtype == ZP_F32 ? 4 : 8;
   if (a.Cout <= 128 && a.Cin >= 8 * E) return 128;
   return 256;
 }
@@ -1425,11 +1431,11 @@ extern "C" int zp_conv2d_grid(const zp_conv_args* a) {
 extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
   ZP_CHECK_ARG(ap != nullptr, "zp_conv2d: null args");
   const zp_conv_args& a = *ap;
-  ZP_CHECK_ARG(a.dtype == ZP_F32 || a.dtype == ZP_BF16, "zp_conv2d: bad dtype %d", a.dtype);
+  ZP_CHECK_ARG(a.dtype == ZP_F32 || a.dtype == ZP_BF16 || a.dtype == ZP_F16, "zp_conv2d: bad dtype %d", a.dtype);
   ZP_CHECK_ARG(a.nsub >= 1 && a.nsub <= ZP_MAX_SUB, "zp_conv2d: nsub %d", a.nsub);
   ZP_CHECK_ARG(a.x && a.N > 0 && a.GH > 0 && a.GW > 0 && a.IH > 0 && a.IW > 0 && a.Cout > 0,
                "zp_conv2d: bad geometry");
-  const int E = a.dtype == ZP_BF16 ? 8 : 4, KE = 8 * E;
+  const int E = a.dtype == ZP_F32 ? 4 : 8, KE = 8 * E;
   const bool smallc = a.Cin < KE;
   ZP_CHECK_ARG(a.Cin > 0 && a.Cin % E == 0 && (smallc || a.Cin % KE == 0),
                "zp_conv2d: Cin %d must be a multiple of %d (or < %d and a multiple of %d)", a.Cin, KE, KE, E);
@@ -1491,7 +1497,10 @@ extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
     sg.x_bytes = tg.x_bytes;
     sg.w_bytes = tg.w_bytes[0];
     const int sgx = (int)(((long)a.N * a.GH * a.GW) / 256);
-    hipLaunchKernelGGL((k_conv_strip<4, 3, 5>), dim3(sgx, gy, 1), dim3(512), 0, st, a, sg, conv_flags());
+    if (a.dtype == ZP_F16)
+      hipLaunchKernelGGL((k_conv_strip<f16_t, 4, 3, 5>), dim3(sgx, gy, 1), dim3(512), 0, st, a, sg, conv_flags());
+    else
+      hipLaunchKernelGGL((k_conv_strip<bf16_t, 4, 3, 5>), dim3(sgx, gy, 1), dim3(512), 0, st, a, sg, conv_flags());
     ZP_LAUNCH_CHECK("zp_conv2d strip");
     return ZP_OK;
   }
@@ -1514,6 +1523,8 @@ extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
   }
   if (a.dtype == ZP_BF16) {
     ZP_DISPATCH(bf16_t)
+  } else if (a.dtype == ZP_F16) {
+    ZP_DISPATCH(f16_t)
   } else {
     ZP_DISPATCH(float)
   }

@@ -37,6 +37,20 @@ template <> struct V16<bf16_t> {
     *(uint4*)p = make_uint4(w[0], w[1], w[2], w[3]);
   }
 };
+template <> struct V16<f16_t> {
+  static constexpr int N = 8;
+  static __device__ __forceinline__ void load(const f16_t* p, float* f) {
+    const f16x8 h = *(const f16x8*)p;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f[i] = (float)h[i];
+  }
+  static __device__ __forceinline__ void store(f16_t* p, const float* f) {
+    f16x8 h;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h[i] = (f16_t)f[i];
+    *(f16x8*)p = h;
+  }
+};
 template <> struct V16<float> {
   static constexpr int N = 4;
   static __device__ __forceinline__ void load(const float* p, float* f) {
@@ -104,6 +118,7 @@ __global__ void k_pack_multi(const zp_pack_job* __restrict__ jobs, const long lo
       v = a.src[idx];
     }
     if (a.dtype == ZP_BF16) ((bf16_t*)a.dst)[le] = f2bf(v);
+    else if (a.dtype == ZP_F16) ((f16_t*)a.dst)[le] = (f16_t)v;
     else ((float*)a.dst)[le] = v;
   }
 }
@@ -745,10 +760,16 @@ __global__ void __launch_bounds__(256) k_adam_multi(const AdamTable T, float lr_
 
 using namespace zp;
 
-#define ZP_DTYPE_CHECK(fn, dt) ZP_CHECK_ARG((dt) == ZP_F32 || (dt) == ZP_BF16, fn ": bad dtype %d", (int)(dt))
+// ZP_F16 is an inference dtype: accepted by the forward-path entry points, refused by the
+// training-only ones (ZP_DTYPE_CHECK_TRAIN)
+#define ZP_DTYPE_CHECK(fn, dt) \
+  ZP_CHECK_ARG((dt) == ZP_F32 || (dt) == ZP_BF16 || (dt) == ZP_F16, fn ": bad dtype %d", (int)(dt))
+#define ZP_DTYPE_CHECK_TRAIN(fn, dt) \
+  ZP_CHECK_ARG((dt) == ZP_F32 || (dt) == ZP_BF16, fn ": dtype %d (fp16 is inference-only)", (int)(dt))
 #define ZP_BY_DTYPE(dt, KERNEL, grid, block, st, ...)                                   \
   do {                                                                                  \
     if ((dt) == ZP_BF16) hipLaunchKernelGGL(KERNEL<bf16_t>, grid, block, 0, st, __VA_ARGS__); \
+    else if ((dt) == ZP_F16) hipLaunchKernelGGL(KERNEL<f16_t>, grid, block, 0, st, __VA_ARGS__); \
     else hipLaunchKernelGGL(KERNEL<float>, grid, block, 0, st, __VA_ARGS__);            \
   } while (0)
 
@@ -823,7 +844,7 @@ extern "C" int zp_bn_train_finalize(float* partials, int parts, int C, long long
 extern "C" int zp_bn_apply(const void* x, int P, int C, const float* scale, const float* shift, const void* res, int ldr,
                            int cr0, int relu, int dtype, void* y, int ldy, int cy0, void* stream) {
   ZP_DTYPE_CHECK("zp_bn_apply", dtype);
-  const int N = dtype == ZP_BF16 ? 8 : 4;
+  const int N = dtype == ZP_F32 ? 4 : 8;
   ZP_CHECK_ARG(x && y && scale && shift && P > 0 && C % N == 0 && ldy % N == 0 && cy0 % N == 0,
                "zp_bn_apply: bad args");
   if (res) ZP_CHECK_ARG(ldr % N == 0 && cr0 % N == 0, "zp_bn_apply: residual alignment");
@@ -831,6 +852,9 @@ extern "C" int zp_bn_apply(const void* x, int P, int C, const float* scale, cons
   if (dtype == ZP_BF16)
     hipLaunchKernelGGL(k_bn_apply<bf16_t>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
                        (long)P, C, scale, shift, (const bf16_t*)res, ldr, cr0, relu, (bf16_t*)y, ldy, cy0);
+  else if (dtype == ZP_F16)
+    hipLaunchKernelGGL(k_bn_apply<f16_t>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, (const f16_t*)x,
+                       (long)P, C, scale, shift, (const f16_t*)res, ldr, cr0, relu, (f16_t*)y, ldy, cy0);
   else
     hipLaunchKernelGGL(k_bn_apply<float>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, (const float*)x,
                        (long)P, C, scale, shift, (const float*)res, ldr, cr0, relu, (float*)y, ldy, cy0);
@@ -846,8 +870,8 @@ extern "C" int zp_bn_bwd_parts(int P, int C) {
 extern "C" int zp_bn_bwd_reduce(const void* dy, int lddy, int cdy0, const void* y, int ldy, int cy0, const void* x, int P,
                                 int C, const float* save, int relu, int dtype, float* partials, float* dgamma,
                                 float* dbeta, int accumulate, void* stream) {
-  ZP_DTYPE_CHECK("zp_bn_bwd_reduce", dtype);
-  const int N = dtype == ZP_BF16 ? 8 : 4;
+  ZP_DTYPE_CHECK_TRAIN("zp_bn_bwd_reduce", dtype);
+  const int N = dtype == ZP_F32 ? 4 : 8;
   ZP_CHECK_ARG(dy && partials && P > 0 && C % N == 0 && (!relu || y) && (!x || save), "zp_bn_bwd_reduce: bad args");
   ZP_CHECK_ARG(C / N <= 256 || (C / N) % 256 == 0, "zp_bn_bwd_reduce: C %d", C);
   const int parts = zp_bn_bwd_parts(P, C);
@@ -871,8 +895,8 @@ extern "C" int zp_bn_bwd_reduce(const void* dy, int lddy, int cdy0, const void* 
 extern "C" int zp_bn_bwd_apply(const void* dy, int lddy, int cdy0, const void* y, int ldy, int cy0, const void* x, int P,
                                int C, const float* save, const float* partials, const float* gamma, int relu, int dtype,
                                void* dx, void* dres, int lddres, int cdres0, int res_accumulate, void* stream) {
-  ZP_DTYPE_CHECK("zp_bn_bwd_apply", dtype);
-  const int N = dtype == ZP_BF16 ? 8 : 4;
+  ZP_DTYPE_CHECK_TRAIN("zp_bn_bwd_apply", dtype);
+  const int N = dtype == ZP_F32 ? 4 : 8;
   ZP_CHECK_ARG(dy && P > 0 && C % N == 0 && (!relu || y) && (!dx || (x && save && partials && gamma)),
                "zp_bn_bwd_apply: bad args");
   const int parts = zp_bn_bwd_parts(P, C);
@@ -895,6 +919,9 @@ extern "C" int zp_bn_bwd_apply(const void* dy, int lddy, int cdy0, const void* y
     if ((dt) == ZP_BF16) {                                                                  \
       using T = bf16_t;                                                                     \
       hipLaunchKernelGGL(KERNEL<T>, grid, dim3(256), 0, st, __VA_ARGS__);                   \
+    } else if ((dt) == ZP_F16) {                                                            \
+      using T = f16_t;                                                                      \
+      hipLaunchKernelGGL(KERNEL<T>, grid, dim3(256), 0, st, __VA_ARGS__);                   \
     } else {                                                                                \
       using T = float;                                                                      \
       hipLaunchKernelGGL(KERNEL<T>, grid, dim3(256), 0, st, __VA_ARGS__);                   \
@@ -912,7 +939,7 @@ extern "C" int zp_nchw_to_nhwc(const float* x, int B, int C, int H, int W, int c
 extern "C" int zp_maxpool3s2(const void* x, int B, int IH, int IW, int ldx, int cx0, int C, int dtype, void* y, int OH,
                              int OW, int ldy, int cy0, void* stream) {
   ZP_DTYPE_CHECK("zp_maxpool3s2", dtype);
-  const int N = dtype == ZP_BF16 ? 8 : 4;
+  const int N = dtype == ZP_F32 ? 4 : 8;
   ZP_CHECK_ARG(x && y && C % N == 0 && cx0 % N == 0 && ldx % N == 0 && cy0 % N == 0 && ldy % N == 0,
                "zp_maxpool3s2: bad args / alignment");
   ZP_CHECK_ARG(OH == (IH - 1) / 2 + 1 && OW == (IW - 1) / 2 + 1, "zp_maxpool3s2: OH/OW");
@@ -926,8 +953,8 @@ extern "C" int zp_maxpool3s2(const void* x, int B, int IH, int IW, int ldx, int 
 extern "C" int zp_maxpool3s2_bwd(const void* x, int ldx, int cx0, const void* dy, int lddy, int cdy0, int B, int IH,
                                  int IW, int C, int OH, int OW, int dtype, void* dx, int lddx, int cdx0, int accumulate,
                                  void* stream) {
-  ZP_DTYPE_CHECK("zp_maxpool3s2_bwd", dtype);
-  const int N = dtype == ZP_BF16 ? 8 : 4;
+  ZP_DTYPE_CHECK_TRAIN("zp_maxpool3s2_bwd", dtype);
+  const int N = dtype == ZP_F32 ? 4 : 8;
   ZP_CHECK_ARG(x && dy && dx && C % N == 0 && cx0 % N == 0 && cdy0 % N == 0 && cdx0 % N == 0,
                "zp_maxpool3s2_bwd: bad args");
   long total = (long)B * IH * IW * (C / N);
@@ -941,11 +968,14 @@ extern "C" int zp_global_avgpool(const void* x, int B, int H, int W, int ldx, in
                                  void* stream) {
   ZP_DTYPE_CHECK("zp_global_avgpool", dtype);
   ZP_CHECK_ARG(x && y && B > 0 && H > 0 && W > 0 && C > 0, "zp_global_avgpool: bad args");
-  const int N = dtype == ZP_BF16 ? 8 : 4;
+  const int N = dtype == ZP_F32 ? 4 : 8;
   if (C % N == 0 && cx0 % N == 0 && ldx % N == 0) {
     if (dtype == ZP_BF16)
       hipLaunchKernelGGL((k_hw_reduce_vec<bf16_t, 0>), dim3((C + 63) / 64, B), dim3(256), 0, (hipStream_t)stream,
                          (const bf16_t*)x, H, W, ldx, cx0, C, (bf16_t*)y);
+    else if (dtype == ZP_F16)
+      hipLaunchKernelGGL((k_hw_reduce_vec<f16_t, 0>), dim3((C + 63) / 64, B), dim3(256), 0, (hipStream_t)stream,
+                         (const f16_t*)x, H, W, ldx, cx0, C, (f16_t*)y);
     else
       hipLaunchKernelGGL((k_hw_reduce_vec<float, 0>), dim3((C + 63) / 64, B), dim3(256), 0, (hipStream_t)stream,
                          (const float*)x, H, W, ldx, cx0, C, (float*)y);
@@ -961,7 +991,7 @@ extern "C" int zp_broadcast_hw(const void* src, int B, int C, int dtype, void* y
   ZP_DTYPE_CHECK("zp_broadcast_hw", dtype);
   ZP_CHECK_ARG(src && y && B > 0 && C > 0, "zp_broadcast_hw: bad args");
   long total = (long)B * H * W * C;
-  const int N = dtype == ZP_BF16 ? 8 : 4;
+  const int N = dtype == ZP_F32 ? 4 : 8;
   if (C % N == 0 && ldy % N == 0 && cy0 % N == 0) {
     ZP_TLAUNCH(dtype, k_broadcast_vec, dim3(grid_for(total / N)), (hipStream_t)stream, (const T*)src, B, C, (T*)y, H,
                W, ldy, cy0);
@@ -975,9 +1005,9 @@ extern "C" int zp_broadcast_hw(const void* src, int B, int C, int dtype, void* y
 
 extern "C" int zp_sum_hw(const void* dy, int B, int H, int W, int lddy, int cdy0, int C, int dtype, void* out,
                          void* stream) {
-  ZP_DTYPE_CHECK("zp_sum_hw", dtype);
+  ZP_DTYPE_CHECK_TRAIN("zp_sum_hw", dtype);
   ZP_CHECK_ARG(dy && out && B > 0 && C > 0, "zp_sum_hw: bad args");
-  const int N = dtype == ZP_BF16 ? 8 : 4;
+  const int N = dtype == ZP_F32 ? 4 : 8;
   if (C % N == 0 && cdy0 % N == 0 && lddy % N == 0) {
     if (dtype == ZP_BF16)
       hipLaunchKernelGGL((k_hw_reduce_vec<bf16_t, 1>), dim3((C + 63) / 64, B), dim3(256), 0, (hipStream_t)stream,
@@ -995,7 +1025,7 @@ extern "C" int zp_sum_hw(const void* dy, int B, int H, int W, int lddy, int cdy0
 
 extern "C" int zp_add_broadcast_hw(const void* src, float mul, int B, int C, int dtype, void* y, int H, int W, int ldy,
                                    int cy0, int accumulate, void* stream) {
-  ZP_DTYPE_CHECK("zp_add_broadcast_hw", dtype);
+  ZP_DTYPE_CHECK_TRAIN("zp_add_broadcast_hw", dtype);
   ZP_CHECK_ARG(src && y && B > 0 && C > 0, "zp_add_broadcast_hw: bad args");
   long total = (long)B * H * W * C;
   ZP_TLAUNCH(dtype, k_broadcast, dim3(grid_for(total)), (hipStream_t)stream, (const T*)src, B, C, mul, (T*)y, H, W,
@@ -1006,8 +1036,8 @@ extern "C" int zp_add_broadcast_hw(const void* src, float mul, int B, int C, int
 
 extern "C" int zp_copy_slice(const void* x, int ldx, int cx0, int xdtype, void* y, int ldy, int cy0, int ydtype, int P,
                              int C, int accumulate, void* stream) {
-  ZP_DTYPE_CHECK("zp_copy_slice", xdtype);
-  ZP_DTYPE_CHECK("zp_copy_slice", ydtype);
+  ZP_DTYPE_CHECK_TRAIN("zp_copy_slice", xdtype);
+  ZP_DTYPE_CHECK_TRAIN("zp_copy_slice", ydtype);
   ZP_CHECK_ARG(x && y && P > 0 && C > 0, "zp_copy_slice: bad args");
   long total = (long)P * C;
   dim3 g(grid_for(total));
@@ -1030,7 +1060,7 @@ extern "C" int zp_copy_slice(const void* x, int ldx, int cx0, int xdtype, void* 
 
 extern "C" int zp_head_grad_to_nhwc(const float* dmask, const float* dcode, int B, int L, int H, int W, int ldy,
                                     int dtype, void* y, void* stream) {
-  ZP_DTYPE_CHECK("zp_head_grad_to_nhwc", dtype);
+  ZP_DTYPE_CHECK_TRAIN("zp_head_grad_to_nhwc", dtype);
   ZP_CHECK_ARG(dmask && dcode && y && ldy >= L + 1, "zp_head_grad_to_nhwc: bad args");
   ZP_TLAUNCH(dtype, k_head_grad, dim3(grid_for((long)B * H * W)), (hipStream_t)stream, dmask, dcode, B, L, H, W, ldy,
              (T*)y);

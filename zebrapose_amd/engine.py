@@ -31,8 +31,8 @@ from . import _lib as L
 from . import geometry as G
 from .model.resnet import TVBottleneck
 
-_KE = {L.ZP_F32: 32, L.ZP_BF16: 64}
-_E = {L.ZP_F32: 4, L.ZP_BF16: 8}
+_KE = {L.ZP_F32: 32, L.ZP_BF16: 64, L.ZP_F16: 64}
+_E = {L.ZP_F32: 4, L.ZP_BF16: 8, L.ZP_F16: 8}
 
 
 class Act:
@@ -228,10 +228,11 @@ class Engine:
             flops = 2.0 * x.B * plan.GH * plan.GW * sum(len(sb.taps) for sb in plan.subs) * x.C * cout
             tc, tp, stages, var = C.c_int(), C.c_int(), C.c_int(), C.c_int()
             L.call("zp_conv2d_config", C.byref(a), C.byref(tc), C.byref(tp), C.byref(stages), C.byref(var))
-            if var.value == 1:  # rocprofv3 name: k_conv_strip<WC, STAGES, SPW = 5>
-                kname = f"k_conv_strip<bf16,WC={tc.value // 32},ST=3>"
+            tn = {L.ZP_F32: "f32", L.ZP_BF16: "bf16", L.ZP_F16: "f16"}[self.dt]
+            if var.value == 1:  # rocprofv3 name: k_conv_strip<T, WC, STAGES, SPW = 5>
+                kname = f"k_conv_strip<{tn},WC={tc.value // 32},ST=3>"
             else:  # rocprofv3 name: k_conv<T, WC = tc / 32, WP = 4, NWP = tp / 64, STAGES, smallC>
-                kname = (f"k_conv<{'bf16' if self.dt == L.ZP_BF16 else 'f32'},WC={tc.value // 32},WP=4,"
+                kname = (f"k_conv<{tn},WC={tc.value // 32},WP=4,"
                          f"NWP={tp.value // 64},ST={stages.value},smallC={int(x.C < _KE[self.dt])}>")
             geo = (f"{label}:{x.C}->{cout} taps{max(len(sb.taps) for sb in plan.subs)} "
                    f"{x.H}x{x.W}->{plan.GH}x{plan.GW}x{a.nsub}")

@@ -10,7 +10,8 @@ no PyTorch-op fallback.
 Precision: ``precision='fp32'`` (default) computes every convolution with exact-f32 MFMA
 (``v_mfma_f32_16x16x4_f32``) and f32 activations -- the parity mode; ``precision='bf16'``
 uses bf16 MFMA with f32 accumulation and bf16 NHWC activations -- the throughput mode
-(configs 2-4).  Set per instance (``net.set_precision``) or with ``ZP_PRECISION``.
+(configs 2-4); ``precision='fp16'`` is the same with IEEE fp16 (``v_mfma_f32_16x16x32_f16``),
+inference only (configs[4]: R50 multi-object inference).  Set per instance (``net.set_precision``) or with ``ZP_PRECISION``.
 """
 from __future__ import annotations
 
@@ -30,7 +31,8 @@ model_urls = {
     "resnet50": "https://download.pytorch.org/models/resnet50-19c8e357.pth",
 }
 
-_PREC = {"fp32": torch.float32, "f32": torch.float32, "bf16": torch.bfloat16}
+_PREC = {"fp32": torch.float32, "f32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16,
+         "f16": torch.float16}
 
 
 # ============================================================================ losses
@@ -209,11 +211,13 @@ class DeepLabV3(nn.Module):
 
     @property
     def precision(self):
-        return "bf16" if self._engine.dtype == torch.bfloat16 else "fp32"
+        return {torch.bfloat16: "bf16", torch.float16: "fp16"}.get(self._engine.dtype, "fp32")
 
     def forward(self, x):
         params = [p for p in self.parameters()]
         if self.training and torch.is_grad_enabled() and any(p.requires_grad for p in params):
+            if self._engine.dtype == torch.float16:
+                raise RuntimeError("precision='fp16' is inference-only (configs[4]); train in 'bf16' or 'fp32'")
             return _DeepLabFn.apply(self, x, *params)
         mask, code, _ = self._engine.forward(x, train=self.training)
         return mask, code
