@@ -270,6 +270,31 @@ def main():
     pnp_res = {"ms_per_batch": round(pnp_ms, 3), "crops_per_s": round(B / (pnp_ms * 1e-3), 1), "iterations": 150,
                "correspondences_per_crop": round(n_corr / B)}
 
+    # ------------------------------------------------------------------ device crop pipeline (extra, §8f rank 2)
+    from zebrapose_amd.crop import CropPipeline
+    cp = CropPipeline()
+    g = torch.Generator(device="cpu").manual_seed(3)
+    imgs = torch.randint(0, 256, (8, 480, 640, 3), generator=g, dtype=torch.uint8).to(dev)
+    gts = torch.randint(0, 256, (8, 480, 640, 3), generator=g, dtype=torch.uint8).to(dev)
+    msk = torch.randint(0, 256, (8, 480, 640), generator=g, dtype=torch.uint8).to(dev)
+    raw = np.stack([rng.integers(0, 500, B), rng.integers(0, 350, B), rng.integers(40, 200, B),
+                    rng.integers(40, 200, B)], 1)
+    pad, _ = cp.boxes(raw, 640, 480)
+    cidx = np.arange(B) % 8
+    cp(imgs, cidx, pad, gts, msk, msk)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        cp(imgs, cidx, pad, gts, msk, msk)
+    e1.record()
+    torch.cuda.synchronize()
+    crop_ms = e0.elapsed_time(e1) / 10
+    crop_res = {"ms_per_batch": round(crop_ms, 3), "crops_per_s": round(B / (crop_ms * 1e-3), 1),
+                "what": "640x480 BGR images -> 256 px INTER_LINEAR normalised crop + 128 px GT code planes and "
+                        "2 masks (INTER_NEAREST), padding 1.5"}
+    del imgs, gts, msk
+
     # ------------------------------------------------------------------ training step (extra)
     train = None
     if not args.no_train:
@@ -343,7 +368,7 @@ def main():
                            "model": "BinaryCodeNet_Deeplab(34, 16, 2, concat=True)", "global_batch": world * B,
                            "per_gpu_batch": B, "input": f"{S}x{S}", "parallelism": f"replicas{world}",
                            "correspondences_last_step": n_corr},
-                "roofline": roofline, "cpu_baseline": cpu, "train": train, "pnp": pnp_res,
+                "roofline": roofline, "cpu_baseline": cpu, "train": train, "pnp": pnp_res, "crop": crop_res,
                 "multi_object": multi}
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -288,6 +288,24 @@ long long zp_pose_error_ws_bytes(int B, int n, int mode);
 int zp_pose_error(int B, const float* pts, int n, const double* R_est, const double* t_est,
                   const double* R_gt, const double* t_gt, int mode, double* out, void* ws, void* stream);
 
+/* ---- device crop pipeline --------------------------------------------
+ * Replaces the DataLoader worker's crop_square_resize (bop_dataset_pytorch.py:36-72) of the image
+ * (cv2.INTER_LINEAR -> S px) + transform_pre (:333-347: ToTensor + ImageNet Normalize on the BGR
+ * array), and of the GT code image / visible mask / entire mask (cv2.INTER_NEAREST -> S px)
+ * + RGB_image_to_class_id_image / class_id_image_to_class_code_images
+ * (class_id_encoder_decoder.py:6-15, 43-63).  Images stay on the device as one stack
+ * u8 [n_img][H][W][3] (masks [n_img][H][W]); crop b reads image img_index[b] with the padded box
+ * bbox[b] = (x, y, w, h) int32 (padding_Bbox output).  A box with w <= 0 and h <= 0 gives the
+ * reference's all-zero dummy crop.
+ *   zp_crop_image: out f32 [B][3][S][S] (normalised, BGR channel order as the reference feeds it)
+ *   zp_crop_gt:    code u8 [B][L][S][S] (0/1, channel 0 = MSB), mask_out / entire_out f32
+ *                  [B][S][S] = v / 255; any of the three outputs may be NULL */
+int zp_crop_image(const uint8_t* imgs, int n_img, int H, int W, const int* img_index, const int* bbox, int B, int S,
+                  float* out, void* stream);
+int zp_crop_gt(const uint8_t* gts, const uint8_t* masks, const uint8_t* entire_masks, int n_img, int H, int W,
+               const int* img_index, const int* bbox, int B, int S, int L, uint8_t* code, float* mask_out,
+               float* entire_out, void* stream);
+
 /* ---- optimizer ----------------------------------------------------------------------- */
 /* torch.optim.Adam (no weight decay, amsgrad off) over one flat f32 buffer; step >= 1 */
 int zp_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, long long n,

@@ -108,6 +108,8 @@ _SIGS = {
     "zp_pnp_ransac": (i32, [i32, i32, vp, vp, vp, vp, i32, f64, f64, vp, vp, vp, vp, vp, vp]),
     "zp_pose_error_ws_bytes": (i64, [i32, i32, i32]),
     "zp_pose_error": (i32, [i32, vp, i32, vp, vp, vp, vp, i32, vp, vp, vp]),
+    "zp_crop_image": (i32, [vp, i32, i32, i32, vp, vp, i32, i32, vp, vp]),
+    "zp_crop_gt": (i32, [vp, vp, vp, i32, i32, i32, vp, vp, i32, i32, i32, vp, vp, vp, vp]),
     "zp_adam_multi": (i32, [i32, vp, vp, vp, vp, vp, f64, f64, f64, f64, i64, vp]),
 }
 
