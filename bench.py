@@ -328,6 +328,42 @@ def main():
                  "parallelism": f"ddp{world}" if world > 1 else "single"}
         del ts, tnet
 
+    # ------------------------------------------------------------------ 3-head v3 network (extra, §8f rank 3)
+    v3 = None
+    if not args.no_train:
+        from zebrapose_amd.model.BinaryCodeNet_v3 import BinaryCodeNet_Deeplab_v3
+        from zebrapose_amd.train import TrainStep
+        n3 = BinaryCodeNet_Deeplab_v3(34, 16, 2, concat=True, output_kernel_size=1, precision=args.precision).to(dev)
+        calibrate_bn(n3, x)
+        with torch.no_grad():
+            n3(x)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with torch.no_grad():
+            for _ in range(args.steps):
+                n3(x)
+        torch.cuda.synchronize()
+        inf_ms = (time.perf_counter() - t0) / args.steps * 1e3
+        n3.train()
+        ts3 = TrainStep(n3, learning_rate=2e-4 * world)
+        g = torch.Generator(device="cpu").manual_seed(9 + rank)
+        gt_code = (torch.rand((B, 16, S // 2, S // 2), generator=g) < 0.5).to(torch.uint8).to(dev)
+        gt_mask = (torch.rand((B, S // 2, S // 2), generator=g) < 0.7).float().to(dev)
+        gt_ent = (torch.rand((B, S // 2, S // 2), generator=g) < 0.8).float().to(dev)
+        for _ in range(2):
+            ts3(x, gt_code, gt_mask, gt_ent)
+        torch.cuda.synchronize()
+        K3 = max(3, args.steps // 4)
+        t0 = time.perf_counter()
+        for _ in range(K3):
+            ts3(x, gt_code, gt_mask, gt_ent)
+        torch.cuda.synchronize()
+        tr_ms = (time.perf_counter() - t0) / K3 * 1e3
+        v3 = {"model": "BinaryCodeNet_Deeplab_v3(34, 16, 2, concat=True) (train_v5.py)", "batch": B,
+              "infer_crops_per_s": round(B / (inf_ms * 1e-3), 1), "infer_ms_per_step": round(inf_ms, 3),
+              "train_crops_per_s": round(B / (tr_ms * 1e-3), 1), "train_ms_per_step": round(tr_ms, 3)}
+        del ts3, n3
+
     # ------------------------------------------------------------------ configs[4] multi-object leg (extra)
     multi = None
     if rank == 0 and world == 1 and not args.no_multi:
@@ -368,7 +404,7 @@ def main():
                            "model": "BinaryCodeNet_Deeplab(34, 16, 2, concat=True)", "global_batch": world * B,
                            "per_gpu_batch": B, "input": f"{S}x{S}", "parallelism": f"replicas{world}",
                            "correspondences_last_step": n_corr},
-                "roofline": roofline, "cpu_baseline": cpu, "train": train, "pnp": pnp_res, "crop": crop_res,
+                "roofline": roofline, "cpu_baseline": cpu, "train": train, "pnp": pnp_res, "crop": crop_res, "v3": v3,
                 "multi_object": multi}
         print(json.dumps(line), flush=True)
     if world > 1:

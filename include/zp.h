@@ -217,6 +217,13 @@ int zp_add_broadcast_hw(const void* src, float mul, int B, int C, int dtype, voi
 /* generic NHWC slice copy / add / cast: y[p, cy0+c] (+)= x[p, cx0+c]  */
 int zp_copy_slice(const void* x, int ldx, int cx0, int xdtype, void* y, int ldy, int cy0, int ydtype,
                   int P, int C, int accumulate, void* stream);
+/* F.interpolate(mask, (OH, OW), mode="bilinear", align_corners=False) of a one-channel f32 NCHW
+ * map into channel cy0 of an NHWC concat buffer (BinaryCodeNet_Deeplab_v3: aspp_v3.py:89, 96-101),
+ * and its backward (gather form, deterministic) into f32 NCHW dx (accumulate: dx += ...). */
+int zp_mask_interp(const float* x, int B, int H, int W, int OH, int OW, int dtype, void* y, int ldy, int cy0,
+                   void* stream);
+int zp_mask_interp_bwd(const void* dy, int lddy, int cdy0, int B, int OH, int OW, int H, int W, int dtype, float* dx,
+                       int accumulate, void* stream);
 /* head gradient f32 NCHW (dmask [B][1][H][W], dcode [B][L][H][W]) -> y NHWC [B][H][W][ldy]
  * (dtype), channel 0 = mask, 1..L = code, channels L+1..ldy-1 zeroed */
 int zp_head_grad_to_nhwc(const float* dmask, const float* dcode, int B, int L, int H, int W, int ldy,

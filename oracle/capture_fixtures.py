@@ -312,6 +312,70 @@ def capture_decode():
     print("decode counts", [int(out[f"ib0_b{b}_count"]) for b in range(B)])
 
 
+def capture_v3():
+    """BinaryCodeNet_Deeplab_v3: layout, 256x256 forward (3 heads) and one
+    train_v5.py:321-334 step (3 * loss_b + loss_mask + loss_entire_mask, backward).  The reference
+    resamples the mask to a fixed 64x64 (aspp_v3.py:95), so only 256x256 inputs run."""
+    from model.BinaryCodeNet_v3 import BinaryCodeNet_Deeplab_v3, BinaryCodeLoss, MaskLoss
+    from common_ops import from_output_to_class_mask
+    import contextlib, io
+    with contextlib.redirect_stdout(io.StringIO()):
+        net = BinaryCodeNet_Deeplab_v3(num_resnet_layers=34, concat=True, binary_code_length=16,
+                                       divided_number_each_iteration=2, output_kernel_size=1)
+    entries, aliases = tv_layout.state_spec("v3", 16)
+    got = [(k, tuple(v.shape)) for k, v in net.state_dict().items()]
+    assert got == [(k, tuple(sh)) for k, sh, _ in entries], "v3 state-dict layout mismatch"
+    with open(os.path.join(GOLDEN, "state_keys_r34v3.txt"), "w") as f:
+        for k, sh in got:
+            f.write(f"{k} {list(sh)}\n")
+    net.load_state_dict(ref_cpu.synthetic_state("v3", 16, seed=0))
+    calibrate_bn(net, seeded((2, 3, 256, 256), 1))
+    bnbuf = {k: net.state_dict()[k].numpy().copy() for k, _, kind in entries
+             if kind in ("bn_rm", "bn_rv", "bn_nbt") and k not in aliases}
+    np.savez(os.path.join(GOLDEN, "r34v3_bn_buffers.npz"), **bnbuf)
+    x = seeded((1, 3, 256, 256), 0)
+    with torch.no_grad():
+        m, e, c = net(x)
+    np.savez(os.path.join(GOLDEN, "r34v3_fwd256.npz"), x=x.numpy(), mask=m.numpy(), entire=e.numpy(), code=c.numpy())
+    sd2 = ref_cpu.synthetic_state("v3", 16, seed=0, bn_buffers=bnbuf)
+    with torch.no_grad():
+        om, oe, oc = ref_cpu.forward_v3(sd2, x)
+    print(f"v3 fwd256 oracle vs reference: mask {np.abs(om.numpy() - m.numpy()).max():.3g} entire "
+          f"{np.abs(oe.numpy() - e.numpy()).max():.3g} code {np.abs(oc.numpy() - c.numpy()).max():.3g}")
+    # one training step
+    net.train()
+    g = np.random.default_rng(17)
+    xt = seeded((2, 3, 256, 256), 5)
+    gt_code = torch.from_numpy((g.random((2, 16, 128, 128)) < 0.5).astype(np.float64))
+    gt_mask = torch.from_numpy((g.random((2, 128, 128)) < 0.7).astype(np.float32))
+    gt_entire = torch.from_numpy((g.random((2, 128, 128)) < 0.8).astype(np.float32))
+    bcl = BinaryCodeLoss("BCE", True, 2, use_histgramm_weighted_binary_loss=True)
+    ml = MaskLoss()
+    net.zero_grad()
+    pm, pe, pc = net(xt)
+    mask01 = torch.tensor(from_output_to_class_mask(pm))
+    loss_b = bcl(pc, mask01, gt_code)
+    loss_m = ml(pm, gt_mask)
+    loss_e = ml(pe, gt_entire)
+    loss = 3 * loss_b + loss_m + loss_e
+    loss.backward()
+    keys = ["net.aspp_v3.conv_1x1_4.weight", "net.aspp_v3.conv_1x1_4.bias", "net.aspp_v3.conv_1x1_3.weight",
+            "net.aspp_v3.upsample_2.0.weight", "net.aspp_v3.bn_conv_1x1_1.weight", "net.aspp.conv_1x1_4.weight",
+            "net.aspp.upsample_2.3.weight", "net.resnet.layer5.2.conv2.weight", "net.resnet.resnet.0.weight"]
+    named = dict(net.named_parameters())
+    grads = {}
+    for k in keys:
+        g_ = named[k].grad.numpy()
+        grads["grad:" + k] = g_[:8].copy()
+        grads["gradsum:" + k] = np.array([g_.astype(np.float64).sum(), (g_.astype(np.float64) ** 2).sum()])
+    np.savez_compressed(os.path.join(GOLDEN, "r34v3_train_step.npz"), x=xt.numpy(),
+             gt_code=gt_code.numpy().astype(np.uint8), gt_mask=gt_mask.numpy().astype(np.uint8),
+             gt_entire=gt_entire.numpy().astype(np.uint8), mask_logits=pm.detach().numpy(),
+             entire_logits=pe.detach().numpy(), loss_b=loss_b.detach().numpy(),
+             loss_m=loss_m.detach().numpy(), loss_e=loss_e.detach().numpy(), loss=loss.detach().numpy(), **grads)
+    print("v3 train step: loss", float(loss), "loss_e", float(loss_e))
+
+
 def main():
     os.makedirs(GOLDEN, exist_ok=True)
     install_shim()
@@ -322,6 +386,8 @@ def main():
     capture_decode()
     if "--r50" in sys.argv:
         capture_network(50)
+    if "--v3" in sys.argv:
+        capture_v3()
 
 
 if __name__ == "__main__":

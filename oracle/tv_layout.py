@@ -78,6 +78,24 @@ def _upsample(p, cin, cout):
 
 
 def state_spec(variant: int = 34, code_bits: int = 16):
+    """variant 34 | 50 (BinaryCodeNet_Deeplab) or "v3" (BinaryCodeNet_Deeplab_v3, ResNet34: the
+    same keys followed by net.aspp_v3.*, aspp_v3.py:8-55)."""
+    if variant == "v3":
+        entries, aliases = state_spec(34, code_bits)
+        a = "net.aspp_v3"
+
+        def cb3(name, bn, cin, cout, k):
+            return (_conv(f"{a}.{name}", cout, cin, k) + [(f"{a}.{name}.bias", (cout,), "bias")]
+                    + _bn(f"{a}.{bn}", cout))
+        entries += cb3("conv_1x1_1", "bn_conv_1x1_1", 512, 256, 1)
+        entries += cb3("conv_3x3_1", "bn_conv_3x3_1", 512, 256, 3)
+        entries += cb3("conv_3x3_2", "bn_conv_3x3_2", 512, 256, 3)
+        entries += cb3("conv_1x1_2", "bn_conv_1x1_2", 512, 256, 1)
+        entries += cb3("conv_1x1_3", "bn_conv_1x1_3", 1025, 256, 1)
+        entries += _upsample(f"{a}.upsample_1", 256, 256)
+        entries += _upsample(f"{a}.upsample_2", 321, 256)
+        entries += _conv(f"{a}.conv_1x1_4", 1, 321, 1) + [(f"{a}.conv_1x1_4.bias", (1,), "bias")]
+        return entries, aliases
     if variant not in (34, 50):
         raise ValueError("variant must be 34 or 50")
     r = "net.resnet"

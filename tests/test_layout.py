@@ -82,3 +82,13 @@ def test_checkpoint_roundtrip(tmp_path, net):
         assert k1 == k2 and torch.equal(v1, v2)
     p = utils_v2.save_best_checkpoint(str(tmp_path / "best"), net, opt, sched, 0.90971, 376000)
     assert os.path.basename(p) == "0_9097step376000"
+
+
+def test_v3_variant_layout():
+    """BinaryCodeNet_Deeplab_v3: the reference's module tree and state_dict keys (+ net.aspp_v3.*)."""
+    from zebrapose_amd.model.BinaryCodeNet_v3 import BinaryCodeNet_Deeplab_v3
+    net = BinaryCodeNet_Deeplab_v3(34, 16, 2, concat=True, output_kernel_size=1)
+    want = open(os.path.join(GOLDEN, "state_keys_r34v3.txt")).read().splitlines()
+    assert [f"{k} {list(v.shape)}" for k, v in net.state_dict().items()] == want
+    with pytest.raises(NotImplementedError):
+        BinaryCodeNet_Deeplab_v3(50, 16, 2, concat=True)

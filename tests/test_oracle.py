@@ -116,3 +116,21 @@ def test_r50_state_spec_and_forward_match_reference(golden):
         m, c = ref_cpu.forward(sd, torch.from_numpy(f["fwd64_x"]), 50)
     np.testing.assert_allclose(m.numpy(), f["fwd64_mask"], atol=1e-5, rtol=0)
     np.testing.assert_allclose(c.numpy(), f["fwd64_code"], atol=1e-5, rtol=0)
+
+
+def test_v3_state_spec_and_forward_match_reference(golden):
+    """BinaryCodeNet_Deeplab_v3: key layout and the 256x256 three-head forward
+    of the oracle against the reference's own outputs (oracle/capture_fixtures.py capture_v3)."""
+    import os
+    from oracle import tv_layout
+    from tests.conftest import GOLDEN
+    entries, _ = tv_layout.state_spec("v3", 16)
+    want = open(os.path.join(GOLDEN, "state_keys_r34v3.txt")).read().splitlines()
+    assert [f"{k} {list(s)}" for k, s, _ in entries] == want
+    f = golden("r34v3_fwd256.npz")
+    sd = ref_cpu.synthetic_state("v3", 16, 0, dict(golden("r34v3_bn_buffers.npz")))
+    with torch.no_grad():
+        m, e, c = ref_cpu.forward_v3(sd, torch.from_numpy(f["x"]))
+    np.testing.assert_array_equal(m.numpy(), f["mask"])
+    np.testing.assert_array_equal(e.numpy(), f["entire"])
+    np.testing.assert_array_equal(c.numpy(), f["code"])

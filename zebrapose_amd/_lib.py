@@ -90,6 +90,8 @@ _SIGS = {
     "zp_add_broadcast_hw": (i32, [vp, f32, i32, i32, i32, vp, i32, i32, i32, i32, i32, vp]),
     "zp_copy_slice": (i32, [vp, i32, i32, i32, vp, i32, i32, i32, i32, i32, i32, vp]),
     "zp_head_grad_to_nhwc": (i32, [vp, vp, i32, i32, i32, i32, i32, i32, vp, vp]),
+    "zp_mask_interp": (i32, [vp, i32, i32, i32, i32, i32, i32, vp, i32, i32, vp]),
+    "zp_mask_interp_bwd": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, i32, vp]),
     "zp_code_loss_ws_bytes": (i64, [i32, i32, i32, i32]),
     "zp_code_loss": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp]),
     "zp_code_loss_bwd": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp]),

@@ -417,6 +417,75 @@ __global__ void k_bn_bwd_apply(const T* __restrict__ dy, int lddy, int cdy0, con
   }
 }
 
+// ------------------------------------------------------------------ mask resampling (v3 net)
+// F.interpolate(mask [B,1,H,W] f32, (OH, OW), mode="bilinear", align_corners=False) written into
+// an NHWC channel of the concat buffer (aspp_v3.py:89, 96-97; torch.cat at :90, :98, :101).  Same
+// arithmetic as PyTorch's CPU kernel: scale = (float)in / out, src = max(scale * (d + 0.5) - 0.5, 0),
+// i0 = (int)src, i1 = i0 + (i0 < in - 1), l1 = src - i0, out = l0 (w0 v00 + w1 v01) + l1 (w0 v10 + w1 v11).
+struct LinIdx {
+  int i0, i1;
+  float l0, l1;
+};
+__device__ __forceinline__ LinIdx lin_idx(int d, int n_in, int n_out) {
+  const float sc = (float)n_in / (float)n_out;
+  float src = sc * ((float)d + 0.5f) - 0.5f;
+  src = src < 0.f ? 0.f : src;
+  LinIdx r;
+  r.i0 = (int)src;
+  r.i1 = r.i0 + (r.i0 < n_in - 1 ? 1 : 0);
+  r.l1 = src - (float)r.i0;
+  r.l0 = 1.f - r.l1;
+  return r;
+}
+
+template <typename T>
+__global__ void k_mask_interp(const float* __restrict__ x, int B, int H, int W, int OH, int OW, T* __restrict__ y,
+                              int ldy, int cy0) {
+  const long total = (long)B * OH * OW;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int ox = (int)(e % OW);
+    const long t = e / OW;
+    const int oy = (int)(t % OH), b = (int)(t / OH);
+    const LinIdx ly = lin_idx(oy, H, OH), lx = lin_idx(ox, W, OW);
+    const float* s = x + (size_t)b * H * W;
+    const float v = ly.l0 * (lx.l0 * s[ly.i0 * W + lx.i0] + lx.l1 * s[ly.i0 * W + lx.i1]) +
+                    ly.l1 * (lx.l0 * s[ly.i1 * W + lx.i0] + lx.l1 * s[ly.i1 * W + lx.i1]);
+    y[e * ldy + cy0] = Elem<T>::cvt(v);
+  }
+}
+
+// weight of input index i in output d (both taps may hit i when i1 == i0)
+__device__ __forceinline__ float lin_w(const LinIdx& l, int i) {
+  return (l.i0 == i ? l.l0 : 0.f) + (l.i1 == i ? l.l1 : 0.f);
+}
+
+// backward, gather form (deterministic): dx[b, h, w] (+)= sum over the outputs whose taps include (h, w)
+template <typename T>
+__global__ void k_mask_interp_bwd(const T* __restrict__ dy, int lddy, int cdy0, int B, int OH, int OW, int H, int W,
+                                  float* __restrict__ dx, int accumulate) {
+  const long total = (long)B * H * W;
+  const float sh = (float)H / (float)OH, sw = (float)W / (float)OW;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int w = (int)(e % W);
+    const long t = e / W;
+    const int h = (int)(t % H), b = (int)(t / H);
+    // outputs d with i0(d) in {i - 1, i}: d ~ (i + 0.5) / scale - 0.5, +-2 of slack
+    const int oy0 = max(0, (int)floorf((h - 0.5f) / sh - 0.5f) - 2), oy1 = min(OH - 1, (int)((h + 1.5f) / sh) + 2);
+    const int ox0 = max(0, (int)floorf((w - 0.5f) / sw - 0.5f) - 2), ox1 = min(OW - 1, (int)((w + 1.5f) / sw) + 2);
+    float acc = 0.f;
+    for (int oy = oy0; oy <= oy1; ++oy) {
+      const float wy = lin_w(lin_idx(oy, H, OH), h);
+      if (wy == 0.f) continue;
+      for (int ox = ox0; ox <= ox1; ++ox) {
+        const float wx = lin_w(lin_idx(ox, W, OW), w);
+        if (wx == 0.f) continue;
+        acc += wy * wx * Elem<T>::ld(dy + (((size_t)b * OH + oy) * OW + ox) * lddy + cdy0);
+      }
+    }
+    dx[e] = accumulate ? dx[e] + acc : acc;
+  }
+}
+
 // ------------------------------------------------------------------ layout / pooling
 template <typename T>
 __global__ void k_nchw_to_nhwc(const float* __restrict__ x, int B, int C, int H, int W, int cpad, T* __restrict__ y) {
@@ -1061,7 +1130,7 @@ extern "C" int zp_copy_slice(const void* x, int ldx, int cx0, int xdtype, void* 
 extern "C" int zp_head_grad_to_nhwc(const float* dmask, const float* dcode, int B, int L, int H, int W, int ldy,
                                     int dtype, void* y, void* stream) {
   ZP_DTYPE_CHECK_TRAIN("zp_head_grad_to_nhwc", dtype);
-  ZP_CHECK_ARG(dmask && dcode && y && ldy >= L + 1, "zp_head_grad_to_nhwc: bad args");
+  ZP_CHECK_ARG(dmask && (dcode || L == 0) && y && ldy >= L + 1, "zp_head_grad_to_nhwc: bad args");
   ZP_TLAUNCH(dtype, k_head_grad, dim3(grid_for((long)B * H * W)), (hipStream_t)stream, dmask, dcode, B, L, H, W, ldy,
              (T*)y);
   ZP_LAUNCH_CHECK("zp_head_grad_to_nhwc");
@@ -1121,5 +1190,27 @@ extern "C" int zp_adam_multi(int count, float* const* params, const float* const
                        (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)sqrt(bc2), (float)eps);
     ZP_LAUNCH_CHECK("zp_adam_multi");
   }
+  return ZP_OK;
+}
+
+extern "C" int zp_mask_interp(const float* x, int B, int H, int W, int OH, int OW, int dtype, void* y, int ldy, int cy0,
+                              void* stream) {
+  ZP_DTYPE_CHECK("zp_mask_interp", dtype);
+  ZP_CHECK_ARG(x && y && B > 0 && H > 0 && W > 0 && OH > 0 && OW > 0 && ldy > cy0 && cy0 >= 0,
+               "zp_mask_interp: bad args");
+  ZP_TLAUNCH(dtype, k_mask_interp, dim3(grid_for((long)B * OH * OW)), (hipStream_t)stream, x, B, H, W, OH, OW, (T*)y,
+             ldy, cy0);
+  ZP_LAUNCH_CHECK("zp_mask_interp");
+  return ZP_OK;
+}
+
+extern "C" int zp_mask_interp_bwd(const void* dy, int lddy, int cdy0, int B, int OH, int OW, int H, int W, int dtype,
+                                  float* dx, int accumulate, void* stream) {
+  ZP_DTYPE_CHECK_TRAIN("zp_mask_interp_bwd", dtype);
+  ZP_CHECK_ARG(dy && dx && B > 0 && H > 0 && W > 0 && OH > 0 && OW > 0 && lddy > cdy0 && cdy0 >= 0,
+               "zp_mask_interp_bwd: bad args");
+  ZP_TLAUNCH(dtype, k_mask_interp_bwd, dim3(grid_for((long)B * H * W)), (hipStream_t)stream, (const T*)dy, lddy, cdy0,
+             B, OH, OW, H, W, dx, accumulate);
+  ZP_LAUNCH_CHECK("zp_mask_interp_bwd");
   return ZP_OK;
 }

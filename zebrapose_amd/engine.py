@@ -314,15 +314,17 @@ class Engine:
             outs.append((o.ptr, o.ld, o.c0, o.H, o.W, scale, shift, None))
         self._conv(x, merged, 256, ws, kp, rows, outs, None, True, label="aspp")
 
-    def head_fwd(self, unit, x: Act, mask, code, tape):
+    def head_fwd(self, unit, x: Act, mask, code, tape, key="head"):
+        """Head conv writing f32 NCHW channel 0 -> mask, channels 1.. -> code (code None when the
+        head has one channel); ``key`` names its output gradient in the backward's gmap."""
         plan = unit.fwd_plan(x.H, x.W)
         OH, OW = unit.out_hw(x.H, x.W)
         ws, kp, rows = self._fwd_weights(unit, plan, cache=True)
-        outs = [(mask.data_ptr(), 0, 0, OH, OW, None, unit.conv.bias, code.data_ptr())]
+        outs = [(mask.data_ptr(), 0, 0, OH, OW, None, unit.conv.bias, L.ptr(code))]
         self._conv(x, plan, unit.cout, ws, kp, rows, outs, None, False, out_mode=L.ZP_OUT_HEAD_NCHW,
                    small=self._small(unit.cin, unit.k, unit.d, unit.p), label="head")
         if tape is not None:
-            tape.recs.append(("head", unit, x, None, None, None, None))
+            tape.recs.append(("head", unit, x, key, None, None, None))
 
     # ------------------------------------------------------------------ backward pieces
     def _grad(self, gmap, act: Act):
@@ -387,7 +389,7 @@ class Engine:
         st = L.stream_ptr()
         plan = unit.fwd_plan(x.H, x.W)
         if kind == "head":
-            gy = gmap["head"]
+            gy = gmap[out]
         else:
             gout = self._grad(gmap, out)
             if kind == "bn":
@@ -430,6 +432,18 @@ class Engine:
     # ------------------------------------------------------------------ network
     def forward(self, x, train):
         """x f32 NCHW [B, 3, H, W] -> (mask [B,1,H/2,W/2], code [B,L,H/2,W/2]) f32, tape (train)."""
+        r = self._forward_main(x, train)
+        return r["mask"], r["code"], r["tape"]
+
+    def forward_v3(self, x, train):
+        """BinaryCodeNet_Deeplab_v3 (BinaryCodeNet_v3.py:152-169): the main network, then the
+        entire-mask head ASPP_v3 on (mask logits, x_high, x_128, x_64) (aspp_v3.py:78-102)
+        -> (mask, entire_mask, code, tape)."""
+        r = self._forward_main(x, train)
+        entire = self._aspp_v3(r)
+        return r["mask"], entire, r["code"], r["tape"]
+
+    def _forward_main(self, x, train):
         dl = self._net()
         rn, aspp = dl.resnet, dl.aspp
         if not rn.concat_decoder:
@@ -493,7 +507,65 @@ class Engine:
         mask = torch.empty((B, 1, H2, W2), dtype=torch.float32, device=dev)
         code = torch.empty((B, ncls - 1, H2, W2), dtype=torch.float32, device=dev)
         self.head_fwd(self._u(aspp.conv_1x1_4, None, False), Act(head_in), mask, code, tape)
-        return mask, code, tape
+        return {"mask": mask, "code": code, "tape": tape, "xh": xh, "x64": x64, "x128": x128}
+
+    def _aspp_v3(self, r):
+        """ASPP_v3.forward (aspp_v3.py:78-102).  The concats are channel slices of three buffers
+        whose widths are padded to the MFMA K step (1025 -> 1088, 321 -> 384 channels, zero
+        padding, zero weight columns): [3 branches | image pool | mask_32 | 0], [up_1 | x_64 |
+        mask_64 | 0], [up_2 | x_128 | mask | 0]; x_64 / x_128 are copied in (16 / 64 KB per crop)."""
+        dl = self._net()
+        a3 = dl.aspp_v3
+        xh, x64, x128, mask, tape = r["xh"], r["x64"], r["x128"], r["mask"], r["tape"]
+        if x64.C != 64:
+            raise NotImplementedError("ASPP_v3 expects the ResNet34 encoder (64-channel x_64)")
+        if (x64.H, x64.W) != (64, 64):
+            raise ValueError("BinaryCodeNet_Deeplab_v3 runs 256x256 inputs only: aspp_v3.py:95 resamples the mask "
+                             "to a fixed 64x64 before concatenating it with x_64")
+        B, H8, W8 = xh.B, xh.H, xh.W
+        H4, W4, H2, W2 = x64.H, x64.W, x128.H, x128.W
+        dev, dt = xh.buf.device, self.dtype
+        st = L.stream_ptr()
+        A = torch.zeros((B, H8, W8, 1088), dtype=dt, device=dev)
+        br = [self._u(a3.conv_1x1_1, a3.bn_conv_1x1_1), self._u(a3.conv_3x3_1, a3.bn_conv_3x3_1),
+              self._u(a3.conv_3x3_2, a3.bn_conv_3x3_2)]
+        self.aspp_branches_fwd(br, xh, [Act(A, 256 * i, 256) for i in range(3)], tape)
+        pool = Act(torch.empty((B, 1, 1, xh.C), dtype=dt, device=dev))
+        L.call("zp_global_avgpool", xh.ptr, B, H8, W8, xh.ld, xh.c0, xh.C, self.dt, pool.ptr, st)
+        if tape is not None:
+            tape.recs.append(("avgpool", xh, pool))
+        imgo = Act(torch.empty((B, 1, 1, 256), dtype=dt, device=dev))
+        self.unit_fwd(self._u(a3.conv_1x1_2, a3.bn_conv_1x1_2), pool, imgo, tape, label="aspp_pool")
+        L.call("zp_broadcast_hw", imgo.ptr, B, 256, self.dt, A.data_ptr(), H8, W8, 1088, 768, st)
+        if tape is not None:
+            tape.recs.append(("broadcast", imgo, Act(A, 768, 256)))
+        self._mask_interp(mask, Act(A, 1024, 1), tape)
+        o = Act(torch.empty((B, H8, W8, 256), dtype=dt, device=dev))
+        self.unit_fwd(self._u(a3.conv_1x1_3, a3.bn_conv_1x1_3, cin_act=1088), Act(A), o, tape, label="aspp_proj")
+        up2 = torch.zeros((B, H4, W4, 384), dtype=dt, device=dev)
+        self._upsample(a3.upsample_1, o, Act(up2, 0, 256), tape)
+        self._copy(x64, Act(up2, 256, 64), tape)
+        self._mask_interp(mask, Act(up2, 320, 1), tape)
+        hin = torch.zeros((B, H2, W2, 384), dtype=dt, device=dev)
+        self._upsample(a3.upsample_2, Act(up2), Act(hin, 0, 256), tape, cin_act=384)
+        self._copy(x128, Act(hin, 256, 64), tape)
+        self._mask_interp(mask, Act(hin, 320, 1), tape)
+        entire = torch.empty((B, 1, H2, W2), dtype=torch.float32, device=dev)
+        self.head_fwd(self._u(a3.conv_1x1_4, None, False, cin_act=384), Act(hin), entire, None, tape, key="head3")
+        return entire
+
+    def _mask_interp(self, mask, dst: Act, tape):
+        B, _, H, W = mask.shape
+        L.call("zp_mask_interp", mask.data_ptr(), B, H, W, dst.H, dst.W, self.dt, dst.ptr, dst.ld, dst.c0,
+               L.stream_ptr())
+        if tape is not None:
+            tape.recs.append(("interp", dst))
+
+    def _copy(self, src: Act, dst: Act, tape):
+        L.call("zp_copy_slice", src.ptr, src.ld, src.c0, self.dt, dst.ptr, dst.ld, dst.c0, self.dt, src.P, src.C, 0,
+               L.stream_ptr())
+        if tape is not None:
+            tape.recs.append(("copy", src, dst))
 
     def _u(self, conv, bn=None, relu=True, cin_act=None):
         key = (id(conv), id(bn), relu, cin_act)
@@ -503,8 +575,8 @@ class Engine:
             u = cache[key] = Unit(conv, bn, relu, cin_act)
         return u
 
-    def _upsample(self, seq, x: Act, out: Act, tape):
-        h1 = self._u(seq[0], seq[1])
+    def _upsample(self, seq, x: Act, out: Act, tape, cin_act=None):
+        h1 = self._u(seq[0], seq[1], cin_act=cin_act)
         OH, OW = h1.out_hw(x.H, x.W)
         dev, dt = x.buf.device, self.dtype
         t1 = Act(torch.empty((x.B, OH, OW, 256), dtype=dt, device=dev))
@@ -552,12 +624,13 @@ class Engine:
         self.unit_fwd(last, mid, out, tape, res=res, label="enc")
         return out
 
-    def backward(self, tape, dmask, dcode):
-        """Returns {parameter: gradient} for every parameter of the network."""
+    def backward(self, tape, dmask, dcode, dentire=None):
+        """Returns {parameter: gradient} for every parameter of the network.  With the v3 head
+        (tape holds a "head3" record), dentire is the entire-mask logits' gradient and the mask
+        resamplings add their gradient into the visible-mask head's before it runs."""
         gmap, grads = {}, {}
         st = L.stream_ptr()
-        head_rec = tape.recs[-1]
-        assert head_rec[0] == "head"
+        head_rec = next(r for r in tape.recs if r[0] == "head" and r[3] == "head")
         hin = head_rec[2]
         B, H2, W2 = hin.B, hin.H, hin.W
         ncls = head_rec[1].cout
@@ -568,12 +641,29 @@ class Engine:
             dcode = torch.zeros((B, ncls - 1, H2, W2), dtype=torch.float32, device=dev)
         dmask, dcode = dmask.contiguous().float(), dcode.contiguous().float()
         ldh = 32 if ncls <= 32 else G.ceil_to(ncls, 64)
-        ghead = torch.empty((B, H2, W2, ldh), dtype=self.dtype, device=dev)
-        L.call("zp_head_grad_to_nhwc", dmask.data_ptr(), dcode.data_ptr(), B, ncls - 1, H2, W2, ldh, self.dt,
-               ghead.data_ptr(), st)
-        gmap["head"] = Act(ghead)
+        v3 = any(r[0] == "head" and r[3] == "head3" for r in tape.recs)
+        if v3:
+            # the v3 head's mask inputs accumulate into a private copy of dmask
+            dmask = dmask.clone()
+            if dentire is None:
+                dentire = torch.zeros((B, 1, H2, W2), dtype=torch.float32, device=dev)
+            g3 = torch.empty((B, H2, W2, 32), dtype=self.dtype, device=dev)
+            L.call("zp_head_grad_to_nhwc", dentire.contiguous().float().data_ptr(), None, B, 0, H2, W2, 32, self.dt,
+                   g3.data_ptr(), st)
+            gmap["head3"] = Act(g3)
+
+        def main_head_grad():
+            ghead = torch.empty((B, H2, W2, ldh), dtype=self.dtype, device=dev)
+            L.call("zp_head_grad_to_nhwc", dmask.data_ptr(), dcode.data_ptr(), B, ncls - 1, H2, W2, ldh, self.dt,
+                   ghead.data_ptr(), st)
+            gmap["head"] = Act(ghead)
+
+        if not v3:
+            main_head_grad()
         for rec in reversed(tape.recs):
             kind = rec[0]
+            if kind == "head" and rec[3] == "head" and v3:
+                main_head_grad()  # every mask resampling of the v3 head has been differentiated
             if kind in ("plain", "bn", "head"):
                 need_dx = rec[2].ld != 8  # the NHWC image input needs no gradient
                 self.unit_bwd(rec, gmap, grads, need_dx=need_dx)
@@ -588,6 +678,16 @@ class Engine:
                 gd = self._grad(gmap, dst)
                 gs = self._grad(gmap, src)
                 L.call("zp_sum_hw", gd.ptr, gd.B, gd.H, gd.W, gd.ld, gd.c0, gd.C, self.dt, gs.ptr, st)
+            elif kind == "interp":
+                _, dst = rec
+                gd = self._grad(gmap, dst)
+                L.call("zp_mask_interp_bwd", gd.ptr, gd.ld, gd.c0, B, dst.H, dst.W, H2, W2, self.dt, dmask.data_ptr(),
+                       1, st)
+            elif kind == "copy":
+                _, src, dst = rec
+                gd = self._grad(gmap, dst)
+                gs = self._grad(gmap, src)
+                L.call("zp_copy_slice", gd.ptr, gd.ld, gd.c0, self.dt, gs.ptr, gs.ld, gs.c0, self.dt, gd.P, gd.C, 1, st)
             elif kind == "avgpool":
                 _, xa, pa = rec
                 gp = self._grad(gmap, pa)

@@ -37,13 +37,23 @@ class TrainStep:
         self.mask_loss = MaskLoss()
         self.optimizer = FusedAdam(self.net.parameters(), lr=learning_rate)
 
-    def __call__(self, x, gt_code, gt_mask):
-        """x f32 [B,3,H,W]; gt_code u8/f64 [B,L,H/2,W/2]; gt_mask f32 [B,H/2,W/2] -> (loss, loss_b, loss_m)."""
+    def __call__(self, x, gt_code, gt_mask, gt_entire_mask=None):
+        """x f32 [B,3,H,W]; gt_code u8/f64 [B,L,H/2,W/2]; gt_mask f32 [B,H/2,W/2] -> (loss, loss_b, loss_m).
+        With the 3-head BinaryCodeNet_Deeplab_v3 (train_v5.py:321-332) gt_entire_mask f32 [B,H/2,W/2] is
+        required and loss = w * loss_b + loss_mask + loss_entire_mask."""
         self.optimizer.zero_grad(set_to_none=True)
-        mask, code = self.net(x)
+        out = self.net(x)
+        if len(out) == 3:
+            if gt_entire_mask is None:
+                raise ValueError("the 3-head network needs gt_entire_mask")
+            mask, entire, code = out
+        else:
+            mask, code = out
         loss_b = self.code_loss.forward_from_logits(code, mask, gt_code)
         loss_m = self.mask_loss(mask, gt_mask)
         loss = self.binary_loss_weight * loss_b + loss_m
+        if len(out) == 3:
+            loss = loss + self.mask_loss(entire, gt_entire_mask)
         loss.backward()
         self.optimizer.step()
         return loss.detach(), loss_b.detach(), loss_m.detach()
