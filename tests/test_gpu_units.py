@@ -22,6 +22,7 @@ GEOMS = [
     ("convT", 320, 256, 3, 2, 1, 1, False, 8),
     # full-width tiles (W 32 / 64 / 128): the bf16 activation-strip kernel (k_conv_strip)
     ("conv", 128, 128, 3, 1, 1, 1, False, 32),
+    ("conv", 64, 64, 3, 1, 1, 1, False, 64),
     ("conv", 256, 256, 3, 1, 2, 2, False, 32),
     ("conv", 512, 512, 3, 1, 4, 4, False, 32),
     ("conv", 256, 256, 3, 1, 1, 1, False, 64),

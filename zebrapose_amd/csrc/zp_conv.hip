@@ -1325,11 +1325,19 @@ static int g_tc256_min_blocks = 512;
 // a loss on 32x32 layers (128 workgroups for 256 CUs) and on the ASPP launch, whose four
 // sub-problems (1 vs 9 taps) are too unbalanced for 512 large tiles.
 static bool strip_eligible(const zp_conv_args& a, strip_geo* sg);
+// strip tile width: 128 channels, or 64 when 128-channel tiles would leave part of the 256 CUs
+// idle (128 -> 128 at 32x32, bs 32: 128 workgroups; 24.2 -> 22.7 us).  64-channel layers stay on
+// k_conv's 128-pixel tiles (27.5 us there vs 29.2 us as a 64-channel strip).
+static int strip_tc(const zp_conv_args& a) {
+  const long tiles = (long)a.N * a.GH * a.GW / 256;
+  if (tiles * ((a.Cout + 127) / 128) < 256) return 64;
+  return 128;
+}
 static int conv_tc(const zp_conv_args& a) {
   // strip-eligible layers take k_conv_strip's 128-channel tile: it stages fewer bytes per FLOP than
   // the 256-channel k_conv tile, and a 256-channel strip tile does not fit the register file
   // (35 spilled VGPRs)
-  if (strip_eligible(a, nullptr)) return 128;
+  if (strip_eligible(a, nullptr)) return strip_tc(a);
   if (a.dtype != ZP_F32 && a.Cout % 256 == 0 && a.Cin >= 64 && conv_tc256_enabled()) {
     const long M = (long)a.N * a.GH * a.GW;
     int tmin = ZP_MAX_TAPS, tmax = 0;
@@ -1363,7 +1371,7 @@ static int conv_flags() {
 // ZP_CONV_STRIP=0 disables.
 static bool strip_eligible(const zp_conv_args& a, strip_geo* sg) {
   static const int en = getenv("ZP_CONV_STRIP") ? env_int("ZP_CONV_STRIP") : 1;
-  if (!en || a.dtype == ZP_F32 || a.nsub != 1 || a.Cin % 64 != 0 || a.Cout <= 64) return false;
+  if (!en || a.dtype == ZP_F32 || a.nsub != 1 || a.Cin % 64 != 0 || a.Cout % 64 != 0 || a.Cout <= 64) return false;
   if (a.sy != 1 || a.sx != 1 || a.GH != a.IH || a.GW != a.IW) return false;
   const zp_conv_sub& S = a.sub[0];
   if (S.ntaps != 9 || S.oys != 1 || S.oxs != 1 || S.oyo != 0 || S.oxo != 0 || S.OH != a.GH || S.OW != a.GW)
@@ -1493,14 +1501,18 @@ extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
   const int gx = zp_conv2d_grid(&a), gy = ceil_div(a.Cout, tc);
   hipStream_t st = (hipStream_t)stream;
   strip_geo sg{};
-  if (tc == 128 && strip_eligible(a, &sg)) {
+  if (tc <= 128 && strip_eligible(a, &sg)) {
     sg.x_bytes = tg.x_bytes;
     sg.w_bytes = tg.w_bytes[0];
     const int sgx = (int)(((long)a.N * a.GH * a.GW) / 256);
-    if (a.dtype == ZP_F16)
-      hipLaunchKernelGGL((k_conv_strip<f16_t, 4, 3, 5>), dim3(sgx, gy, 1), dim3(512), 0, st, a, sg, conv_flags());
-    else
-      hipLaunchKernelGGL((k_conv_strip<bf16_t, 4, 3, 5>), dim3(sgx, gy, 1), dim3(512), 0, st, a, sg, conv_flags());
+    const dim3 grid(sgx, gy, 1);
+    if (a.dtype == ZP_F16) {
+      if (tc == 64) hipLaunchKernelGGL((k_conv_strip<f16_t, 2, 3, 5>), grid, dim3(512), 0, st, a, sg, conv_flags());
+      else hipLaunchKernelGGL((k_conv_strip<f16_t, 4, 3, 5>), grid, dim3(512), 0, st, a, sg, conv_flags());
+    } else {
+      if (tc == 64) hipLaunchKernelGGL((k_conv_strip<bf16_t, 2, 3, 5>), grid, dim3(512), 0, st, a, sg, conv_flags());
+      else hipLaunchKernelGGL((k_conv_strip<bf16_t, 4, 3, 5>), grid, dim3(512), 0, st, a, sg, conv_flags());
+    }
     ZP_LAUNCH_CHECK("zp_conv2d strip");
     return ZP_OK;
   }
@@ -1674,7 +1686,7 @@ extern "C" int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* st
   *tc = conv_tc(*a);
   *tp = conv_tp(*a);
   *stages = *tc == 256 ? 2 : conv_stages(*tp / 64);
-  *variant = *tc == 128 && strip_eligible(*a, nullptr) ? 1 : 0;
+  *variant = *tc <= 128 && strip_eligible(*a, nullptr) ? 1 : 0;
   return ZP_OK;
 }
 
