@@ -125,7 +125,8 @@ int zp_pack_weight(const float* src, int d0, int d1, int kh, int kw, int transpo
 
 /* Many zp_pack_weight jobs in one launch (training repacks every conv's weights once per
  * optimizer step).  `jobs` and `prefix` are DEVICE arrays: prefix[i] = sum of rows_pad*k_pad of
- * jobs before i (prefix[n] = total elements).  Same element mapping as zp_pack_weight. */
+ * jobs before i (prefix[n] = total elements; validated, the kernel maps one grid row per job,
+ * n <= 65535).  Same element mapping as zp_pack_weight. */
 typedef struct zp_pack_job {
   const float* src;
   void* dst;

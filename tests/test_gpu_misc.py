@@ -49,3 +49,49 @@ def test_nchw_to_nhwc(gpu, prec, cpad):
     want = torch.zeros(2, 9, 14, cpad)
     want[..., :3] = x.permute(0, 2, 3, 1)
     assert torch.equal(y.cpu().float(), want.to(dt).float())
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32, torch.float16])
+def test_pack_weight_multi_matches_single_packs(gpu, dt):
+    """The batched repack of training (one grid row per job) against zp_pack_weight job by job:
+    plain 3x3, a tap subset (ConvT phase), transposed (dgrad / ConvT layout), a padded-channel stem
+    (cstride 8 > 3 channels, k_pad tail) and a 1x1 with padded rows."""
+    import ctypes as C
+    from zebrapose_amd import _lib as L
+    torch.manual_seed(0)
+    code = L.dtype_code(dt)
+    specs = [  # d0, d1, k, transposed, taps, cstride, rows_pad, k_pad
+        (128, 64, 3, 0, [(i // 3, i % 3) for i in range(9)], 64, 128, 576),
+        (64, 96, 3, 0, [(0, 0), (0, 2), (2, 0), (2, 2)], 96, 64, 384),
+        (96, 64, 3, 1, [(i // 3, i % 3) for i in range(9)], 96, 64, 896),
+        (64, 3, 7, 0, [(i // 7, i % 7) for i in range(49)], 8, 64, 448),
+        (17, 320, 1, 0, [(0, 0)], 320, 32, 320),
+    ]
+    jobs, singles, outs = [], [], []
+    srcs = []
+    for d0, d1, k, tr, taps, cs, rp, kp in specs:
+        src = torch.randn(d0, d1, k, k, device="cuda")
+        srcs.append(src)
+        ky = [t[0] for t in taps]
+        kx = [t[1] for t in taps]
+        ref = torch.empty((rp, kp), dtype=dt, device="cuda")
+        L.call("zp_pack_weight", src.data_ptr(), d0, d1, k, k, tr, len(taps), (C.c_int * len(ky))(*ky),
+               (C.c_int * len(kx))(*kx), cs, code, ref.data_ptr(), rp, kp, L.stream_ptr())
+        got = torch.full((rp, kp), 7.0, dtype=dt, device="cuda")  # garbage: every element must be written
+        j = L.PackJob()
+        j.src, j.dst, j.d0, j.d1, j.kh, j.kw, j.transposed = src.data_ptr(), got.data_ptr(), d0, d1, k, k, tr
+        j.ntaps, j.cstride, j.rows_pad, j.k_pad, j.dtype = len(taps), cs, rp, kp, code
+        for t, (a, b) in enumerate(taps):
+            j.ky[t], j.kx[t] = a, b
+        jobs.append(j)
+        singles.append(ref)
+        outs.append(got)
+    arr = (L.PackJob * len(jobs))(*jobs)
+    table = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).cuda()
+    pre = [0]
+    for j in jobs:
+        pre.append(pre[-1] + j.rows_pad * j.k_pad)
+    prefix = torch.tensor(pre, dtype=torch.int64, device="cuda")
+    L.call("zp_pack_weight_multi", len(jobs), table.data_ptr(), prefix.data_ptr(), pre[-1], L.stream_ptr())
+    for ref, got in zip(singles, outs):
+        assert torch.equal(ref, got)

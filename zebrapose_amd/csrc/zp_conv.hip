@@ -1329,6 +1329,8 @@ static bool strip_eligible(const zp_conv_args& a, strip_geo* sg);
 // idle (128 -> 128 at 32x32, bs 32: 128 workgroups; 24.2 -> 22.7 us).  64-channel layers stay on
 // k_conv's 128-pixel tiles (27.5 us there vs 29.2 us as a 64-channel strip).
 static int strip_tc(const zp_conv_args& a) {
+  static const int en64 = getenv("ZP_STRIP_TC64") ? env_int("ZP_STRIP_TC64") : 1;
+  if (!en64) return 128;
   const long tiles = (long)a.N * a.GH * a.GW / 256;
   if (tiles * ((a.Cout + 127) / 128) < 256) return 64;
   return 128;

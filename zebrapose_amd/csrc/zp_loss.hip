@@ -85,43 +85,54 @@ __global__ void __launch_bounds__(256) k_code_partials(const float* __restrict__
   if (threadIdx.x == 0) out[2 * L] = m;
 }
 
-__global__ void __launch_bounds__(256) k_code_finalize(const double* __restrict__ part, int nblk, int B, int L, int HW,
-                                                       int use_hist, double* __restrict__ hist, double* __restrict__ out,
-                                                       double* __restrict__ coef) {
+// column sums of the per-block partials: one block per column (same summation order as a
+// single block walking the columns, so the result is unchanged and deterministic)
+__global__ void __launch_bounds__(256) k_code_colsum(const double* __restrict__ part, int nblk, int nv,
+                                                     double* __restrict__ tot) {
   __shared__ double sh[4];
-  __shared__ double tot[2 * LOSS_MAXL + 1];
-  const int nv = 2 * L + 1;
-  for (int j = 0; j < nv; ++j) {
-    double s = 0;
-    for (int k = threadIdx.x; k < nblk; k += 256) s += part[(size_t)k * nv + j];
-    s = block_sum(s, sh);
-    if (threadIdx.x == 0) tot[j] = s;
+  const int j = blockIdx.x;
+  double s = 0;
+  for (int k = threadIdx.x; k < nblk; k += 256) s += part[(size_t)k * nv + j];
+  s = block_sum(s, sh);
+  if (threadIdx.x == 0) tot[j] = s;
+}
+
+// per-bit work (EMA histogram, weight exp) on lane i < L, the sums serially on lane 0 in bit order
+// (the reference's summation order)
+__global__ void __launch_bounds__(64) k_code_finalize(const double* __restrict__ tot, int B, int L, int HW,
+                                                      int use_hist, double* __restrict__ hist,
+                                                      double* __restrict__ out, double* __restrict__ coef) {
+  __shared__ double sw[LOSS_MAXL], shn[LOSS_MAXL];
+  const int i = threadIdx.x;
+  const double msum = tot[2 * L];
+  const bool first = hist[L] == 0.0;
+  if (i < L) {
+    const double hn = tot[i] / (msum + 1.0);
+    shn[i] = hn;
+    if (use_hist) {
+      const double h = first ? hn : hn * 0.05 + hist[i] * 0.95;
+      hist[i] = h;
+      sw[i] = exp(fmin(h, 0.51 - h) * 3.0);
+    } else {
+      sw[i] = 1.0;
+    }
   }
   __syncthreads();
-  if (threadIdx.x != 0) return;
-  const double N = (double)B * HW;
-  const double msum = tot[2 * L];
-  double w[LOSS_MAXL];
-  double wsum = 0, hmean = 0;
-  const bool first = hist[L] == 0.0;
-  for (int i = 0; i < L; ++i) {
-    double hn = tot[i] / (msum + 1.0);
-    hmean += hn;
-    if (use_hist) {
-      double h = first ? hn : hn * 0.05 + hist[i] * 0.95;
-      hist[i] = h;
-      w[i] = exp(fmin(h, 0.51 - h) * 3.0);
-    } else {
-      w[i] = 1.0;
+  if (i == 0) {
+    const double N = (double)B * HW;
+    double wsum = 0, hmean = 0, lb = 0;
+    for (int k = 0; k < L; ++k) {
+      hmean += shn[k];
+      wsum += sw[k];
     }
-    wsum += w[i];
+    if (use_hist) hist[L] = 1.0;
+    for (int k = 0; k < L; ++k) lb += (tot[L + k] / N) * sw[k];
+    out[0] = lb / wsum;
+    out[1] = hmean / L;
+    shn[0] = wsum;  // hn no longer needed
   }
-  if (use_hist) hist[L] = 1.0;
-  double lb = 0;
-  for (int i = 0; i < L; ++i) lb += (tot[L + i] / N) * w[i];
-  out[0] = lb / wsum;
-  out[1] = hmean / L;
-  for (int i = 0; i < L; ++i) coef[i] = w[i] / wsum / N;
+  __syncthreads();
+  if (i < L) coef[i] = sw[i] / shn[0] / ((double)B * HW);
 }
 
 __global__ void k_code_grad(const float* __restrict__ clog, const double* __restrict__ m01,
@@ -187,7 +198,7 @@ using namespace zp;
 
 extern "C" long long zp_code_loss_ws_bytes(int B, int L, int H, int W) {
   long long N = (long long)B * H * W;
-  return ((N + 255) / 256) * (2LL * L + 1) * 8 + 64;
+  return ((N + 255) / 256) * (2LL * L + 1) * 8 + (2LL * LOSS_MAXL + 1) * 8 + 64;
 }
 
 extern "C" int zp_code_loss(const float* code_logits, const double* mask01, const float* mask_logits, const void* gt,
@@ -204,8 +215,12 @@ extern "C" int zp_code_loss(const float* code_logits, const double* mask01, cons
   hipLaunchKernelGGL(k_code_partials, dim3(nblk), dim3(256), 0, st, code_logits, mask01, mask_logits, gt, gt_f64, B, L,
                      HW, mask_code, part);
   ZP_LAUNCH_CHECK("zp_code_loss partials");
-  hipLaunchKernelGGL(k_code_finalize, dim3(1), dim3(256), 0, st, (const double*)part, nblk, B, L, HW, use_hist,
-                     hist_state, out, coef);
+  const int nv = 2 * L + 1;
+  double* tot = part + (size_t)nblk * nv;
+  hipLaunchKernelGGL(k_code_colsum, dim3(nv), dim3(256), 0, st, (const double*)part, nblk, nv, tot);
+  ZP_LAUNCH_CHECK("zp_code_loss colsum");
+  hipLaunchKernelGGL(k_code_finalize, dim3(1), dim3(64), 0, st, (const double*)tot, B, L, HW, use_hist, hist_state,
+                     out, coef);
   ZP_LAUNCH_CHECK("zp_code_loss finalize");
   return ZP_OK;
 }

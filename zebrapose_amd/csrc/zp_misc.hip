@@ -93,33 +93,43 @@ __global__ void k_pack(const PackArgs a) {
   }
 }
 
-// one launch for many pack jobs: element e -> job by binary search over the element prefix
-__global__ void k_pack_multi(const zp_pack_job* __restrict__ jobs, const long long* __restrict__ prefix, int n,
-                             long long total) {
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-       e += (long long)gridDim.x * blockDim.x) {
-    int lo = 0, hi = n - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (prefix[mid] <= e) lo = mid;
-      else hi = mid - 1;
+// one launch for many pack jobs: blockIdx.y = job (read once, uniform), threads over the job's
+// (row, channel) pairs; each thread reads its pair's kh x kw taps (contiguous in the checkpoint
+// layout, so a wave reads one contiguous span) and writes them at k = t * cstride + c (adjacent
+// threads -> adjacent k: coalesced 2-byte stores), then the pair's share of the k_pad tail (zeros).
+// Same result as zp_pack_weight per job.
+__device__ __forceinline__ void pack_store(const zp_pack_job& a, int d, float v) {
+  if (a.dtype == ZP_BF16) ((bf16_t*)a.dst)[d] = f2bf(v);
+  else if (a.dtype == ZP_F16) ((f16_t*)a.dst)[d] = (f16_t)v;
+  else ((float*)a.dst)[d] = v;
+}
+
+__global__ void __launch_bounds__(256) k_pack_multi(const zp_pack_job* __restrict__ jobs) {
+  const zp_pack_job& a = jobs[blockIdx.y];
+  // tap offsets in LDS (a private copy of the job's tap arrays would live in scratch)
+  __shared__ int toff[ZP_MAX_TAPS];
+  if ((int)threadIdx.x < a.ntaps) toff[threadIdx.x] = a.ky[threadIdx.x] * a.kw + a.kx[threadIdx.x];
+  __syncthreads();
+  const int rows = a.transposed ? a.d1 : a.d0;
+  const int chans = a.transposed ? a.d0 : a.d1;
+  const int pairs = a.rows_pad * a.cstride;
+  const int kt = a.ntaps * a.cstride, khw = a.kh * a.kw;
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < pairs; q += gridDim.x * blockDim.x) {
+    const int r = q / a.cstride, c = q - r * a.cstride;
+    const bool live = r < rows && c < chans;
+    const float* sp = a.src + (a.transposed ? ((size_t)c * a.d1 + r) : ((size_t)r * a.d1 + c)) * khw;
+    const int o = r * a.k_pad + c;
+    if (a.ntaps <= 9) {  // all loads in flight before the stores
+      float v[9];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) v[t] = (live && t < a.ntaps) ? sp[toff[t]] : 0.f;
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+        if (t < a.ntaps) pack_store(a, o + t * a.cstride, v[t]);
+    } else {
+      for (int t = 0; t < a.ntaps; ++t) pack_store(a, o + t * a.cstride, live ? sp[toff[t]] : 0.f);
     }
-    const zp_pack_job& a = jobs[lo];
-    const long long le = e - prefix[lo];
-    const int r = (int)(le / a.k_pad), k = (int)(le - (long long)r * a.k_pad);
-    const int rows = a.transposed ? a.d1 : a.d0;
-    const int chans = a.transposed ? a.d0 : a.d1;
-    const int t = k / a.cstride, c = k - t * a.cstride;
-    float v = 0.f;
-    if (r < rows && t < a.ntaps && c < chans) {
-      const int ky = a.ky[t], kx = a.kx[t];
-      const size_t idx = a.transposed ? (((size_t)c * a.d1 + r) * a.kh + ky) * a.kw + kx
-                                      : (((size_t)r * a.d1 + c) * a.kh + ky) * a.kw + kx;
-      v = a.src[idx];
-    }
-    if (a.dtype == ZP_BF16) ((bf16_t*)a.dst)[le] = f2bf(v);
-    else if (a.dtype == ZP_F16) ((f16_t*)a.dst)[le] = (f16_t)v;
-    else ((float*)a.dst)[le] = v;
+    for (int kk = kt + c; kk < a.k_pad; kk += a.cstride) pack_store(a, r * a.k_pad + kk, 0.f);
   }
 }
 
@@ -871,10 +881,10 @@ extern "C" int zp_pack_weight(const float* src, int d0, int d1, int kh, int kw, 
 
 extern "C" int zp_pack_weight_multi(int n, const zp_pack_job* jobs, const long long* prefix, long long total,
                                     void* stream) {
-  ZP_CHECK_ARG(n >= 0 && total >= 0 && (n == 0 || (jobs && prefix)), "zp_pack_weight_multi: bad args");
+  ZP_CHECK_ARG(n >= 0 && n <= 65535 && total >= 0 && total < (1ll << 40) && (n == 0 || (jobs && prefix)),
+               "zp_pack_weight_multi: bad args");
   if (n == 0 || total == 0) return ZP_OK;
-  hipLaunchKernelGGL(k_pack_multi, dim3(grid_for(total, 256, 16384)), dim3(256), 0, (hipStream_t)stream, jobs, prefix,
-                     n, total);
+  hipLaunchKernelGGL(k_pack_multi, dim3(256, n), dim3(256), 0, (hipStream_t)stream, jobs);
   ZP_LAUNCH_CHECK("zp_pack_weight_multi");
   return ZP_OK;
 }
