@@ -201,3 +201,32 @@ def test_maxpool(gpu, prec):
            0, 1, L.stream_ptr())
     got = dx.float().permute(0, 3, 1, 2).cpu()
     assert (got - xx.grad).abs().max().item() <= (1e-6 if prec == "fp32" else 2e-2)
+
+
+@pytest.mark.parametrize("ih,iw", [(128, 128), (9, 14), (2, 3), (1, 1)])
+def test_maxpool_bwd_channel_slices(gpu, ih, iw):
+    """Backward of the stem max pool into a channel slice of a wider buffer (ld/c0 offsets) without
+    accumulation, odd and tiny extents included, against torch's max_pool2d backward (bf16 values,
+    so ties between equal inputs occur and the first-maximum rule is exercised)."""
+    from zebrapose_amd import _lib as L
+    torch.manual_seed(3)
+    B, C, ld, c0 = 3, 64, 80, 8
+    x = (torch.randn(B, C, ih, iw) * 4).round().to(torch.bfloat16).float()  # many exact ties
+    xx = x.clone().requires_grad_(True)
+    y = F.max_pool2d(xx, 3, 2, 1)
+    g = torch.randn_like(y).to(torch.bfloat16).float()
+    y.backward(g)
+    OH, OW = y.shape[2], y.shape[3]
+    xb = torch.zeros(B, ih, iw, ld, dtype=torch.bfloat16)
+    xb[..., c0:c0 + C] = x.permute(0, 2, 3, 1).to(torch.bfloat16)
+    gb = torch.zeros(B, OH, OW, ld, dtype=torch.bfloat16)
+    gb[..., c0:c0 + C] = g.permute(0, 2, 3, 1).to(torch.bfloat16)
+    xd, gd = xb.to(gpu), gb.to(gpu)
+    dx = torch.full((B, ih, iw, ld), 5.0, dtype=torch.bfloat16, device=gpu)
+    L.call("zp_maxpool3s2_bwd", xd.data_ptr(), ld, c0, gd.data_ptr(), ld, c0, B, ih, iw, C, OH, OW,
+           L.dtype_code(torch.bfloat16), dx.data_ptr(), ld, c0, 0, L.stream_ptr())
+    got = dx.cpu().float()
+    assert torch.equal(got[..., :c0], torch.full_like(got[..., :c0], 5.0))  # outside the slice untouched
+    assert torch.equal(got[..., c0 + C:], torch.full_like(got[..., c0 + C:], 5.0))
+    want = xx.grad.permute(0, 2, 3, 1).to(torch.bfloat16).float()
+    assert (got[..., c0:c0 + C] - want).abs().max().item() <= 2e-2

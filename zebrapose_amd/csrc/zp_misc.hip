@@ -267,13 +267,23 @@ __global__ void k_bn_apply(const T* __restrict__ x, long P, int C, const float* 
   }
 }
 
-constexpr int BNB_PIX = 512;  // pixels per partial slot in the backward reduction
+// Pixels per partial slot of the backward reduction: 16 pixel rows per thread row, fewer (down to
+// 4) while that leaves fewer than 512 slots -- 32x32 layers at 256-512 channels would otherwise
+// run on 64 workgroups (more slots make the totals pass, which reads every slot, the slower one).  Rows per block assume 16-byte bf16 lanes (C/8 lanes, at most 256); any
+// multiple of the kernel's row count works, the fp32 kernel included.
+static inline int bn_bwd_pix(int P, int C) {
+  const int lanes = C / 8 < 256 ? (C / 8 > 0 ? C / 8 : 1) : 256;
+  const int R = 256 / lanes > 0 ? 256 / lanes : 1;
+  int rows = 16;
+  while (rows > 4 && (P + R * rows - 1) / (R * rows) < 512) rows >>= 1;
+  return R * rows;
+}
 
 // block: 256 threads = (C/N) chunk lanes x R rows
 template <typename T>
 __global__ void k_bn_bwd_reduce(const T* __restrict__ dy, int lddy, int cdy0, const T* __restrict__ y, int ldy, int cy0,
                                 const T* __restrict__ x, long P, int C, const float* __restrict__ save, int relu,
-                                float* __restrict__ part, int parts, int cgroups) {
+                                float* __restrict__ part, int parts, int pix) {
   constexpr int N = V16<T>::N;
   __shared__ float red[2][256][N];
   const int CV = C / N;
@@ -282,8 +292,8 @@ __global__ void k_bn_bwd_reduce(const T* __restrict__ dy, int lddy, int cdy0, co
   const int cgi = blockIdx.y;
   const int cl = threadIdx.x % lanes, row = threadIdx.x / lanes;
   const int c = (cgi * lanes + cl) * N;
-  const long p0 = (long)blockIdx.x * BNB_PIX;
-  const long p1 = min(P, p0 + BNB_PIX);
+  const long p0 = (long)blockIdx.x * pix;
+  const long p1 = min(P, p0 + pix);
   float sg[N], sgx[N], mean[N], inv[N];
 #pragma unroll
   for (int i = 0; i < N; ++i) {
@@ -350,7 +360,6 @@ __global__ void k_bn_bwd_reduce(const T* __restrict__ dy, int lddy, int cdy0, co
       part[((size_t)(parts + 1) + blockIdx.x) * C + c + i] = sgx[i];
     }
   }
-  (void)cgroups;
 }
 
 // totals over parts -> part[0][parts][c], part[1][parts][c]; dgamma / dbeta
@@ -362,9 +371,22 @@ __global__ void __launch_bounds__(1024) k_bn_bwd_totals(float* __restrict__ part
   const int c = blockIdx.x * 32 + cl;
   double s = 0, q = 0;
   if (c < C)
-    for (int k = pl; k < parts; k += 32) {
-      s += part[(size_t)k * C + c];
-      q += part[((size_t)parts + 1 + k) * C + c];
+    for (int k0 = pl; k0 < parts; k0 += 32 * 8) {
+      // eight parts' loads in flight, summed in part order
+      // (clamped, unconditional loads: no branch between them)
+      float a[8], b[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int k = min(k0 + 32 * u, parts - 1);
+        a[u] = part[(size_t)k * C + c];
+        b[u] = part[((size_t)parts + 1 + k) * C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const bool in = k0 + 32 * u < parts;
+        s += in ? (double)a[u] : 0.0;
+        q += in ? (double)b[u] : 0.0;
+      }
     }
   sh[0][pl][cl] = s;
   sh[1][pl][cl] = q;
@@ -380,6 +402,19 @@ __global__ void __launch_bounds__(1024) k_bn_bwd_totals(float* __restrict__ part
   if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)s : (float)s;
 }
 
+// N consecutive per-channel floats (16-byte aligned: c and C are multiples of N)
+template <int N>
+__device__ __forceinline__ void load_chan(const float* __restrict__ p, float* v) {
+#pragma unroll
+  for (int i = 0; i < N; i += 4) {
+    const float4 q = *(const float4*)(p + i);
+    v[i] = q.x;
+    v[i + 1] = q.y;
+    v[i + 2] = q.z;
+    v[i + 3] = q.w;
+  }
+}
+
 template <typename T>
 __global__ void k_bn_bwd_apply(const T* __restrict__ dy, int lddy, int cdy0, const T* __restrict__ y, int ldy, int cy0,
                                const T* __restrict__ x, long P, int C, const float* __restrict__ save,
@@ -389,6 +424,9 @@ __global__ void k_bn_bwd_apply(const T* __restrict__ dy, int lddy, int cdy0, con
   const int CV = C / N;
   const long total = P * CV;
   const float invP = 1.f / (float)P;
+  // per-channel terms of the current chunk (the grid stride usually keeps a thread on one chunk)
+  int cur = -1;
+  float mean[N], inv[N], sg[N], sgx[N], gm[N];
   for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
     long p = e / CV;
     int c = (int)(e - p * CV) * N;
@@ -401,14 +439,23 @@ __global__ void k_bn_bwd_apply(const T* __restrict__ dy, int lddy, int cdy0, con
     }
     if (dx) {
       V16<T>::load(x + p * C + c, xx);
+      if (c != cur) {
+        cur = c;
+        load_chan<N>(save + c, mean);
+        load_chan<N>(save + C + c, inv);
+        load_chan<N>(part + (size_t)parts * C + c, sg);
+        load_chan<N>(part + ((size_t)parts + 1 + parts) * C + c, sgx);
+        load_chan<N>(gamma + c, gm);
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+          sg[i] *= invP;
+          sgx[i] *= invP;
+        }
+      }
 #pragma unroll
       for (int i = 0; i < N; ++i) {
-        int cc = c + i;
-        float mean = save[cc], inv = save[C + cc];
-        float sg = part[(size_t)parts * C + cc] * invP;
-        float sgx = part[((size_t)parts + 1 + parts) * C + cc] * invP;
-        float xh = (xx[i] - mean) * inv;
-        o[i] = gamma[cc] * inv * (g[i] - sg - xh * sgx);
+        float xh = (xx[i] - mean[i]) * inv[i];
+        o[i] = gm[i] * inv[i] * (g[i] - sg[i] - xh * sgx[i]);
       }
       V16<T>::store(dx + p * C + c, o);
     }
@@ -549,67 +596,112 @@ __global__ void k_maxpool(const T* __restrict__ x, int B, int IH, int IW, int ld
   }
 }
 
-// gather form: each input element receives dy of every window whose (first) argmax it is
+// Window (oy, ox) of the 3x3 / stride-2 / pad-1 pool: per channel, the tap (ky*3+kx, -1 when the
+// window lies outside the output) of its first maximum in (ky, kx) scan order (PyTorch CPU rule:
+// `>` or NaN) and the window's dy.
 template <typename T>
-__global__ void k_maxpool_bwd(const T* __restrict__ x, int ldx, int cx0, const T* __restrict__ dy, int lddy, int cdy0,
-                              int B, int IH, int IW, int C, int OH, int OW, T* __restrict__ dx, int lddx, int cdx0,
-                              int accumulate) {
+__device__ __forceinline__ void mp_window(const T* __restrict__ x, int ldx, int cx0, const T* __restrict__ dy,
+                                          int lddy, int cdy0, int b, int c, int IH, int IW, int OH, int OW, int oy,
+                                          int ox, int* pos, float* g) {
   constexpr int N = V16<T>::N;
-  const int CV = C / N;
-  const long total = (long)B * IH * IW * CV;
-  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    long pix = e / CV;
-    int c = (int)(e - pix * CV) * N;
-    int ix = (int)(pix % IW);
-    long t = pix / IW;
-    int iy = (int)(t % IH), b = (int)(t / IH);
-    float acc[N];
 #pragma unroll
-    for (int i = 0; i < N; ++i) acc[i] = 0.f;
-    int oy0 = (iy) / 2, oy1 = (iy + 1) / 2;  // windows oy with 2oy-1 <= iy <= 2oy+1
-    int ox0 = (ix) / 2, ox1 = (ix + 1) / 2;
-    for (int oy = oy0; oy <= oy1 && oy < OH; ++oy) {
-      if (oy * 2 - 1 > iy || oy * 2 + 1 < iy) continue;
-      for (int ox = ox0; ox <= ox1 && ox < OW; ++ox) {
-        if (ox * 2 - 1 > ix || ox * 2 + 1 < ix) continue;
-        float m[N];
-        int am[N];
+  for (int i = 0; i < N; ++i) pos[i] = -1;
+  if (oy >= OH || ox >= OW) return;
+  float m[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) m[i] = -INFINITY;
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky) {
+    const int yy = oy * 2 - 1 + ky;
+    if ((unsigned)yy >= (unsigned)IH) continue;
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      const int xx = ox * 2 - 1 + kx;
+      if ((unsigned)xx >= (unsigned)IW) continue;
+      float v[N];
+      V16<T>::load(x + (((size_t)b * IH + yy) * IW + xx) * ldx + cx0 + c, v);
+#pragma unroll
+      for (int i = 0; i < N; ++i)
+        if (v[i] > m[i] || isnan(v[i])) {
+          m[i] = v[i];
+          pos[i] = ky * 3 + kx;
+        }
+    }
+  }
+  V16<T>::load(dy + (((size_t)b * OH + oy) * OW + ox) * lddy + cdy0 + c, g);
+}
+
+// Backward of the 3x3 / stride-2 / pad-1 max pool, gather form without atomics.  A thread owns the
+// 2x2 input block (rows 2k, 2k+1; cols 2j, 2j+1) for one 16-byte channel vector, over a chunk of
+// MP_ROWS consecutive k.  Row 2k lies only in window row k, row 2k+1 in window rows k and k+1 (same
+// for columns), so the block needs windows (k|k+1, j|j+1); the k+1 pair is carried to the next k,
+// i.e. two windows (18 loads) per block instead of a window walk per input pixel.  Contributions are
+// added in (oy, ox) order, then the existing dx when accumulating.
+constexpr int MP_ROWS = 4;
+template <typename T>
+__global__ void __launch_bounds__(256) k_maxpool_bwd(const T* __restrict__ x, int ldx, int cx0,
+                                                     const T* __restrict__ dy, int lddy, int cdy0, int B, int IH,
+                                                     int IW, int C, int OH, int OW, T* __restrict__ dx, int lddx,
+                                                     int cdx0, int accumulate) {
+  constexpr int N = V16<T>::N;
+  const int CV = C / N, JP = (IW + 1) / 2, KP = (IH + 1) / 2, KC = (KP + MP_ROWS - 1) / MP_ROWS;
+  const long total = (long)B * KC * JP * CV;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % CV) * N;
+    long t = e / CV;
+    const int j = (int)(t % JP);
+    t /= JP;
+    const int kc = (int)(t % KC), b = (int)(t / KC);
+    const int k0 = kc * MP_ROWS, k1 = min(k0 + MP_ROWS, KP);
+    int p00[N], p01[N], p10[N], p11[N];
+    float g00[N], g01[N], g10[N], g11[N];
+    mp_window(x, ldx, cx0, dy, lddy, cdy0, b, c, IH, IW, OH, OW, k0, j, p00, g00);
+    mp_window(x, ldx, cx0, dy, lddy, cdy0, b, c, IH, IW, OH, OW, k0, j + 1, p01, g01);
+    for (int k = k0; k < k1; ++k) {
+      mp_window(x, ldx, cx0, dy, lddy, cdy0, b, c, IH, IW, OH, OW, k + 1, j, p10, g10);
+      mp_window(x, ldx, cx0, dy, lddy, cdy0, b, c, IH, IW, OH, OW, k + 1, j + 1, p11, g11);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int iy = 2 * k + (q >> 1), ix = 2 * j + (q & 1);
+        if (iy >= IH || ix >= IW) continue;
+        float acc[N];
 #pragma unroll
         for (int i = 0; i < N; ++i) {
-          m[i] = -INFINITY;
-          am[i] = -1;
-        }
-        for (int ky = 0; ky < 3; ++ky) {
-          int yy = oy * 2 - 1 + ky;
-          if ((unsigned)yy >= (unsigned)IH) continue;
-          for (int kx = 0; kx < 3; ++kx) {
-            int xx = ox * 2 - 1 + kx;
-            if ((unsigned)xx >= (unsigned)IW) continue;
-            float v[N];
-            V16<T>::load(x + (((size_t)b * IH + yy) * IW + xx) * ldx + cx0 + c, v);
-#pragma unroll
-            for (int i = 0; i < N; ++i)
-              if (v[i] > m[i] || isnan(v[i])) {
-                m[i] = v[i];
-                am[i] = yy * IW + xx;
-              }
+          float a = 0.f;
+          // taps of (iy, ix) in windows (k, j), (k, j+1), (k+1, j), (k+1, j+1)
+          if (q == 0) {
+            if (p00[i] == 4) a += g00[i];
+          } else if (q == 1) {
+            if (p00[i] == 5) a += g00[i];
+            if (p01[i] == 3) a += g01[i];
+          } else if (q == 2) {
+            if (p00[i] == 7) a += g00[i];
+            if (p10[i] == 1) a += g10[i];
+          } else {
+            if (p00[i] == 8) a += g00[i];
+            if (p01[i] == 6) a += g01[i];
+            if (p10[i] == 2) a += g10[i];
+            if (p11[i] == 0) a += g11[i];
           }
+          acc[i] = a;
         }
-        float g[N];
-        V16<T>::load(dy + (((size_t)b * OH + oy) * OW + ox) * lddy + cdy0 + c, g);
+        T* o = dx + (((size_t)b * IH + iy) * IW + ix) * lddx + cdx0 + c;
+        if (accumulate) {
+          float r[N];
+          V16<T>::load(o, r);
 #pragma unroll
-        for (int i = 0; i < N; ++i)
-          if (am[i] == iy * IW + ix) acc[i] += g[i];
+          for (int i = 0; i < N; ++i) acc[i] += r[i];
+        }
+        V16<T>::store(o, acc);
+      }
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        p00[i] = p10[i];
+        g00[i] = g10[i];
+        p01[i] = p11[i];
+        g01[i] = g11[i];
       }
     }
-    T* o = dx + pix * lddx + cdx0 + c;
-    if (accumulate) {
-      float r[N];
-      V16<T>::load(o, r);
-#pragma unroll
-      for (int i = 0; i < N; ++i) acc[i] += r[i];
-    }
-    V16<T>::store(o, acc);
   }
 }
 
@@ -942,8 +1034,8 @@ extern "C" int zp_bn_apply(const void* x, int P, int C, const float* scale, cons
 }
 
 extern "C" int zp_bn_bwd_parts(int P, int C) {
-  (void)C;
-  return (P + BNB_PIX - 1) / BNB_PIX;
+  const int pix = bn_bwd_pix(P, C);
+  return (P + pix - 1) / pix;
 }
 
 extern "C" int zp_bn_bwd_reduce(const void* dy, int lddy, int cdy0, const void* y, int ldy, int cy0, const void* x, int P,
@@ -956,14 +1048,15 @@ extern "C" int zp_bn_bwd_reduce(const void* dy, int lddy, int cdy0, const void* 
   const int parts = zp_bn_bwd_parts(P, C);
   const int CV = C / N;
   const int cgroups = CV > 256 ? CV / 256 : 1;
+  const int pix = bn_bwd_pix(P, C);
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(parts, cgroups);
   if (dtype == ZP_BF16)
     hipLaunchKernelGGL(k_bn_bwd_reduce<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)dy, lddy, cdy0, (const bf16_t*)y,
-                       ldy, cy0, (const bf16_t*)x, (long)P, C, save, relu, partials, parts, cgroups);
+                       ldy, cy0, (const bf16_t*)x, (long)P, C, save, relu, partials, parts, pix);
   else
     hipLaunchKernelGGL(k_bn_bwd_reduce<float>, grid, dim3(256), 0, st, (const float*)dy, lddy, cdy0, (const float*)y,
-                       ldy, cy0, (const float*)x, (long)P, C, save, relu, partials, parts, cgroups);
+                       ldy, cy0, (const float*)x, (long)P, C, save, relu, partials, parts, pix);
   ZP_LAUNCH_CHECK("zp_bn_bwd_reduce");
   hipLaunchKernelGGL(k_bn_bwd_totals, dim3((C + 31) / 32), dim3(1024), 0, st, partials, parts, C, dgamma, dbeta,
                      accumulate);
@@ -1036,7 +1129,8 @@ extern "C" int zp_maxpool3s2_bwd(const void* x, int ldx, int cx0, const void* dy
   const int N = dtype == ZP_F32 ? 4 : 8;
   ZP_CHECK_ARG(x && dy && dx && C % N == 0 && cx0 % N == 0 && cdy0 % N == 0 && cdx0 % N == 0,
                "zp_maxpool3s2_bwd: bad args");
-  long total = (long)B * IH * IW * (C / N);
+  ZP_CHECK_ARG(OH == (IH + 1) / 2 && OW == (IW + 1) / 2, "zp_maxpool3s2_bwd: OH/OW must be the 3x3 s2 p1 output");
+  const long total = (long)B * (((IH + 1) / 2 + MP_ROWS - 1) / MP_ROWS) * ((IW + 1) / 2) * (C / N);
   ZP_TLAUNCH(dtype, k_maxpool_bwd, dim3(grid_for(total)), (hipStream_t)stream, (const T*)x, ldx, cx0, (const T*)dy,
              lddy, cdy0, B, IH, IW, C, OH, OW, (T*)dx, lddx, cdx0, accumulate);
   ZP_LAUNCH_CHECK("zp_maxpool3s2_bwd");

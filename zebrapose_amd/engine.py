@@ -624,11 +624,14 @@ class Engine:
         self.unit_fwd(last, mid, out, tape, res=res, label="enc")
         return out
 
-    def backward(self, tape, dmask, dcode, dentire=None):
+    def backward(self, tape, dmask, dcode, dentire=None, grads=None):
         """Returns {parameter: gradient} for every parameter of the network.  With the v3 head
         (tape holds a "head3" record), dentire is the entire-mask logits' gradient and the mask
-        resamplings add their gradient into the visible-mask head's before it runs."""
-        gmap, grads = {}, {}
+        resamplings add their gradient into the visible-mask head's before it runs.  ``grads`` is
+        the dict the gradients are assigned into as they are enqueued (parallel.grads_sink: a
+        data-parallel run starts each bucket's all-reduce from those assignments)."""
+        gmap = {}
+        grads = {} if grads is None else grads
         st = L.stream_ptr()
         head_rec = next(r for r in tape.recs if r[0] == "head" and r[3] == "head")
         hin = head_rec[2]

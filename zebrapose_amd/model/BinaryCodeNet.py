@@ -22,6 +22,7 @@ import torch.nn as nn
 
 from .. import _lib as L
 from ..engine import Engine
+from ..parallel import finish_grads, grads_sink
 from .aspp import ASPP, ASPP_50
 from .resnet import ResNet34_OS8, ResNet50_OS8
 
@@ -177,7 +178,8 @@ class _DeepLabFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dmask, dcode):
-        grads = ctx.module._engine.backward(ctx.tape, dmask, dcode)
+        sink = grads_sink(ctx.module)
+        grads = finish_grads(ctx.module, ctx.module._engine.backward(ctx.tape, dmask, dcode, grads=sink))
         ctx.tape = None
         by_ptr = {p.data_ptr(): g for p, g in grads.items()}
         out = []

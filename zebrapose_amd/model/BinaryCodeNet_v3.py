@@ -22,6 +22,7 @@ from .aspp import ASPP
 from .aspp_v3 import ASPP_v3
 from .resnet import ResNet34_OS8
 from ..engine import Engine
+from ..parallel import finish_grads, grads_sink
 
 
 class _DeepLabV3Fn(torch.autograd.Function):
@@ -34,7 +35,8 @@ class _DeepLabV3Fn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dmask, dentire, dcode):
-        grads = ctx.module._engine.backward(ctx.tape, dmask, dcode, dentire)
+        sink = grads_sink(ctx.module)
+        grads = finish_grads(ctx.module, ctx.module._engine.backward(ctx.tape, dmask, dcode, dentire, grads=sink))
         ctx.tape = None
         by_ptr = {p.data_ptr(): g for p, g in grads.items()}
         return (None, None) + tuple(by_ptr.get(k) for k in ctx.keys)

@@ -66,3 +66,145 @@ def max_over_ranks(seconds, device=None):
     t = torch.tensor([float(seconds)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return t.item()
+
+
+class GradBuckets:
+    """DDP's gradient exchange (train_v6.py:252-264 wraps the net in DistributedDataParallel),
+    overlapped with the libzp backward.
+
+    torch's DDP sees the network as one autograd node that returns all 152 gradients at once, so
+    its buckets could only all-reduce after the whole backward.  Here the engine reports each
+    gradient as it is enqueued (``ready``); the gradient is copied into its bucket's flat f32
+    buffer, and when a bucket is complete it is divided by the world size and all-reduced (SUM)
+    with ``async_op=True``.  The collective is ordered after the kernels enqueued so far on the
+    current stream and runs on the process group's own stream (RCCL over xGMI for 'nccl') while
+    the rest of the backward is computed.  ``finish`` makes the current stream wait for every
+    bucket and returns the averaged gradients.
+
+    DDP semantics kept: parameters broadcast from rank 0 at construction, module buffers (BN
+    running statistics) broadcast from rank 0 before every forward (broadcast_buffers=True),
+    buckets of ~25 MB over the parameters in reverse registration order (the backward's order),
+    gradient = mean over ranks (pre-divided, then summed, as DDP does).  Every rank issues the same
+    collectives in the same order because the backward is deterministic.
+    """
+
+    def __init__(self, module, bucket_mb=25.0, group=None):
+        self.module = module
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.params = [p for p in module.parameters() if p.requires_grad]
+        with torch.no_grad():
+            states = [t for t in list(module.parameters()) + list(module.buffers())]
+            if states:
+                dist._broadcast_coalesced(self._pg(), states, 250 * 1024 * 1024, 0)
+        cap = int(bucket_mb * 1024 * 1024)
+        self.buckets = []  # [flat, [params], pending count, work]
+        self.slot = {}  # param -> (bucket index, view)
+        cur, size = [], 0
+        for p in reversed(self.params):
+            cur.append(p)
+            size += p.numel() * p.element_size()
+            if size >= cap:
+                self._add_bucket(cur)
+                cur, size = [], 0
+        if cur:
+            self._add_bucket(cur)
+        self._reset()
+
+    def _pg(self):
+        return self.group if self.group is not None else dist.distributed_c10d._get_default_group()
+
+    def _add_bucket(self, ps):
+        dt, dev = ps[0].dtype, ps[0].device
+        if any(p.dtype != dt or p.device != dev for p in ps):
+            raise ValueError("GradBuckets: one dtype / device per bucket")
+        flat = torch.empty(sum(p.numel() for p in ps), dtype=dt, device=dev)
+        b = len(self.buckets)
+        off = 0
+        for p in ps:
+            self.slot[p] = (b, flat[off:off + p.numel()].view_as(p))
+            off += p.numel()
+        self.buckets.append([flat, ps, 0, None])
+
+    def _reset(self):
+        for bk in self.buckets:
+            bk[2] = len(bk[1])
+            bk[3] = None
+        self.seen = set()
+
+    def sync_buffers(self):
+        """DDP broadcast_buffers=True: rank 0's BN running statistics before every forward."""
+        bufs = list(self.module.buffers())
+        if bufs:
+            with torch.no_grad():
+                dist._broadcast_coalesced(self._pg(), bufs, 250 * 1024 * 1024, 0)
+
+    def _launch(self, b):
+        bk = self.buckets[b]
+        bk[0].div_(self.world)
+        bk[3] = dist.all_reduce(bk[0], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+
+    def ready(self, p, g):
+        """Gradient g of parameter p has been enqueued on the current stream."""
+        s = self.slot.get(p)
+        if s is None:
+            return
+        if p in self.seen:
+            raise RuntimeError("GradBuckets: a parameter received two gradients in one backward")
+        self.seen.add(p)
+        b, view = s
+        view.copy_(g)
+        self.buckets[b][2] -= 1
+        if self.buckets[b][2] == 0:
+            self._launch(b)
+
+    def finish(self):
+        """Launch any bucket still open (gradients never produced count as zero, in the same order
+        on every rank), wait for all, and return {parameter: averaged gradient view}."""
+        for b, bk in enumerate(self.buckets):
+            if bk[3] is None:
+                for p in bk[1]:
+                    if p not in self.seen:
+                        self.slot[p][1].zero_()
+                self._launch(b)
+        for bk in self.buckets:
+            bk[3].wait()
+        out = {p: self.slot[p][1] for p in self.params}
+        self._reset()
+        return out
+
+
+class _ReadyDict(dict):
+    """The engine's {parameter: gradient} map; each assignment reports to GradBuckets.ready."""
+
+    def __init__(self, reducer):
+        super().__init__()
+        self._reducer = reducer
+
+    def __setitem__(self, k, v):
+        super().__setitem__(k, v)
+        self._reducer.ready(k, v)
+
+
+def grads_sink(module):
+    """The dict the engine backward writes into: a plain dict, or one feeding the module's
+    attached GradBuckets (see attach_grad_buckets)."""
+    red = getattr(module, "_grad_buckets", None)
+    return {} if red is None else _ReadyDict(red)
+
+
+def finish_grads(module, grads):
+    """After the engine backward: the averaged gradients when GradBuckets is attached."""
+    red = getattr(module, "_grad_buckets", None)
+    return grads if red is None else red.finish()
+
+
+def attach_grad_buckets(net, bucket_mb=25.0, group=None):
+    """Attach a GradBuckets to the libzp-executed module(s) inside net (the DeepLabV3 whose
+    autograd node runs the engine backward); returns it."""
+    inner = [m for m in net.modules() if hasattr(m, "_engine")]
+    if len(inner) != 1:
+        raise ValueError("attach_grad_buckets: expected exactly one engine-executed module")
+    red = GradBuckets(net, bucket_mb=bucket_mb, group=group)
+    object.__setattr__(inner[0], "_grad_buckets", red)
+    return red

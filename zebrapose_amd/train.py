@@ -5,17 +5,22 @@ Per step: forward (train-mode BN) -> visible-mask threshold on device (train_v6.
 it on the host in f64) -> loss_b = BinaryCodeLoss('BCE', True, 2, hist=True) (f64) and
 loss_m = MaskLoss -> loss = 3 loss_b + loss_m -> backward -> Adam.  Under torch.distributed
 (one process per GPU, backend 'nccl' = RCCL over xGMI) the network is wrapped in DDP exactly as
-the reference does, so the gradient all-reduce (mean) runs over RCCL; lr is multiplied and the
+the reference does (parallel.GradBuckets: DDP's bucketed mean, its all-reduces started while the
+backward is still running; ZP_TORCH_DDP=1 selects torch's DDP wrapper), so the gradient
+all-reduce (mean) runs over RCCL; lr is multiplied and the
 iteration budget divided by the world size (train_v6.py:82-91); BN statistics stay per rank and
 rank 0's BN buffers are broadcast at every forward (DDP default broadcast_buffers=True).
 """
 from __future__ import annotations
+
+import os
 
 import torch
 import torch.distributed as dist
 
 from .model.BinaryCodeNet import BinaryCodeLoss, MaskLoss
 from .optim import FusedAdam
+from .parallel import attach_grad_buckets
 
 
 def scale_for_world(learning_rate, total_iteration, world_size):
@@ -24,14 +29,19 @@ def scale_for_world(learning_rate, total_iteration, world_size):
 
 
 class TrainStep:
-    def __init__(self, net, learning_rate=2e-4, binary_loss_weight=3.0, ddp=None, device=None):
+    def __init__(self, net, learning_rate=2e-4, binary_loss_weight=3.0, ddp=None, device=None, bucket_mb=25.0):
         self.module = net
         self.net = net
         if ddp is None:
             ddp = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+        self.buckets = None
         if ddp:
-            dev = device if device is not None else torch.cuda.current_device()
-            self.net = torch.nn.parallel.DistributedDataParallel(net, device_ids=[dev])
+            if any(hasattr(m, "_engine") for m in net.modules()) and os.environ.get("ZP_TORCH_DDP", "0") != "1":
+                # DDP semantics with the all-reduce overlapped with the libzp backward
+                self.buckets = attach_grad_buckets(net, bucket_mb=bucket_mb)
+            else:
+                dev = device if device is not None else torch.cuda.current_device()
+                self.net = torch.nn.parallel.DistributedDataParallel(net, device_ids=[dev])
         self.binary_loss_weight = binary_loss_weight
         self.code_loss = BinaryCodeLoss("BCE", True, 2, use_histgramm_weighted_binary_loss=True)
         self.mask_loss = MaskLoss()
@@ -42,6 +52,8 @@ class TrainStep:
         With the 3-head BinaryCodeNet_Deeplab_v3 (train_v5.py:321-332) gt_entire_mask f32 [B,H/2,W/2] is
         required and loss = w * loss_b + loss_mask + loss_entire_mask."""
         self.optimizer.zero_grad(set_to_none=True)
+        if self.buckets is not None:
+            self.buckets.sync_buffers()
         out = self.net(x)
         if len(out) == 3:
             if gt_entire_mask is None:
