@@ -327,14 +327,39 @@ class Engine:
             tape.recs.append(("head", unit, x, key, None, None, None))
 
     # ------------------------------------------------------------------ backward pieces
-    def _grad(self, gmap, act: Act):
-        """gradient slice twin of an activation slice (zero-initialised buffer per activation buffer)."""
+    def _grad_buf(self, gmap, act: Act):
+        """gradient buffer twin of an activation buffer; allocated uninitialised and recorded as
+        fresh (no writer yet) in gmap["__fresh__"]."""
         key = act.buf.data_ptr()
         g = gmap.get(key)
         if g is None:
-            g = torch.zeros_like(act.buf)
+            g = torch.empty_like(act.buf)
             gmap[key] = g
+            gmap.setdefault("__fresh__", set()).add(key)
+        return key, g
+
+    def _grad(self, gmap, act: Act):
+        """gradient slice twin of an activation slice, to be read or accumulated into: a fresh
+        buffer is zeroed first."""
+        key, g = self._grad_buf(gmap, act)
+        fresh = gmap.setdefault("__fresh__", set())
+        if key in fresh:
+            fresh.discard(key)
+            g.zero_()
         return Act(g, act.c0, act.C)
+
+    def _grad_out(self, gmap, act: Act, whole_write):
+        """gradient slice a kernel is about to write -> (slice, accumulate).  The first writer of a
+        buffer that writes all of it (whole_write: every pixel; the slice spans every channel)
+        overwrites instead of accumulating, so the buffer needs no zero fill."""
+        key, g = self._grad_buf(gmap, act)
+        fresh = gmap.setdefault("__fresh__", set())
+        if key in fresh:
+            fresh.discard(key)
+            if whole_write and act.c0 == 0 and act.C == act.ld:
+                return Act(g, act.c0, act.C), False
+            g.zero_()
+        return Act(g, act.c0, act.C), True
 
     def _wgrad(self, unit, x: Act, plan, dy: Act, dw):
         a = L.WgradArgs()
@@ -368,8 +393,9 @@ class Engine:
             return
         L.check(L.lib.zp_conv2d_wgrad(C.byref(a), ws.data_ptr(), L.stream_ptr()), "zp_conv2d_wgrad")
 
-    def _dgrad(self, unit, gy: Act, gx: Act):
-        """gx (+)= dgrad(gy): accumulate into the input gradient slice (residual = itself)."""
+    def _dgrad(self, unit, gy: Act, gx: Act, accumulate=True):
+        """gx (+)= dgrad(gy): accumulate into the input gradient slice (residual = itself), or
+        overwrite it (accumulate False: its first writer, see _grad_out)."""
         plan = unit.dgrad_plan(gx.H, gx.W)
         cin_l = gy.C  # = cout (padded for the head)
         kp = max(self._kpad(len(sb.taps), cin_l) for sb in plan.subs)
@@ -380,7 +406,16 @@ class Engine:
         small = self._small(cin_l, unit.k, -unit.d, -unit.p) if unit.kind == "conv" and unit.s == 1 else None
         if cin_l < _KE[self.dt]:
             assert small is not None, "small-channel dgrad only for stride-1 convs"
-        self._conv(gy, plan, unit.cin, ws, kp, rows, outs, res=gx, relu=False, small=small, label="dgrad")
+        self._conv(gy, plan, unit.cin, ws, kp, rows, outs, res=gx if accumulate else None, relu=False, small=small,
+                   label="dgrad")
+
+    def _dgrad_whole(self, unit, x: Act):
+        """True when the dgrad launch writes every input pixel (one sub whose grid is x's pixels)."""
+        plan = unit.dgrad_plan(x.H, x.W)
+        if len(plan.subs) != 1 or plan.GH != x.H or plan.GW != x.W:
+            return False
+        sb = plan.subs[0]
+        return (sb.oys, sb.oyo, sb.oxs, sb.oxo) == (1, 0, 1, 0)
 
     def unit_bwd(self, rec, gmap, grads, need_dx=True):
         kind, unit, x, out, res, raw, save = rec
@@ -402,11 +437,11 @@ class Engine:
                        unit.cout, save.data_ptr(), int(unit.relu), self.dt, partials.data_ptr(), dgamma.data_ptr(),
                        dbeta.data_ptr(), 0, st)
                 graw = torch.empty_like(raw)
-                gres = self._grad(gmap, res) if res is not None else None
+                gres, racc = self._grad_out(gmap, res, True) if res is not None else (None, True)
                 L.call("zp_bn_bwd_apply", gout.ptr, gout.ld, gout.c0, out.ptr, out.ld, out.c0, raw.data_ptr(), P,
                        unit.cout, save.data_ptr(), partials.data_ptr(), bn.weight.data_ptr(), int(unit.relu),
                        self.dt, graw.data_ptr(), None if gres is None else gres.ptr,
-                       0 if gres is None else gres.ld, 0 if gres is None else gres.c0, 1, st)
+                       0 if gres is None else gres.ld, 0 if gres is None else gres.c0, int(racc), st)
                 grads[bn.weight] = dgamma
                 grads[bn.bias] = dbeta
                 if conv.bias is not None:
@@ -427,7 +462,8 @@ class Engine:
         self._wgrad(unit, x, plan, wdy, dw)
         grads[conv.weight] = dw
         if need_dx:
-            self._dgrad(unit, gy, self._grad(gmap, x))
+            gx, acc = self._grad_out(gmap, x, self._dgrad_whole(unit, x))
+            self._dgrad(unit, gy, gx, accumulate=acc)
 
     # ------------------------------------------------------------------ network
     def forward(self, x, train):
