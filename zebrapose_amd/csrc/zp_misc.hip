@@ -243,6 +243,19 @@ __global__ void k_bn_train_finalize(const float* __restrict__ part, int parts, i
   if (c == 0 && nbt) nbt[0] += 1;
 }
 
+// N consecutive per-channel floats (16-byte aligned: c and C are multiples of N)
+template <int N>
+__device__ __forceinline__ void load_chan(const float* __restrict__ p, float* v) {
+#pragma unroll
+  for (int i = 0; i < N; i += 4) {
+    const float4 q = *(const float4*)(p + i);
+    v[i] = q.x;
+    v[i + 1] = q.y;
+    v[i + 2] = q.z;
+    v[i + 3] = q.w;
+  }
+}
+
 template <typename T>
 __global__ void k_bn_apply(const T* __restrict__ x, long P, int C, const float* __restrict__ scale,
                            const float* __restrict__ shift, const T* __restrict__ res, int ldr, int cr0, int relu,
@@ -250,15 +263,22 @@ __global__ void k_bn_apply(const T* __restrict__ x, long P, int C, const float* 
   constexpr int N = V16<T>::N;
   const int CV = C / N;
   const long total = P * CV;
+  int cur = -1;  // channel chunk whose scale / shift are in registers (16-byte loads)
+  float sc[N], sh[N];
   for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
     long p = e / CV;
     int c = (int)(e - p * CV) * N;
     float v[N], r[N];
     V16<T>::load(x + p * C + c, v);
     if (res) V16<T>::load(res + p * ldr + cr0 + c, r);
+    if (c != cur) {
+      cur = c;
+      load_chan<N>(scale + c, sc);
+      load_chan<N>(shift + c, sh);
+    }
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-      float o = v[i] * scale[c + i] + shift[c + i];
+      float o = v[i] * sc[i] + sh[i];
       if (res) o += r[i];
       if (relu) o = fmaxf(o, 0.f);
       v[i] = o;
@@ -400,19 +420,6 @@ __global__ void __launch_bounds__(1024) k_bn_bwd_totals(float* __restrict__ part
   part[((size_t)parts + 1 + parts) * C + c] = (float)q;
   if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)q : (float)q;
   if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)s : (float)s;
-}
-
-// N consecutive per-channel floats (16-byte aligned: c and C are multiples of N)
-template <int N>
-__device__ __forceinline__ void load_chan(const float* __restrict__ p, float* v) {
-#pragma unroll
-  for (int i = 0; i < N; i += 4) {
-    const float4 q = *(const float4*)(p + i);
-    v[i] = q.x;
-    v[i + 1] = q.y;
-    v[i + 2] = q.z;
-    v[i + 3] = q.w;
-  }
 }
 
 template <typename T>
