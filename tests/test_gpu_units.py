@@ -18,6 +18,10 @@ GEOMS = [
     ("conv", 512, 256, 3, 1, 6, 6, True, 8),
     ("conv", 512, 256, 3, 1, 18, 18, True, 8),
     ("conv", 1280, 256, 1, 1, 0, 1, True, 8),
+    # ASPP at its real 32 x 32 size: 8-row tiles inside one image, so k_conv trims the tap rows
+    # that only ever read padding (dilation 12: first / last tile; dilation 18: every tile)
+    ("conv", 512, 256, 3, 1, 12, 12, True, 32),
+    ("conv", 512, 256, 3, 1, 18, 18, True, 32),
     ("convT", 256, 256, 3, 2, 1, 1, False, 8),
     ("convT", 320, 256, 3, 2, 1, 1, False, 8),
     # full-width tiles (W 32 / 64 / 128): the bf16 activation-strip kernel (k_conv_strip)

@@ -387,7 +387,7 @@ __global__ void __launch_bounds__(128 * NWP) k_conv(const zp_conv_args A, const 
   const T* __restrict__ X = (const T*)A.x;
   const T* __restrict__ Wt = (const T*)S.w;
   const int CB = SMALLC ? 1 : A.Cin / KE;
-  const int nK = SMALLC ? A.k_pad / KE : S.ntaps * CB;
+  int nK = SMALLC ? A.k_pad / KE : S.ntaps * CB;
 
   // ---- staging addresses (Cin >= 64 B-chunk path): buffer loads with per-lane 32-bit byte
   // offsets.  The tap walk (ty, tx, channel chunk) is scalar state advanced by one K step per
@@ -409,11 +409,38 @@ __global__ void __launch_bounds__(128 * NWP) k_conv(const zp_conv_args A, const 
     ymask[i] = gvalid[i] ? ym : 0u;
     xmask[i] = xm;
   }
+  // Tap-row trimming (flags & 16): a tap row whose input rows lie outside the image for every
+  // output row of this tile only ever stages zeros.  A tile inside one image runs just the K
+  // steps of tap rows [qlo, qhi] (the valid rows are contiguous: the row offset is monotonic in
+  // q).  ASPP's dilation-12 / -18 convs at 32 x 32 run 6 of 9 taps on most 8-row tiles.  The
+  // test is scalar (wave-uniform) and conservative: it never drops a row holding a valid tap.
+  int qlo = 0, qhi = ny - 1;
+  if (!SMALLC && (flags & 16) && ny > 1) {
+    const int mlast = min(p0 + TP, M) - 1;
+    const int n0 = p0 / GHW, n1 = mlast / GHW;
+    if (n0 == n1) {
+      const int ya = (p0 - n0 * GHW) / A.GW * A.sy, yb = (mlast - n1 * GHW) / A.GW * A.sy;
+      int lo = ny, hi = -1;
+      for (int q = 0; q < ny; ++q) {
+        const int off = TG.ty0[tb] + q * dty;
+        if (yb + off >= 0 && ya + off <= A.IH - 1) {
+          lo = min(lo, q);
+          hi = q;
+        }
+      }
+      if (hi >= lo) {
+        qlo = lo;
+        qhi = hi;
+        nK = (qhi - qlo + 1) * nx * CB;
+      }
+    }
+  }
+  const int kb0 = qlo * nx * CB;  // first K step (weights are tap-major: K = (q nx + r) CB + cb)
   const unsigned wbase = (unsigned)(((size_t)(c0 + wid * 8 + lrow) * A.k_pad + csrc * E) * sizeof(T));
   // scalar tap walk: the next K step to issue is (tap row tyi, tap column txi, chunk cb) with
   // act_off = ((ty * IW + tx) * ldx + cb * KE) * sizeof(T)
-  int w_tyi = 0, w_txi = 0, w_cb = 0;
-  int act_off = ((TG.ty0[tb] * A.IW + TG.tx0[tb]) * A.ldx) * (int)sizeof(T);
+  int w_tyi = qlo, w_txi = 0, w_cb = 0;
+  int act_off = (((TG.ty0[tb] + qlo * dty) * A.IW + TG.tx0[tb]) * A.ldx) * (int)sizeof(T);
   const int step_x = dtx * A.ldx * (int)sizeof(T), step_y = dty * A.IW * A.ldx * (int)sizeof(T);
   const int chunk_b = KE * (int)sizeof(T);
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -478,7 +505,7 @@ __global__ void __launch_bounds__(128 * NWP) k_conv(const zp_conv_args A, const 
         const int g = wid + NW * i;
         auto* d = (__attribute__((address_space(3))) void*)&dst[g * 64];
         if (i < WPW)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(wrsrc, d, 16, voff[i], ks * chunk_b, 0, 0);
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(wrsrc, d, 16, voff[i], (kb0 + ks) * chunk_b, 0, 0);
         else if (ZP_ABL != 3)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(xrsrc, d, 16, voff[i], 0, 0, 0);
       }
@@ -1361,10 +1388,11 @@ static int conv_stages_override() {
 }
 
 // k_conv schedule switches: bit 1 XCD-aware tile order, bit 2 s_setprio(1) around the MFMA
-// cluster, bit 3 ping-pong (staggered wave groups).  Default (measured, profiles/r01_conv_sweep.md):
-// setprio + ping-pong.  ZP_CONV_FLAGS overrides for sweeps.
+// cluster, bit 3 ping-pong (staggered wave groups), bit 4 tap-row trimming (tap rows that read only
+// padding for a whole tile are skipped).  Default (measured, profiles/r01_conv_sweep.md):
+// setprio + ping-pong + trimming.  ZP_CONV_FLAGS overrides for sweeps.
 static int conv_flags() {
-  static const int v = getenv("ZP_CONV_FLAGS") ? env_int("ZP_CONV_FLAGS") : 12;
+  static const int v = getenv("ZP_CONV_FLAGS") ? env_int("ZP_CONV_FLAGS") : 28;
   return v;
 }
 
