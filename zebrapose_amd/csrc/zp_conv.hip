@@ -1453,10 +1453,16 @@ static int conv_tp(const zp_conv_args& a) {
 }
 
 // LDS ring depth: 3 (measured faster than 2 for both tile shapes; 2 is kept for sweeps)
-static int conv_stages(int nwp) {
-  (void)nwp;
+// LDS ring depth: 3, except for the two launches with very few or gather-bound K steps, where the
+// 2-deep ring's smaller LDS footprint (more resident workgroups) wins (R34 bs 32, layer report):
+// the small-Cin stem (7x7, per-lane tap gather: 100 -> 75 us) and the 32-channel-tile head
+// (1x1 320 -> 17 at 128x128, 5 K steps, HBM-bound: 99 -> 90 us).  Every other k_conv launch loses
+// with 2 stages (ASPP 217 -> 329 us).
+static int conv_stages(const zp_conv_args& a, int tc) {
   const int ov = conv_stages_override();
   if (ov == 2 || ov == 3) return ov;
+  const int ke = a.dtype == ZP_F32 ? 32 : 64;  // elements per K step
+  if (a.Cin < ke || tc <= 32) return 2;
   return 3;
 }
 
@@ -1547,7 +1553,7 @@ extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
     return ZP_OK;
   }
   const int nwp = conv_tp(a) / 64;
-  const int stages = conv_stages(nwp);
+  const int stages = conv_stages(a, tc);
 #define ZP_DISPATCH_ST(T, WC, NWP, ST)                                   \
   if (smallc) launch_conv<T, WC, NWP, ST, true>(a, tg, gx, gy, st);      \
   else launch_conv<T, WC, NWP, ST, false>(a, tg, gx, gy, st);
@@ -1715,7 +1721,7 @@ extern "C" int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* st
   ZP_CHECK_ARG(a && tc && tp && stages && variant, "zp_conv2d_config: null args");
   *tc = conv_tc(*a);
   *tp = conv_tp(*a);
-  *stages = *tc == 256 ? 2 : conv_stages(*tp / 64);
+  *stages = *tc == 256 ? 2 : conv_stages(*a, *tc);
   *variant = *tc <= 128 && strip_eligible(*a, nullptr) ? 1 : 0;
   return ZP_OK;
 }
