@@ -1442,6 +1442,7 @@ static int conv_tp(const zp_conv_args& a) {
   int tc = a.Cout > 64 ? 128 : (a.Cout > 32 ? 64 : 32);
   if (tc == 32) return 128;  // 32 + 256 rows do not split over 8 waves in 8-row groups
   if (strip_eligible(a, nullptr)) return 256;
+  if (conv_tc(a) == 256) return 256;  // the 256-channel tile exists only with 256-pixel tiles
   const int ov = conv_tp_override();
   if (ov == 128 || ov == 256) return ov;
   // Cout <= 128 (one cout tile): 128-pixel tiles double the workgroup count of the 32x32 / 64x64
@@ -1452,7 +1453,6 @@ static int conv_tp(const zp_conv_args& a) {
   return 256;
 }
 
-// LDS ring depth: 3 (measured faster than 2 for both tile shapes; 2 is kept for sweeps)
 // LDS ring depth: 3, except for the two launches with very few or gather-bound K steps, where the
 // 2-deep ring's smaller LDS footprint (more resident workgroups) wins (R34 bs 32, layer report):
 // the small-Cin stem (7x7, per-lane tap gather: 100 -> 75 us) and the 32-channel-tile head
