@@ -1342,14 +1342,15 @@ static bool conv_tc256_enabled() {
   return v;
 }
 // runtime tuning knobs (zp_conv_tuning): minimum workgroup count for the 256-channel tile
-static int g_tc256_min_blocks = 512;
+static int g_tc256_min_blocks = 1024;
 
 // cout tile: 256 (the whole layer: activations are staged once per pixel tile instead of once per
 // 128-channel tile, and 64 MFMAs per wave per LDS step instead of 32) for bf16 layers with
 // Cout % 256 == 0; else 128 / 64 / 32.
-// Measured (R34 bs 32, profiles/r01_conv_sweep.md): a win when the launch still has >= 512
+// Measured (R34 bs 32, profiles/r01_conv_sweep.md): a win when the launch still has >= 1024
 // workgroups of 256 pixels (64x64 / 128x128 layers, the 64x64 transposed-conv phases: 1.1-1.2x),
-// a loss on 32x32 layers (128 workgroups for 256 CUs) and on the ASPP launch, whose four
+// a loss on 32x32 layers (128 workgroups for 256 CUs), on the 32x32 transposed-conv phases (512
+// workgroups: 78.7 us vs 70.7 us on the 128-channel tile) and on the ASPP launch, whose four
 // sub-problems (1 vs 9 taps) are too unbalanced for 512 large tiles.
 static bool strip_eligible(const zp_conv_args& a, strip_geo* sg);
 // strip tile width: 128 channels, or 64 when 128-channel tiles would leave part of the 256 CUs
