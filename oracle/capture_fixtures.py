@@ -2,7 +2,7 @@
 
 Run in the build container (where /root/reference exists):
 
-    PYTHONDONTWRITEBYTECODE=1 python -B -m oracle.capture_fixtures
+    PYTHONDONTWRITEBYTECODE=1 python -B -m oracle.capture_fixtures [--only=fwd256,gt,add] [--r50] [--v3]
 
 It imports ``/root/reference/zebrapose`` read-only through a small import shim
 (SURVEY §8c): the reference's only missing imports are torchvision (its ResNet
@@ -189,10 +189,6 @@ def capture_network(variant=34):
         x = seeded((2, 3, 64, 64), 0)
         m, c = net(x)
         out["fwd64_x"], out["fwd64_mask"], out["fwd64_code"] = x.numpy(), m.numpy(), c.numpy()
-        if variant == 34:
-            x = seeded((1, 3, 256, 256), 2)
-            m, c = net(x)
-            np.savez(os.path.join(GOLDEN, "r34_fwd256_b1.npz"), x=x.numpy(), mask=m.numpy(), code=c.numpy())
     np.savez(os.path.join(GOLDEN, f"r{variant}_fwd64.npz"), **out)
     # the oracle must agree with the reference it restates
     sd2 = ref_cpu.synthetic_state(variant, 16, seed=0, bn_buffers=bnbuf)
@@ -376,14 +372,120 @@ def capture_v3():
     print("v3 train step: loss", float(loss), "loss_e", float(loss_e))
 
 
+def capture_fwd256():
+    """The bench geometry's parity anchor (configs[1]: 256x256 crops): the R34 net with the
+    synthetic weights, BN running stats calibrated on four 256x256 crops (so the logits sit in the
+    range a trained model's do, not the 64x64-calibrated fixture's 300), forward of two other
+    256x256 crops (model/BinaryCodeNet.py:161-174)."""
+    net = build_reference(34)
+    net.load_state_dict(ref_cpu.synthetic_state(34, 16, seed=0))
+    calibrate_bn(net, seeded((4, 3, 256, 256), 21))
+    bnbuf = canonical_bn_buffers(net, 34)
+    np.savez(os.path.join(GOLDEN, "r34_bn_buffers256.npz"), **bnbuf)
+    x = seeded((2, 3, 256, 256), 22)
+    with torch.no_grad():
+        m, c = net(x)
+    np.savez_compressed(os.path.join(GOLDEN, "r34_fwd256.npz"), x=x.numpy(), mask=m.numpy(), code=c.numpy())
+    sd2 = ref_cpu.synthetic_state(34, 16, seed=0, bn_buffers=bnbuf)
+    with torch.no_grad():
+        om, oc = ref_cpu.forward(sd2, x, 34)
+    print(f"r34 fwd256 (256-calibrated BN): |logit| max {np.abs(c.numpy()).max():.3g}; oracle vs reference: "
+          f"mask {np.abs(om.numpy() - m.numpy()).max():.3g} code {np.abs(oc.numpy() - c.numpy()).max():.3g}")
+
+
+def capture_gt_codes():
+    """GT code planes: the reference's RGB_image_to_class_id_image +
+    class_id_image_to_class_code_images (class_id_encoder_decoder.py:6-15, 43-63) on BGR GT crops
+    as bop_dataset_pytorch.py:311-312 calls them (base 2, 16 iterations, 65536 classes), then the
+    transform_pre permute to CHW (:345).  Random colours plus planted extremes (0, 255, ids above
+    2^16 whose high byte must be ignored)."""
+    from binary_code_helper.class_id_encoder_decoder import (RGB_image_to_class_id_image,
+                                                             class_id_image_to_class_code_images)
+    rng = np.random.default_rng(31)
+    gt = rng.integers(0, 256, (3, 128, 128, 3), dtype=np.uint8)
+    gt[1, :16] = 0
+    gt[1, 16:32] = 255
+    gt[2, :, :, 0] = rng.integers(1, 256, (128, 128), dtype=np.uint8)  # B != 0: id >= 2^16
+    codes = []
+    for b in range(gt.shape[0]):
+        cid = RGB_image_to_class_id_image(gt[b])
+        cc = class_id_image_to_class_code_images(cid, 2, 16, 65536)
+        codes.append(torch.from_numpy(cc).permute(2, 0, 1).numpy())
+    codes = np.stack(codes)
+    assert set(np.unique(codes)) <= {0.0, 1.0}
+    np.savez_compressed(os.path.join(GOLDEN, "gt_codes.npz"), gt_bgr=gt, code=codes.astype(np.uint8),
+                        code_dtype=np.array(str(codes.dtype)))
+    print("gt codes:", codes.shape, codes.dtype)
+
+
+def _import_pose_error():
+    """lib/pysixd/pose_error.py imports lib.utils.logger (needs termcolor, absent) and
+    lib.pysixd.misc / visibility (need cv2 and mmcv, absent).  add / adi use only numpy, scipy and
+    the module's own transform_pts_Rt, so those imports are stubbed with empty modules."""
+    tc = types.ModuleType("termcolor")
+    tc.colored = lambda s, *a, **k: s
+    sys.modules.setdefault("termcolor", tc)
+    import lib.pysixd as P
+    for n in ("misc", "visibility"):
+        if "lib.pysixd." + n not in sys.modules:
+            m = types.ModuleType("lib.pysixd." + n)
+            sys.modules["lib.pysixd." + n] = m
+            setattr(P, n, m)
+    from lib.pysixd import pose_error
+    return pose_error
+
+
+def _rot(rng):
+    q = rng.normal(size=4)
+    q /= np.linalg.norm(q)
+    w, x, y, z = q
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                     [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                     [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
+
+
+def capture_add_adi():
+    """ADD / ADI: the reference's lib/pysixd/pose_error.add / adi (:297-336)
+    on model points and pose pairs (identical, small and large errors, a symmetric flip)."""
+    pose_error = _import_pose_error()
+    rng = np.random.default_rng(41)
+    pts = rng.uniform(-60, 60, (2000, 3)).astype(np.float32)
+    n = 6
+    Rg = np.stack([_rot(rng) for _ in range(n)])
+    tg = rng.uniform(-50, 50, (n, 3)) + np.array([0, 0, 800])
+    Re = Rg.copy()
+    te = tg.copy()
+    Re[1] = Rg[1] @ _rot(np.random.default_rng(5)) * 1.0
+    te[2] = tg[2] + rng.normal(0, 5, 3)
+    Re[3] = Rg[3] @ np.diag([-1.0, -1.0, 1.0])  # 180 deg about z
+    Re[4] = _rot(rng)
+    te[4] = tg[4] + rng.normal(0, 40, 3)
+    te[5] = tg[5] + np.array([0, 0, 1e-3])
+    add = np.array([pose_error.add(Re[b], te[b].reshape(3, 1), Rg[b], tg[b].reshape(3, 1), pts) for b in range(n)])
+    adi = np.array([pose_error.adi(Re[b], te[b].reshape(3, 1), Rg[b], tg[b].reshape(3, 1), pts) for b in range(n)])
+    np.savez(os.path.join(GOLDEN, "add_adi.npz"), pts=pts, R_est=Re, t_est=te, R_gt=Rg, t_gt=tg, add=add, adi=adi)
+    print("add", add, "adi", adi)
+
+
 def main():
     os.makedirs(GOLDEN, exist_ok=True)
     install_shim()
     torch.manual_seed(0)
     torch.set_num_threads(8)
-    net, _ = capture_network(34)
-    capture_train_step(net)
-    capture_decode()
+    only = None
+    for a in sys.argv[1:]:
+        if a.startswith("--only="):
+            only = set(a[7:].split(","))
+    if only is None:
+        net, _ = capture_network(34)
+        capture_train_step(net)
+        capture_decode()
+    if only is None or "fwd256" in only:
+        capture_fwd256()
+    if only is None or "gt" in only:
+        capture_gt_codes()
+    if only is None or "add" in only:
+        capture_add_adi()
     if "--r50" in sys.argv:
         capture_network(50)
     if "--v3" in sys.argv:

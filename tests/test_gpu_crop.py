@@ -58,3 +58,18 @@ def test_crop_feeds_network_and_rejects_bad_input(gpu):
         cp(imgs.float(), [0], pad[:1])
     with pytest.raises(ValueError):
         cp(imgs, [5], pad[:1])
+
+
+def test_gt_code_planes_match_reference_fixture(gpu, golden):
+    """A15 pinned to the reference itself: zp_crop_gt's code planes on 128x128 BGR GT crops (same-size
+    ROI) equal RGB_image_to_class_id_image + class_id_image_to_class_code_images + the CHW permute of
+    bop_dataset_pytorch.py:311-312, 345 (tests/golden/gt_codes.npz, captured from the reference),
+    including colours whose id exceeds 2^16 (the blue byte is ignored by the 16-bit split)."""
+    from zebrapose_amd.crop import CropPipeline
+    f = golden("gt_codes.npz")
+    gt = torch.from_numpy(f["gt_bgr"]).cuda()
+    n = gt.shape[0]
+    img = torch.zeros((n, 128, 128, 3), dtype=torch.uint8, device="cuda")
+    cp = CropPipeline()
+    out = cp(img, np.arange(n), np.tile(np.array([[0, 0, 128, 128]], np.int32), (n, 1)), gt)
+    np.testing.assert_array_equal(out["code"].cpu().numpy(), f["code"])

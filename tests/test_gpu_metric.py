@@ -39,3 +39,14 @@ def test_add_adi_match_reference_formulas(gpu, n):
     # reference-signature drop-ins (metric.py:8-18)
     assert abs(Calculate_ADD_Error_BOP(Rg[1], tg[1], Re[1], te[1], pts) - add[1]) < 1e-12
     assert abs(Calculate_ADI_Error_BOP(Rg[1], tg[1], Re[1], te[1], pts) - adi[1]) < 1e-12
+
+
+def test_add_adi_match_reference_fixture(gpu, golden):
+    """ADD / ADI against the values the reference's own lib/pysixd/pose_error.add / adi returned
+    (tests/golden/add_adi.npz: identical pose, rotated, translated, 180-degree flip, random, 1 um)."""
+    from zebrapose_amd.metric import pose_errors, ADD, ADI
+    f = golden("add_adi.npz")
+    add = pose_errors(f["pts"], f["R_est"], f["t_est"], f["R_gt"], f["t_gt"], ADD).cpu().numpy()
+    adi = pose_errors(f["pts"], f["R_est"], f["t_est"], f["R_gt"], f["t_gt"], ADI).cpu().numpy()
+    np.testing.assert_allclose(add, f["add"], rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(adi, f["adi"], rtol=1e-9, atol=1e-12)

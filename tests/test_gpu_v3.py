@@ -53,23 +53,29 @@ def test_v3_forward_bf16_within_band(v3, golden):
         agree = ((got > THR) == (ref > THR))[np.abs(ref) > 0.25].mean()
         print(f"v3 bf16 {key}: rel-L2 {rel:.3g}, bits agree {agree:.4f} outside |ref| <= 0.25")
         # 256x256 with BN calibrated on two crops conditions worse than the 64x64 main-network
-        # fixture (rel-L2 0.16 there); the main network on r34_fwd256_b1 is printed for comparison
+        # fixture (rel-L2 0.16 there); test_main_network_bf16_at_256 below is the main-network analogue
         assert rel <= 0.5 and agree >= 0.85, (key, rel, agree)
 
 
-def test_main_network_bf16_at_256_for_comparison(golden):
+def test_main_network_bf16_at_256(golden):
+    """The main network in bf16 on the reference's 256x256 fixture (BN calibrated at 256x256):
+    in the conditioning band of this model (the bf16-emulating oracle sits at 18.6% rel-L2 from
+    fp32; tests/test_gpu_bench_geometry.py checks bf16 teacher-forced layer by layer)."""
     from oracle import ref_cpu
     from zebrapose_amd.model.BinaryCodeNet import BinaryCodeNet_Deeplab
-    f = golden("r34_fwd256_b1.npz")
+    f = golden("r34_fwd256.npz")
     net = BinaryCodeNet_Deeplab(34, 16, 2, concat=True, output_kernel_size=1, precision="bf16")
-    net.load_state_dict(ref_cpu.synthetic_state(34, 16, 0, dict(golden("r34_bn_buffers.npz"))))
+    net.load_state_dict(ref_cpu.synthetic_state(34, 16, 0, dict(golden("r34_bn_buffers256.npz"))))
     net = net.cuda().eval()
     with torch.no_grad():
         m, c = net(torch.from_numpy(f["x"]).cuda())
     for got, key in ((m, "mask"), (c, "code")):
         ref = f[key]
-        rel = np.linalg.norm(got.cpu().numpy() - ref) / np.linalg.norm(ref)
-        print(f"main bf16 @256 {key}: rel-L2 {rel:.3g}")
+        got = got.cpu().numpy()
+        rel = np.linalg.norm(got - ref) / np.linalg.norm(ref)
+        agree = ((got > THR) == (ref > THR))[np.abs(ref) > 0.25].mean()
+        print(f"main bf16 @256 {key}: rel-L2 {rel:.3g}, bits agree {agree:.4f} outside |ref| <= 0.25")
+        assert rel <= 0.35 and agree >= 0.90, (key, rel, agree)
 
 
 def test_v3_rejects_other_input_sizes(v3):

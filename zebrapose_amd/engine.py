@@ -104,6 +104,10 @@ class Engine:
         self._folds = {}
         self._fold_epoch = 0
         self.timing = None  # optional list of (label, start_event, end_event) for conv launches
+        # optional list: every eval-mode op appends (kind, unit, x, out, res) with the buffers it
+        # read and wrote (kept alive by the list) -- the teacher-forced layer parity tests replay
+        # each op on the host from the device's own stored inputs (tests/test_gpu_bench_geometry.py)
+        self.trace = None
 
     # ------------------------------------------------------------------ weight / BN caches
     def invalidate(self):
@@ -267,6 +271,8 @@ class Engine:
             scale, shift = self._fold(unit)
             outs = [(out.ptr, out.ld, out.c0, OH, OW, scale, shift, None)] * len(plan.subs)
             self._conv(x, plan, unit.cout, ws, kp, rows, outs, res, unit.relu, small=small, label=label)
+            if self.trace is not None and not train:
+                self.trace.append(("conv", unit, x, out, res))
             if train:
                 tape.recs.append(("plain", unit, x, out, res, None, None))
             return
@@ -313,6 +319,9 @@ class Engine:
             scale, shift = self._fold(u)
             outs.append((o.ptr, o.ld, o.c0, o.H, o.W, scale, shift, None))
         self._conv(x, merged, 256, ws, kp, rows, outs, None, True, label="aspp")
+        if self.trace is not None:
+            for u, o in zip(units, outs_act):
+                self.trace.append(("conv", u, x, o, None))
 
     def head_fwd(self, unit, x: Act, mask, code, tape, key="head"):
         """Head conv writing f32 NCHW channel 0 -> mask, channels 1.. -> code (code None when the
@@ -325,6 +334,8 @@ class Engine:
                    small=self._small(unit.cin, unit.k, unit.d, unit.p), label="head")
         if tape is not None:
             tape.recs.append(("head", unit, x, key, None, None, None))
+        elif self.trace is not None:
+            self.trace.append(("head", unit, x, (mask, code), None))
 
     # ------------------------------------------------------------------ backward pieces
     def _grad_buf(self, gmap, act: Act):
@@ -503,6 +514,8 @@ class Engine:
         st = L.stream_ptr()
         xin = new(H, W, 8)
         L.call("zp_nchw_to_nhwc", x.data_ptr(), B, 3, H, W, 8, self.dt, xin.ptr, st)
+        if self.trace is not None and tape is None:
+            self.trace.append(("input", None, x, xin, None))
         r = rn.resnet
         H2, W2 = H // 2, W // 2
         H4, W4, H8, W8 = H // 4, W // 4, H // 8, W // 8
@@ -514,6 +527,8 @@ class Engine:
         L.call("zp_maxpool3s2", x128.ptr, B, H2, W2, x128.ld, x128.c0, 64, self.dt, pooled.ptr, H4, W4, 64, 0, st)
         if tape is not None:
             tape.recs.append(("maxpool", x128, pooled))
+        elif self.trace is not None:
+            self.trace.append(("maxpool", None, x128, pooled, None))
         up2_in = torch.empty((B, H4, W4, 256 + c64), dtype=dt, device=dev)
         x64 = Act(up2_in, 256, c64)
         h = self._layer(r[4], pooled, x64, tape)
@@ -529,11 +544,15 @@ class Engine:
         L.call("zp_global_avgpool", xh.ptr, B, H8, W8, xh.ld, xh.c0, xh.C, self.dt, pool.ptr, st)
         if tape is not None:  # tape order = forward order (the backward walks it reversed)
             tape.recs.append(("avgpool", xh, pool))
+        elif self.trace is not None:
+            self.trace.append(("avgpool", None, xh, pool, None))
         imgo = Act(torch.empty((B, 1, 1, 256), dtype=dt, device=dev))
         self.unit_fwd(self._u(aspp.conv_1x1_2, aspp.bn_conv_1x1_2), pool, imgo, tape, label="aspp_pool")
         L.call("zp_broadcast_hw", imgo.ptr, B, 256, self.dt, A.data_ptr(), H8, W8, 1280, 1024, st)
         if tape is not None:
             tape.recs.append(("broadcast", imgo, Act(A, 1024, 256)))
+        elif self.trace is not None:
+            self.trace.append(("broadcast", None, imgo, Act(A, 1024, 256), None))
         o = new(H8, W8, 256)
         self.unit_fwd(self._u(aspp.conv_1x1_3, aspp.bn_conv_1x1_3), Act(A), o, tape, label="aspp_proj")
         # ---- decoder (aspp.py:101-112)
