@@ -16,6 +16,13 @@ Also the configs[4] leg (rank 0, N = 1): R50 fp16 batched multi-object inference
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--no-train] [--no-cpu] [--no-multi]
     torchrun --nproc-per-node N bench.py --gpus N ...
+
+``--gpus N`` (N > 1) without a torchrun environment launches the N ranks itself (one process per
+GPU, torch.multiprocessing spawn, as train_v6.py:465-468 does with mp.spawn); the parent process
+never touches the GPU.  Each rank joins the process group (RCCL for the GPU run); ``n_gpus`` is
+the size of the group that actually formed.  ``--dry-run`` swaps the network for a CPU stub and
+RCCL for gloo: it exercises exactly this launcher / rendezvous / timing path on a host without a
+GPU (tests/test_bench_launcher.py).
 """
 from __future__ import annotations
 
@@ -39,7 +46,7 @@ FWD_GFLOP_PER_CROP = 109.136  # 2 x 54,568,026,112 MAC per 256
 R50_GFLOP_PER_CROP = 747.68  # ResNet50_OS8 + ASPP_50 forward per crop
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -50,12 +57,14 @@ def parse():
     ap.add_argument("--no-train", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--train-steps", type=int, default=None)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=60.0, help="bound on each CPU-baseline timing loop")
     ap.add_argument("--layer-report", default=None, help="write per-launch conv timings (JSON) here")
     ap.add_argument("--no-multi", action="store_true", help="skip the configs[4] multi-object leg")
     ap.add_argument("--mo-objects", type=int, default=30)
     ap.add_argument("--mo-crops", type=int, default=8, help="crops per object per step (configs[4] leg)")
-    return ap.parse_args()
+    ap.add_argument("--no-fp32", action="store_true", help="skip the fp32-mode inference line")
+    ap.add_argument("--dry-run", action="store_true", help="CPU stub workload over gloo (launcher test)")
+    return ap.parse_args(argv)
 
 
 def calibrate_bn(net, x):
@@ -115,6 +124,124 @@ def _device_init_(net, seed):
                 m.num_batches_tracked.zero_()
 
 
+def _cpu_model():
+    try:
+        import subprocess
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                return line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(args, net, x, bboxes):
+    """SURVEY §8(d) / BASELINE.md CPU-baseline protocol: the oracle (oracle/ref_cpu.py: the reference's
+    op sequence on the torch CPU backend, fp32; decode in the reference's own per-pixel-loop form,
+    CNN_output_to_pose.py:53-64) on the host cores, 2 warm-ups then the median of 10 timed iterations,
+    at bs=1 and bs=32, forward / decode / end-to-end.  Threads: torch's default, i.e. OMP_NUM_THREADS
+    when set -- on the GPU box that is 16, the CPU share one GPU's job is given there (the machine
+    shows more CPUs, reported as host_cpus, but belongs to 8 GPUs' jobs)."""
+    from oracle import ref_cpu
+    threads = torch.get_num_threads()
+    sd = {k: v.detach().cpu() for k, v in net.state_dict().items()}
+    lut = synthetic_lut()
+    ld = ref_cpu.lut_dict(lut)
+    res = {}
+    t_all = time.perf_counter()
+    with torch.no_grad():
+        for bs in (1, x.shape[0]):
+            xb = x[:bs].cpu()
+            fw = []
+            n_it = 10
+            it = 0
+            while it < 2 + n_it:
+                t0 = time.perf_counter()
+                m, c = ref_cpu.forward(sd, xb, 34)
+                dtf = time.perf_counter() - t0
+                if it >= 2:
+                    fw.append(dtf)
+                elif it == 1 and dtf * n_it > args.cpu_seconds:  # bound the sample (reported below)
+                    n_it = max(3, int(args.cpu_seconds / dtf))
+                it += 1
+            dec = []
+            for b in range(bs):
+                t0 = time.perf_counter()
+                ref_cpu.decode_crop_loop(m[b, 0].numpy(), c[b].numpy(), ld, bboxes[b])
+                dec.append(time.perf_counter() - t0)
+            f_med = float(np.median(fw))
+            d_crop = float(np.median(dec))
+            res[f"bs{bs}"] = {"forward_ms": round(f_med * 1e3, 1), "forward_crops_per_s": round(bs / f_med, 3),
+                              "decode_ms_per_crop": round(d_crop * 1e3, 2), "e2e_crops_per_s":
+                              round(bs / (f_med + sum(dec)), 3), "timed_forward_iterations": len(fw)}
+    total = time.perf_counter() - t_all
+    big = res[f"bs{x.shape[0]}"]
+    return {"value": big["e2e_crops_per_s"], "unit": "crops/s", "cores": threads, "kind": "port",
+            "host_cpus": os.cpu_count(), "cpu_model": _cpu_model(), **res,
+            "sample": f"oracle/ref_cpu.py forward (torch CPU fp32, {threads} threads) + the reference-form per-pixel "
+                      f"decode loop, 256x256 synthetic crops; 2 warm-ups then the median of the timed iterations "
+                      f"at bs=1 and bs={x.shape[0]}; value = bs={x.shape[0]} end-to-end; {total:.0f} s of CPU work"}
+
+
+def train_breakdown(ts, tnet, x, gt_code, gt_mask, world, rank, steps=3):
+    """Per-step timeline of the train step from HIP events on the compute stream: forward + loss,
+    backward (engine reverse pass; at N > 1 up to the moment the current stream has waited for every
+    gradient bucket's RCCL all-reduce), optimizer.  At N > 1 also: when each bucket's all-reduce
+    was enqueued relative to the backward start, the exposed communication (last bucket enqueued ->
+    all buckets complete), and the same buckets all-reduced standalone (no overlapping compute).
+    Per-rank bucket order goes to stderr (BASELINE.md configs[3]: all-reduce time vs backward)."""
+    rows = []
+    ts.events = []
+    if ts.buckets is not None:
+        ts.buckets.timing = []
+    for _ in range(steps):
+        ts.events.clear()
+        if ts.buckets is not None:
+            ts.buckets.timing.clear()
+        ts(x, gt_code, gt_mask)
+        torch.cuda.synchronize()
+        ev = dict(ts.events)
+        r = {"fwd_loss_ms": ev["start"].elapsed_time(ev["backward"]),
+             "backward_ms": ev["backward"].elapsed_time(ev["optimizer"]),
+             "optimizer_ms": ev["optimizer"].elapsed_time(ev["end"])}
+        if ts.buckets is not None:
+            tl = ts.buckets.timing
+            launches = [(b, e) for b, e in tl if b != "done"]
+            done = [e for b, e in tl if b == "done"][0]
+            r["bucket_enqueue_ms"] = [round(ev["backward"].elapsed_time(e), 3) for _, e in launches]
+            r["exposed_comm_ms"] = launches[-1][1].elapsed_time(done)
+        rows.append(r)
+    ts.events = None
+    med = {k: round(float(np.median([r[k] for r in rows])), 3) for k in rows[0] if not isinstance(rows[0][k], list)}
+    out = dict(med, steps=steps)
+    if ts.buckets is not None:
+        out["bucket_enqueue_ms"] = rows[-1]["bucket_enqueue_ms"]
+        ts.buckets.timing = None
+        names = {p: n for n, p in tnet.named_parameters()}
+        layout = ts.buckets.describe(names)
+        flats = [bk[0] for bk in ts.buckets.buckets]
+        nbytes = sum(f.numel() * f.element_size() for f in flats)
+        times = []
+        for _ in range(5):
+            dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for f in flats:
+                dist.all_reduce(f, op=dist.ReduceOp.SUM)
+            torch.cuda.synchronize()
+            times.append(time.perf_counter() - t0)
+        ar = float(np.median(times))
+        out.update(buckets=len(flats), bucket_mb=[b[1] for b in layout], grad_mb=round(nbytes / 2 ** 20, 2),
+                   allreduce_ms_standalone=round(ar * 1e3, 3),
+                   allreduce_busbw_GBps=round(2 * (world - 1) / world * nbytes / ar / 1e9, 1))
+        print(f"[rank {rank}] grad buckets (launch order): " + "; ".join(
+            f"#{b} {mb} MB {n} params {first}..{last}" for b, mb, n, first, last in layout)
+            + f" | enqueue ms into backward {out['bucket_enqueue_ms']} | exposed comm {out['exposed_comm_ms']} ms",
+            file=sys.stderr, flush=True)
+    return out
+
+
 def multi_object_leg(args, dev):
     """configs[4]: ResNet50 + ASPP_50, fp16 MFMA, batched multi-object inference (T-LESS-style 30
     objects, one weight set + LUT each) with the code->vertex decode and PnP on the device
@@ -157,15 +284,84 @@ def multi_object_leg(args, dev):
     return res
 
 
+# ---------------------------------------------------------------------------------- launcher
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def _rank_main(local_rank, args, port):
+    """One spawned rank: the torchrun environment, then the normal single-rank body."""
+    os.environ.update(RANK=str(local_rank), LOCAL_RANK=str(local_rank), WORLD_SIZE=str(args.gpus),
+                      LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    run(args)
+
+
+def launch(args):
+    """``bench.py --gpus N`` without torchrun: spawn N ranks (train_v6.py:465-468 mp.spawn).  The
+    parent only counts devices (no GPU initialisation on this image) and never runs GPU work."""
+    import torch.multiprocessing as mp
+    if not args.dry_run:
+        n = torch.cuda.device_count()
+        if n < args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but only {n} GPU(s) are visible")
+    mp.start_processes(_rank_main, args=(args, _free_port()), nprocs=args.gpus, join=True, start_method="spawn")
+
+
+def dry_run(args, world, rank):
+    """The launcher / rendezvous / barrier / max-over-ranks path with a CPU stub step (gloo)."""
+    torch.manual_seed(rank)
+    a = torch.randn(256, 256)
+    for _ in range(args.warmup):
+        a = torch.tanh(a @ a) * 0.5
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        a = torch.tanh(a @ a) * 0.5
+    el = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = t.item()
+    if rank == 0:
+        print(json.dumps({"metric": "dry-run stub steps/s", "value": round(world * args.steps / el, 2),
+                          "unit": "steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
+                          "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+                          "data": "dry-run: CPU stub step over gloo, no GPU work",
+                          "config": {"workload": "launcher dry run", "parallelism": f"replicas{world}",
+                                     "backend": dist.get_backend() if world > 1 else "none"}}), flush=True)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        launch(args)
+        return
+    run(args)
+
+
+def run(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        if world > 1:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+            world = dist.get_world_size()
+        dry_run(args, world, rank)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        world = dist.get_world_size()  # the ranks that actually joined the RCCL group
 
     from zebrapose_amd.model.BinaryCodeNet import BinaryCodeNet_Deeplab
     from zebrapose_amd.decode import Decoder
@@ -252,6 +448,31 @@ def main():
                 "all_conv_tflops": round(all_conv_flops / all_conv_time / 1e12, 2),
                 "whole_step_tflops": round(FWD_GFLOP_PER_CROP * 1e9 * B / (ms_per_step * 1e-3) / 1e12, 2)}
 
+    # ------------------------------------------------------------------ fp32 mode at the same config
+    # (the reference's own precision; f32 MFMA v_mfma_f32_16x16x4_f32, 157.3 TFLOP/s dense peak)
+    fp32 = None
+    if not args.no_fp32 and args.precision != "fp32":
+        net.set_precision("fp32")
+        for _ in range(2):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        K2 = max(3, args.steps // 2)
+        t0 = time.perf_counter()
+        for _ in range(K2):
+            step()
+        torch.cuda.synchronize()
+        el2 = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el2], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el2 = t.item()
+        tfl = FWD_GFLOP_PER_CROP * 1e9 * B * K2 / el2 / 1e12
+        fp32 = {"crops_per_s": round(world * B * K2 / el2, 2), "ms_per_step": round(el2 / K2 * 1e3, 3), "steps": K2,
+                "dtype": "f32", "whole_step_tflops": round(tfl, 2), "frac_of_f32_peak": round(tfl / PEAK["fp32"], 4)}
+        net.set_precision(args.precision)
+
     # ------------------------------------------------------------------ on-device PnP (extra, §8f rank 1)
     # RANSAC-EPnP (150 iterations, 2 px) over the last step's decoded correspondences; the random
     # network gives random correspondences, i.e. the worst case (no early RANSAC termination)
@@ -326,6 +547,7 @@ def main():
                  "steps": K, "global_batch": world * B, "loss": round(float(loss[0].item()), 5),
                  "achieved_tflops": round(3 * FWD_GFLOP_PER_CROP * 1e9 * world * B * K / tel / 1e12 / world, 2),
                  "parallelism": f"ddp{world}" if world > 1 else "single"}
+        train["breakdown"] = train_breakdown(ts, tnet, x, gt_code, gt_mask, world, rank)
         del ts, tnet
 
     # ------------------------------------------------------------------ 3-head v3 network (extra, §8f rank 3)
@@ -372,27 +594,7 @@ def main():
     # ------------------------------------------------------------------ CPU baseline (rank 0, N = 1)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        from oracle import ref_cpu
-        threads = min(16, os.cpu_count() or 1)
-        torch.set_num_threads(threads)
-        sd = {k: v.detach().cpu() for k, v in net.state_dict().items()}
-        xb = x[:2].cpu()
-        lut = synthetic_lut()
-        with torch.no_grad():
-            ref_cpu.forward(sd, xb, 34)
-            n = 0
-            t0 = time.perf_counter()
-            while True:
-                m, c = ref_cpu.forward(sd, xb, 34)
-                for b in range(xb.shape[0]):
-                    ref_cpu.decode_crop(m[b, 0].numpy(), c[b].numpy(), lut, bboxes[b])
-                n += xb.shape[0]
-                if time.perf_counter() - t0 > args.cpu_seconds:
-                    break
-            cel = time.perf_counter() - t0
-        cpu = {"value": round(n / cel, 3), "unit": "crops/s", "cores": threads, "kind": "port",
-               "sample": f"{n} crops (batches of 2, 256x256) through oracle/ref_cpu.py forward (torch CPU fp32) + "
-                         f"numpy decode, {cel:.1f} s on {threads} threads"}
+        cpu = cpu_baseline(args, net, x, bboxes)
 
     if rank == 0:
         line = {"metric": "256x256 crops/sec (R34 DeepLabv3 inference bs=32, forward + code->vertex decode)",
@@ -404,7 +606,7 @@ def main():
                            "model": "BinaryCodeNet_Deeplab(34, 16, 2, concat=True)", "global_batch": world * B,
                            "per_gpu_batch": B, "input": f"{S}x{S}", "parallelism": f"replicas{world}",
                            "correspondences_last_step": n_corr},
-                "roofline": roofline, "cpu_baseline": cpu, "train": train, "pnp": pnp_res, "crop": crop_res, "v3": v3,
+                "roofline": roofline, "fp32": fp32, "cpu_baseline": cpu, "train": train, "pnp": pnp_res, "crop": crop_res, "v3": v3,
                 "multi_object": multi}
         print(json.dumps(line), flush=True)
     if world > 1:

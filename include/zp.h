@@ -111,7 +111,7 @@ int zp_conv2d_stat_parts(const zp_conv_args* a);
  * (0 = k_conv, 1 = k_conv_strip: 3x3 stride-1 convs with activation-strip reuse) */
 int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* stages, int* variant);
 /* runtime tuning knob (tests / sweeps): key 0 = minimum workgroup count for the 256-channel
- * tile (default 512).  Returns the previous value, -1 for an unknown key. */
+ * tile (default 1024).  Returns the previous value, -1 for an unknown key. */
 int zp_conv_tuning(int key, int value);
 
 /* Pack an f32 weight tensor src[d0][d1][kh][kw] into dst[rows_pad][k_pad] (dtype), taps

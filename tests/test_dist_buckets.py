@@ -94,8 +94,10 @@ def test_grad_buckets_gloo_cpu():
                 torch.testing.assert_close(torch.tensor(got), w, rtol=1e-5, atol=1e-6)
 
 
-def _gpu_worker(rank, world, port, q):
+def _gpu_worker(rank, world, port, q, mode="buckets"):
     _env(rank, world, port)
+    if mode == "torch_ddp":  # torch's DistributedDataParallel(net) over the libzp network
+        os.environ["ZP_TORCH_DDP"] = "1"
     torch.cuda.set_device(0)
     from zebrapose_amd import parallel as P
     from zebrapose_amd.model.BinaryCodeNet import BinaryCodeNet_Deeplab
@@ -120,13 +122,16 @@ def _gpu_worker(rank, world, port, q):
         local = {n: params[n].grad.detach().double().cpu() for n in names}
         norm_local = sum(float(p.grad.double().pow(2).sum()) for p in net.parameters())
         # data-parallel step: the same forward / backward with the buckets attached
-        ts = TrainStep(net, ddp=True, learning_rate=0.0)
+        ts = TrainStep(net, ddp=True, learning_rate=0.0, device=0)
         ts.optimizer.step = lambda: None
-        assert ts.buckets is not None and ts.net is net
+        if mode == "torch_ddp":
+            assert ts.buckets is None and isinstance(ts.net, torch.nn.parallel.DistributedDataParallel)
+        else:
+            assert ts.buckets is not None and ts.net is net
         ts(x, gt, gm)
         torch.cuda.synchronize()
         avg = {n: params[n].grad.detach().double().cpu() for n in names}
-        nb = len(ts.buckets.buckets)
+        nb = len(ts.buckets.buckets) if ts.buckets is not None else None
         q.put((rank, nb, {n: local[n].tolist() for n in names}, {n: avg[n].tolist() for n in names}, norm_local))
     finally:
         if dist.is_initialized():
@@ -134,12 +139,15 @@ def _gpu_worker(rank, world, port, q):
 
 
 @pytest.mark.gpu
-def test_grad_buckets_engine_two_ranks(gpu):
+@pytest.mark.parametrize("mode", ["buckets", "torch_ddp"])
+def test_grad_buckets_engine_two_ranks(gpu, mode):
+    """Both data-parallel paths over the libzp network: GradBuckets (default) and torch's own
+    DistributedDataParallel(net) (ZP_TORCH_DDP=1, the wrapper train_v6.py:259 uses)."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_gpu_worker, args=(r, world, port, q)) for r in range(world)]
+    ps = [ctx.Process(target=_gpu_worker, args=(r, world, port, q, mode)) for r in range(world)]
     for p in ps:
         p.start()
     try:
@@ -149,7 +157,8 @@ def test_grad_buckets_engine_two_ranks(gpu):
             p.join(timeout=60)
     for p in ps:
         assert p.exitcode == 0
-    assert res[0][1] >= 4  # 116 MB of f32 gradients in ~25 MB buckets
+    if mode == "buckets":
+        assert res[0][1] >= 4  # 116 MB of f32 gradients in ~25 MB buckets
     for n in res[0][2]:
         want = (torch.tensor(res[0][2][n]) / 2 + torch.tensor(res[1][2][n]) / 2)
         scale = want.abs().max().item() + 1e-12

@@ -334,3 +334,49 @@ def test_binary_code_helper_dropins(golden):
             p2d, p3d = decode_correspondences(mask, code, d["bboxes"][b], 128, dd)
             np.testing.assert_array_equal(p2d, d[f"ib{ib}_b{b}_p2d"])
             np.testing.assert_array_equal(p3d, d[f"ib{ib}_b{b}_p3d"])
+
+
+def test_decoder_cache_tracks_dict_identity_and_content():
+    """CNN_output_to_pose's LUT cache: a new dict (even if it reused a collected dict's id) or an edited
+    entry must not decode with a stale LUT; the cache stays bounded."""
+    from zebrapose_amd.binary_code_helper import CNN_output_to_pose as C
+    mask = np.ones((4, 4), np.uint8)
+    code = np.zeros((4, 4, 16))  # every pixel -> class id 0
+    bb = np.array([0, 0, 128, 128])
+
+    def mk(v):
+        return {float(i): np.array([v, v, v], np.float64) for i in range(65536)}
+    d1 = mk(1.0)
+    _, p3 = C.decode_correspondences(mask, code, bb, 128, d1)
+    assert np.all(p3 == 1.0)
+    d1[0.0] = np.array([5.0, 5.0, 5.0])  # edit in place: the sampled fingerprint sees id 0
+    _, p3 = C.decode_correspondences(mask, code, bb, 128, d1)
+    assert np.all(p3 == 5.0)
+    for k in range(40):  # many dicts: new ids, some recycled; never stale, cache bounded
+        d = mk(float(k))
+        _, p3 = C.decode_correspondences(mask, code, bb, 128, d)
+        assert np.all(p3 == float(k))
+        del d
+    assert len(C._DEC_CACHE) <= C._DEC_CACHE_MAX
+
+
+def test_fused_adam_multi_with_empty_tensors_inside_a_chunk():
+    """zp_adam_multi packs up to 40 non-empty tensors per launch; empty tensors inside a chunk of 41+
+    tensors must not make the next launch revisit (and double-update) a tensor."""
+    from zebrapose_amd.optim import FusedAdam
+    torch.manual_seed(3)
+    sizes = [5, 0, 33, 0, 0, 7] * 9 + [11, 0, 2]
+    ref = [torch.randn(n, dtype=torch.float32, requires_grad=True) for n in sizes]
+    dev = [r.detach().clone().cuda().requires_grad_(True) for r in ref]
+    o_ref = torch.optim.Adam(ref, lr=1e-2)
+    o = FusedAdam(dev, lr=1e-2)
+    for s in range(2):
+        for r, d in zip(ref, dev):
+            g = torch.randn(r.shape)
+            r.grad = g.clone()
+            d.grad = g.cuda()
+        o_ref.step()
+        o.step()
+    torch.cuda.synchronize()
+    for r, d in zip(ref, dev):
+        np.testing.assert_allclose(d.detach().cpu().numpy(), r.detach().numpy(), rtol=1e-6, atol=1e-8)

@@ -184,3 +184,15 @@ def test_v3_state_spec_and_forward_match_reference(golden):
     np.testing.assert_array_equal(m.numpy(), f["mask"])
     np.testing.assert_array_equal(e.numpy(), f["entire"])
     np.testing.assert_array_equal(c.numpy(), f["code"])
+
+
+def test_decode_loop_form_equals_vectorised(golden):
+    """The CPU baseline's loop-form decode (the reference's per-pixel loop) gives the same outputs
+    as the vectorised oracle and the reference fixture."""
+    d = golden("decode.npz")
+    ld = ref_cpu.lut_dict(d["lut"])
+    for b in range(d["mask_logits"].shape[0]):
+        n, p2d, p3d = ref_cpu.decode_crop_loop(d["mask_logits"][b, 0], d["code_logits"][b], ld, d["bboxes"][b])
+        assert n == int(d[f"ib0_b{b}_count"])
+        assert np.array_equal(p2d, d[f"ib0_b{b}_p2d"])
+        assert np.array_equal(p3d, d[f"ib0_b{b}_p3d"])

@@ -11,6 +11,8 @@ the reference.
 """
 from __future__ import annotations
 
+from collections import OrderedDict
+
 import numpy as np
 import torch
 
@@ -38,14 +40,35 @@ def _lut_from_dict(dict_class_id_3D_points):
     return np.stack([np.asarray(dict_class_id_3D_points[float(i)], dtype=np.float64).reshape(3) for i in range(n)])
 
 
-_DEC_CACHE = {}
+_DEC_CACHE = OrderedDict()  # id(dict) -> (the dict itself, fingerprint, Decoder); LRU, bounded
+_DEC_CACHE_MAX = 32
+_FP_IDS = (0.0, 1.0, 255.0, 4097.0, 32768.0, 65535.0)
+
+
+def _fingerprint(d):
+    """Cheap change detector: size plus a few sampled entries (a rebuilt LUT from the reference's
+    dict costs ~65K lookups, too slow to repeat per crop at test.py's bs=1)."""
+    vals = []
+    for k in _FP_IDS:
+        v = d.get(k)
+        vals.append(None if v is None else np.asarray(v, dtype=np.float64).reshape(-1).tobytes())
+    return len(d), tuple(vals)
 
 
 def _decoder_for(dict_class_id_3D_points, device):
+    """The cache entry keeps a strong reference to the dict, so its id() cannot be recycled by
+    another object while cached; a changed size / sampled entry rebuilds the LUT."""
     key = (id(dict_class_id_3D_points), str(device))
-    dec = _DEC_CACHE.get(key)
-    if dec is None:
-        dec = _DEC_CACHE[key] = Decoder(_lut_from_dict(dict_class_id_3D_points), device=device)
+    fp = _fingerprint(dict_class_id_3D_points)
+    hit = _DEC_CACHE.get(key)
+    if hit is not None and hit[0] is dict_class_id_3D_points and hit[1] == fp:
+        _DEC_CACHE.move_to_end(key)
+        return hit[2]
+    dec = Decoder(_lut_from_dict(dict_class_id_3D_points), device=device)
+    _DEC_CACHE[key] = (dict_class_id_3D_points, fp, dec)
+    _DEC_CACHE.move_to_end(key)
+    while len(_DEC_CACHE) > _DEC_CACHE_MAX:
+        _DEC_CACHE.popitem(last=False)
     return dec
 
 

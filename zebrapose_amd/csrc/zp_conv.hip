@@ -1467,6 +1467,8 @@ static int conv_stages(const zp_conv_args& a, int tc) {
   return 3;
 }
 
+extern "C" int zp_conv2d_stat_parts(const zp_conv_args* a);
+
 extern "C" int zp_conv2d_grid(const zp_conv_args* a) {
   if (!a) return 0;
   long M = (long)a->N * a->GH * a->GW;
@@ -1543,6 +1545,11 @@ extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
     sg.w_bytes = tg.w_bytes[0];
     const int sgx = (int)(((long)a.N * a.GH * a.GW) / 256);
     const dim3 grid(sgx, gy, 1);
+    // train-mode statistics: the caller sized the partials buffer with zp_conv2d_stat_parts; the
+    // launch must emit exactly that many parts (NWP = 4 wave-halves per 256-pixel tile)
+    ZP_CHECK_ARG(!a.stats || 4 * sgx == zp_conv2d_stat_parts(&a),
+                 "zp_conv2d: strip launch emits %d stat parts, zp_conv2d_stat_parts says %d", 4 * sgx,
+                 zp_conv2d_stat_parts(&a));
     if (a.dtype == ZP_F16) {
       if (tc == 64) hipLaunchKernelGGL((k_conv_strip<f16_t, 2, 3, 5>), grid, dim3(512), 0, st, a, sg, conv_flags());
       else hipLaunchKernelGGL((k_conv_strip<f16_t, 4, 3, 5>), grid, dim3(512), 0, st, a, sg, conv_flags());
@@ -1555,6 +1562,12 @@ extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
   }
   const int nwp = conv_tp(a) / 64;
   const int stages = conv_stages(a, tc);
+  {
+    const int launched_nwp = tc == 256 ? 4 : nwp;  // launch_conv_tc256 is always the 256-pixel tile
+    ZP_CHECK_ARG(!a.stats || launched_nwp * gx * a.nsub == zp_conv2d_stat_parts(&a),
+                 "zp_conv2d: launch emits %d stat parts, zp_conv2d_stat_parts says %d", launched_nwp * gx * a.nsub,
+                 zp_conv2d_stat_parts(&a));
+  }
 #define ZP_DISPATCH_ST(T, WC, NWP, ST)                                   \
   if (smallc) launch_conv<T, WC, NWP, ST, true>(a, tg, gx, gy, st);      \
   else launch_conv<T, WC, NWP, ST, false>(a, tg, gx, gy, st);
@@ -1731,7 +1744,7 @@ extern "C" int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* st
 }
 
 /* runtime tuning knobs (tests / sweeps).  key 0: minimum workgroups for the 256-channel conv tile
- * (default 512).  Returns the previous value. */
+ * (default 1024).  Returns the previous value. */
 extern "C" int zp_conv_tuning(int key, int value) {
   if (key == 0) {
     const int old = g_tc256_min_blocks;

@@ -1276,12 +1276,15 @@ extern "C" int zp_adam_multi(int count, float* const* params, const float* const
                "zp_adam_multi: bad args");
   const double bc1 = 1.0 - pow(beta1, (double)step);
   const double bc2 = 1.0 - pow(beta2, (double)step);
-  for (int t0 = 0; t0 < count; t0 += ADAM_MT) {
+  // each launch takes up to ADAM_MT non-empty tensors; the next launch starts where this one's scan
+  // stopped (empty tensors are skipped, never counted twice)
+  for (int t0 = 0; t0 < count;) {
     AdamTable T{};
     int nb = 0;
     T.count = 0;
-    for (int t = t0; t < count && T.count < ADAM_MT; ++t) {
-      ZP_CHECK_ARG(params[t] && grads[t] && exp_avg[t] && exp_avg_sq[t] && numel[t] >= 0,
+    int t = t0;
+    for (; t < count && T.count < ADAM_MT; ++t) {
+      ZP_CHECK_ARG(numel[t] >= 0 && (numel[t] == 0 || (params[t] && grads[t] && exp_avg[t] && exp_avg_sq[t])),
                    "zp_adam_multi: tensor %d", t);
       if (numel[t] == 0) continue;
       const int k = T.count++;
@@ -1295,6 +1298,7 @@ extern "C" int zp_adam_multi(int count, float* const* params, const float* const
       ZP_CHECK_ARG(nb + blocks < (1ll << 30), "zp_adam_multi: too many elements");
       nb += (int)blocks;
     }
+    t0 = t;
     T.blk0[T.count] = nb;
     if (nb == 0) continue;
     hipLaunchKernelGGL(k_adam_multi, dim3(nb), dim3(256), 0, (hipStream_t)stream, T, (float)(lr / bc1),

@@ -109,7 +109,16 @@ class GradBuckets:
                 cur, size = [], 0
         if cur:
             self._add_bucket(cur)
+        # optional per-step timeline (bench.py's DDP leg): (bucket, event recorded on the current
+        # stream when the bucket's all-reduce is enqueued); finish() appends ("done", event)
+        self.timing = None
         self._reset()
+
+    def describe(self, names=None):
+        """Bucket layout in launch order: [(bucket, MB, n params, first / last parameter name)]."""
+        names = names or {}
+        return [(b, round(bk[0].numel() * bk[0].element_size() / 2 ** 20, 2), len(bk[1]),
+                 names.get(bk[1][0], "?"), names.get(bk[1][-1], "?")) for b, bk in enumerate(self.buckets)]
 
     def _pg(self):
         return self.group if self.group is not None else dist.distributed_c10d._get_default_group()
@@ -141,6 +150,10 @@ class GradBuckets:
 
     def _launch(self, b):
         bk = self.buckets[b]
+        if self.timing is not None and torch.cuda.is_available() and bk[0].is_cuda:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            self.timing.append((b, ev))
         bk[0].div_(self.world)
         bk[3] = dist.all_reduce(bk[0], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
@@ -169,6 +182,10 @@ class GradBuckets:
                 self._launch(b)
         for bk in self.buckets:
             bk[3].wait()
+        if self.timing is not None and torch.cuda.is_available() and self.buckets and self.buckets[0][0].is_cuda:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()  # the current stream has waited for every bucket
+            self.timing.append(("done", ev))
         out = {p: self.slot[p][1] for p in self.params}
         self._reset()
         return out

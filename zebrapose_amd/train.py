@@ -46,11 +46,19 @@ class TrainStep:
         self.code_loss = BinaryCodeLoss("BCE", True, 2, use_histgramm_weighted_binary_loss=True)
         self.mask_loss = MaskLoss()
         self.optimizer = FusedAdam(self.net.parameters(), lr=learning_rate)
+        self.events = None  # optional list: (label, event) at step start / before backward / after backward / end
+
+    def _mark(self, label):
+        if self.events is not None:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            self.events.append((label, ev))
 
     def __call__(self, x, gt_code, gt_mask, gt_entire_mask=None):
         """x f32 [B,3,H,W]; gt_code u8/f64 [B,L,H/2,W/2]; gt_mask f32 [B,H/2,W/2] -> (loss, loss_b, loss_m).
         With the 3-head BinaryCodeNet_Deeplab_v3 (train_v5.py:321-332) gt_entire_mask f32 [B,H/2,W/2] is
         required and loss = w * loss_b + loss_mask + loss_entire_mask."""
+        self._mark("start")
         self.optimizer.zero_grad(set_to_none=True)
         if self.buckets is not None:
             self.buckets.sync_buffers()
@@ -66,6 +74,9 @@ class TrainStep:
         loss = self.binary_loss_weight * loss_b + loss_m
         if len(out) == 3:
             loss = loss + self.mask_loss(entire, gt_entire_mask)
+        self._mark("backward")
         loss.backward()
+        self._mark("optimizer")
         self.optimizer.step()
+        self._mark("end")
         return loss.detach(), loss_b.detach(), loss_m.detach()
