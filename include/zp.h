@@ -108,10 +108,12 @@ int zp_conv2d_grid(const zp_conv_args* a);
 /* number of partial-sum slots `stats` needs: 2 * grid_x * nsub */
 int zp_conv2d_stat_parts(const zp_conv_args* a);
 /* launch configuration zp_conv2d picks: cout tile, pixel tile, LDS ring depth, kernel variant
- * (0 = k_conv, 1 = k_conv_strip: 3x3 stride-1 convs with activation-strip reuse) */
+ * (0 = k_conv, 1 = k_conv_strip: 3x3 stride-1 convs with activation-strip reuse, 2 = k_conv_strip2:
+ * the same with the lean main loop) */
 int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* stages, int* variant);
-/* runtime tuning knob (tests / sweeps): key 0 = minimum workgroup count for the 256-channel
- * tile (default 1024).  Returns the previous value, -1 for an unknown key. */
+/* runtime tuning knobs (tests / sweeps): key 0 = minimum workgroup count for the 256-channel
+ * tile (default 1024); key 1 = conv schedule flags (-1 = ZP_CONV_FLAGS or the default).  Returns
+ * the previous value, -1 for an unknown key. */
 int zp_conv_tuning(int key, int value);
 
 /* Pack an f32 weight tensor src[d0][d1][kh][kw] into dst[rows_pad][k_pad] (dtype), taps

@@ -1,0 +1,87 @@
+#!/usr/bin/env python3
+"""A/B of conv schedule variants in ONE process (interleaved rounds, median + min), eval forward
+(BN folded, ReLU), bf16, random activations.  Variants are zp_conv_tuning knobs (key 1 = conv flags,
+key 0 = 256-channel-tile threshold).  Every variant's output is compared bitwise with the first
+variant's (a schedule change must not change a single bit: same K order per output).
+
+    python tools/conv_ab.py --layers 256:256:128:1,512:512:32:4 --flags 28,60 [--rounds 7 --iters 10]
+
+layer = cin:cout:hw:dilation[:k]  (3x3 by default; batch --batch)."""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ.setdefault("ZP_QUIET", "1")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--layers", default="256:256:128:1,512:512:32:4,256:256:32:2,256:256:64:1")
+    ap.add_argument("--flags", default="28,60")
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args()
+    import zebrapose_amd._lib as L
+    from zebrapose_amd.engine import Engine, Unit, Act
+    from zebrapose_amd.model import layers as LY
+    dev = torch.device("cuda", 0)
+    flags = [int(f) for f in a.flags.split(",")]
+    rows = []
+    for spec in a.layers.split(","):
+        f = [int(v) for v in spec.split(":")]
+        cin, cout, hw, d = f[:4]
+        k = f[4] if len(f) > 4 else 3
+        torch.manual_seed(0)
+        conv = LY.Conv2d(cin, cout, k, 1, d * (k // 2), d, bias=False).to(dev)
+        torch.nn.init.normal_(conv.weight, 0, (2.0 / (cin * k * k)) ** 0.5)
+        bn = LY.BatchNorm2d(cout).to(dev).eval()
+        unit = Unit(conv, bn, relu=True)
+        eng = Engine(torch.nn.Module(), torch.bfloat16)
+        x = Act(torch.randn(a.batch, hw, hw, cin, device=dev).bfloat16())
+        y = Act(torch.empty(a.batch, hw, hw, cout, device=dev, dtype=torch.bfloat16))
+        fl = 2.0 * a.batch * hw * hw * k * k * cin * cout
+        times = {fv: [] for fv in flags}
+        ref = None
+        for r in range(a.rounds):
+            for fv in flags:
+                L.lib.zp_conv_tuning(1, fv)
+                eng.unit_fwd(unit, x, y, None)
+                torch.cuda.synchronize()
+                if r == 0:
+                    if ref is None:
+                        ref = y.buf.clone()
+                    else:
+                        same = torch.equal(ref.view(torch.int16), y.buf.view(torch.int16))
+                        if not same:
+                            nd = int((ref.view(torch.int16) != y.buf.view(torch.int16)).sum())
+                            print(f"!! {spec} flags {fv}: output differs from flags {flags[0]} in {nd} elements",
+                                  flush=True)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(a.iters):
+                    eng.unit_fwd(unit, x, y, None)
+                e1.record()
+                torch.cuda.synchronize()
+                times[fv].append(e0.elapsed_time(e1) * 1e3 / a.iters)
+        L.lib.zp_conv_tuning(1, -1)
+        for fv in flags:
+            med, mn = float(np.median(times[fv])), float(np.min(times[fv]))
+            row = {"layer": spec, "flags": fv, "us_median": round(med, 2), "us_min": round(mn, 2),
+                   "tflops_median": round(fl / med * 1e-6, 1)}
+            rows.append(row)
+            print(f"{spec:>16s} flags {fv:4d}: {med:8.1f} us (min {mn:8.1f})  {fl / med * 1e-6:7.1f} TFLOP/s", flush=True)
+    if a.json:
+        with open(a.json, "w") as fh:
+            json.dump(rows, fh, indent=0)
+
+
+if __name__ == "__main__":
+    main()

@@ -15,8 +15,9 @@
 #include "zp_common.h"
 
 // Diagnostic ablation builds only (tools/build_ablation.sh -> libzp_abl<N>.so; wrong results):
-// ZP_ABL 1 = k_conv / k_wgrad_lds issue no LDS-DMA, 2 = they run no MFMA, 3 = k_conv stages only
-// the weights (no activation DMA).  The product build is ZP_ABL 0.
+// ZP_ABL 1 = k_conv / k_conv_strip / k_wgrad_lds issue no LDS-DMA, 2 = they run no MFMA, 3 = k_conv
+// / k_conv_strip stage only the weights (no activation DMA), 4 = k_conv_strip stages only the strips.
+// The product build is ZP_ABL 0.
 #ifndef ZP_ABL
 #define ZP_ABL 0
 #endif
@@ -673,7 +674,20 @@ __global__ void __launch_bounds__(512) k_conv_strip(const zp_conv_args A, const 
   const int wc = wid / NWP, wp = wid % NWP;
   const int GHW = A.GH * A.GW;
   const int M = A.N * GHW;
-  const int bx = blockIdx.x, by = blockIdx.y;
+  int bx = blockIdx.x, by = blockIdx.y;
+  if (flags & 2) {
+    // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs (bid % 8 share one L2).
+    // Give each XCD a contiguous run of (pixel tile, cout tile) pairs, cout tiles fastest, so the
+    // cout tiles of one pixel tile (same strip) and neighbouring pixel tiles (shared halo rows)
+    // are served by the same L2 instead of each fetching its strip from beyond it.  Bijective for
+    // any total (cdna_hip_programming.md T1).
+    const int total = gridDim.x * gridDim.y;
+    const int bid = blockIdx.x + gridDim.x * blockIdx.y;
+    const int xcd = bid & 7, pos = bid >> 3, q = total >> 3, r = total & 7;
+    const int lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
+    bx = lin / gridDim.y;
+    by = lin - bx * gridDim.y;
+  }
   const int p0 = bx * TP, c0 = by * TC;
   const int n_img = p0 / GHW, y0 = (p0 - n_img * GHW) / SG.W;
   const int CB = A.Cin / 64;
@@ -713,24 +727,28 @@ __global__ void __launch_bounds__(512) k_conv_strip(const zp_conv_args A, const 
     }
 #endif
   };
-  auto issue_s = [&](int g, uint4* dst) {
+  // strip pieces [I0, I1) of group g (all SPW pieces by default)
+  auto issue_s = [&](int g, uint4* dst, auto i0_c, auto i1_c) {
+    constexpr int I0 = decltype(i0_c)::value, I1 = decltype(i1_c)::value;
     const int ky = g / CB, cb = g - ky * CB;
     const int ty = SG.ty0 + ky * SG.dty;
     unsigned voff[SPW];
 #pragma unroll
-    for (int i = 0; i < SPW; ++i) {
+    for (int i = I0; i < I1; ++i) {
       const int tr = sbase[i] & 15;
       const bool ok = sbase[i] >= 0 && (unsigned)(y0 + ty + tr) < (unsigned)A.IH;
       voff[i] = ok ? (unsigned)((sbase[i] & ~15) + ty * rowb + cb * 128) : 0x80000000u;
     }
 #if defined(__HIP_DEVICE_COMPILE__)
 #pragma unroll
-    for (int i = 0; i < SPW; ++i) {
+    for (int i = I0; i < I1; ++i) {
       auto* d = (__attribute__((address_space(3))) void*)&dst[(wid + 8 * i) * 64];
       __builtin_amdgcn_raw_ptr_buffer_load_lds(xrsrc, d, 16, voff[i], 0, 0, 0);
     }
 #endif
   };
+  using C0 = std::integral_constant<int, 0>;
+  using CS = std::integral_constant<int, SPW>;
 
   f32x4 acc[WC][WP];
 #pragma unroll
@@ -754,14 +772,34 @@ __global__ void __launch_bounds__(512) k_conv_strip(const zp_conv_args A, const 
   }
   const int jrow = SG.W == 32 ? SG.SW - 32 : 0;  // extra offset for fragments 2, 3 when W == 32
   const bool pingpong = (flags & 8) != 0;
+  // flags & 32 (3-stage ring only): the next group's strip DMA is spread over the three steps of the
+  // current group (pieces [0,N0) | [N0,N0+N1) | [N0+N1,SPW)) instead of all SPW pieces in one step,
+  // so no read section carries SPW + WPW LDS-DMA issues (~60-180 cycles each) at once
+  const bool spread = STAGES == 3 && (flags & 32) != 0;
+  constexpr int N0 = (SPW + 2) / 3, N1 = (SPW + 1) / 3;
 
   // step phase PH = ks % 3 = tap column (compile-time); weight slot ks % STAGES, strip slot g & 1
   auto step = [&](auto ph_c, int ks) {
     constexpr int PH = decltype(ph_c)::value;
     const bool more_w = ks + (STAGES - 1) < nK;
     const bool strip_next = ((PH + 2) % 3 == 0) && ks + 2 < nK;
-    if (more_w) issue_w(ks + (STAGES - 1), wbuf((ks + STAGES - 1) % STAGES));
-    if (strip_next) issue_s((ks + 2) / 3, sbuf(((ks + 2) / 3) & 1));
+    const int gnext = ks / 3 + 1;
+    const bool has_next = gnext * 3 < nK;  // the next group exists (its strip is staged by this group)
+    if (!spread) {
+      // (diagnostic builds: ZP_ABL 1 = no DMA in the loop, 3 = weights only, 4 = strips only)
+      if (ZP_ABL != 1 && ZP_ABL != 4 && more_w) issue_w(ks + (STAGES - 1), wbuf((ks + STAGES - 1) % STAGES));
+      if (ZP_ABL != 1 && ZP_ABL != 3 && strip_next) issue_s((ks + 2) / 3, sbuf(((ks + 2) / 3) & 1), C0{}, CS{});
+    } else if constexpr (PH == 0) {
+      if (more_w) issue_w(ks + 2, wbuf((ks + 2) % 3));
+      if (has_next) issue_s(gnext, sbuf(gnext & 1), C0{}, std::integral_constant<int, N0>{});
+    } else if constexpr (PH == 1) {
+      if (more_w) issue_w(ks + 2, wbuf((ks + 2) % 3));
+      if (has_next) issue_s(gnext, sbuf(gnext & 1), std::integral_constant<int, N0>{},
+                            std::integral_constant<int, N0 + N1>{});
+    } else {
+      if (has_next) issue_s(gnext, sbuf(gnext & 1), std::integral_constant<int, N0 + N1>{}, CS{});
+      if (more_w) issue_w(ks + 2, wbuf((ks + 2) % 3));
+    }
     const int g = ks / 3;
     const int txo = SG.tx0 + PH * SG.dtx;
     const unsigned cw = lds_addr(wbuf(ks % STAGES));
@@ -771,6 +809,25 @@ __global__ void __launch_bounds__(512) k_conv_strip(const zp_conv_args A, const 
     constexpr int OUT = (STAGES == 3 ? WPW : 0) + OUT_S2;
     // (a step whose strip slot would have been refilled past the end issued no strip)
     auto wait_out = [&]() {
+      if (spread) {
+        // loads allowed in flight: this step's weights (for ks + 2) and the pieces of the next
+        // strip issued after the weights of step ks + 1, except in the group's last step
+        if constexpr (PH == 0) {
+          if (more_w && has_next) vm_wait<WPW + N0>();
+          else if (more_w) vm_wait<WPW>();
+          else if (has_next) vm_wait<N0>();
+          else vm_wait<0>();
+        } else if constexpr (PH == 1) {
+          if (more_w && has_next) vm_wait<WPW + N0 + N1>();
+          else if (more_w) vm_wait<WPW>();
+          else if (has_next) vm_wait<N0 + N1>();
+          else vm_wait<0>();
+        } else {
+          if (more_w) vm_wait<WPW>();
+          else vm_wait<0>();
+        }
+        return;
+      }
       if (strip_next) vm_wait<OUT>();
       else if (more_w) vm_wait<OUT - OUT_S2>();
       else vm_wait<0>();
@@ -795,12 +852,21 @@ __global__ void __launch_bounds__(512) k_conv_strip(const zp_conv_args A, const 
       __builtin_amdgcn_sched_barrier(0);
     }
     __builtin_amdgcn_s_setprio(1);
+    if constexpr (ZP_ABL != 2) {
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
+      for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-      for (int i = 0; i < WC; ++i)
+        for (int i = 0; i < WC; ++i)
 #pragma unroll
-        for (int j = 0; j < WP; ++j) MfmaTraits<T>::mma(acc[i][j], af[s2][i], bfr[s2][j]);
+          for (int j = 0; j < WP; ++j) MfmaTraits<T>::mma(acc[i][j], af[s2][i], bfr[s2][j]);
+    } else {
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int i = 0; i < WC; ++i)
+#pragma unroll
+          for (int j = 0; j < WP; ++j) acc[i][j][0] += __uint_as_float(af[s2][i].x ^ bfr[s2][j].y);
+    }
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(0);
     if (!pingpong) wait_out();
@@ -809,7 +875,7 @@ __global__ void __launch_bounds__(512) k_conv_strip(const zp_conv_args A, const 
   };
   // prologue: strip of group 0, weights of steps 0 .. STAGES-2; the strip of group 1 is issued
   // at step 1 (two steps ahead of step 3)
-  issue_s(0, sbuf(0));
+  issue_s(0, sbuf(0), C0{}, CS{});
   issue_w(0, wbuf(0));
   if (STAGES == 3) issue_w(1, wbuf(1));
   if (STAGES == 3) vm_wait<WPW>();  // strip(0) and weights(0) landed; weights(1) may be in flight
@@ -825,6 +891,256 @@ __global__ void __launch_bounds__(512) k_conv_strip(const zp_conv_args A, const 
     step(P1{}, ks + 1);
     step(P2{}, ks + 2);
   }
+  if (pingpong && wid < 4) __builtin_amdgcn_s_barrier();
+  conv_epilogue<T, WC, WP, NWP>(A, S, acc, p0, c0, wc, wp, lane, M, GHW, bx);
+}
+
+// ------------------------------------------------------------------------------------
+// k_conv_strip2: k_conv_strip's algorithm (same staging, same K order, bit-identical results)
+// with a lean main loop.  Profiling k_conv_strip (256 -> 256 at 128 x 128, bs 32) showed the
+// read section of every step -- not the MFMAs, not L2 / HBM -- as the critical path: the MFMA-free
+// ablation ran exactly as long as the full kernel, and each step issued ~65 SALU (runtime
+// divisions for the tap / chunk / slot of every DMA, a branch tree of counted waits) and ~70 VALU
+// (per-step fragment and DMA address arithmetic, an SGPR-spilled buffer descriptor rebuilt with
+// v_readlane) besides its 16 ds_reads and 2-7 LDS-DMAs.  Here:
+//   * the loop is unrolled by group parity x tap column, so every LDS address is a per-lane base
+//     register + an immediate (weight slot = tap column, strip slot = group parity) and every wait
+//     count is a constant; the steady-state groups (all of whose steps prefetch) are separated
+//     from the last group, so the loop body has no prefetch conditions;
+//   * DMA offsets are per-lane registers computed once (weights: row offsets; strips: one per tap
+//     row and piece) plus a scalar offset advanced by additions (no divisions);
+//   * one __shared__ array (weights ring, then strip ring).
+// ------------------------------------------------------------------------------------
+template <typename T, int WC, int SPW>
+__global__ void __launch_bounds__(512) k_conv_strip2(const zp_conv_args A, const strip_geo SG, const int flags) {
+  constexpr int WP = 4, NWP = 4, NW = 8;
+  constexpr int TC = 32 * WC, TP = 256;
+  constexpr int WPW = TC / 8 / NW;  // weight DMA instrs per wave per step
+  constexpr int SRP = 64 * SPW;     // strip rows incl. padding
+  constexpr int WSLOT = TC * 128;   // bytes per weight slot (3 slots)
+  constexpr int SSLOT = SRP * 128;  // bytes per strip slot (2 slots)
+  static_assert(SSLOT < 65536 && 2 * WSLOT + 2048 * (WC - 1) < 65536, "ds_read immediate range");
+  __shared__ uint4 lds[(3 * TC + 2 * SRP) * 8];
+  const zp_conv_sub& S = A.sub[0];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wid / NWP, wp = wid % NWP;
+  const int GHW = A.GH * A.GW;
+  const int M = A.N * GHW;
+  int bx = blockIdx.x, by = blockIdx.y;
+  if (flags & 2) {  // XCD-aware order, as k_conv_strip
+    const int total = gridDim.x * gridDim.y;
+    const int bid = blockIdx.x + gridDim.x * blockIdx.y;
+    const int xcd = bid & 7, pos = bid >> 3, q = total >> 3, r = total & 7;
+    const int lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
+    bx = lin / gridDim.y;
+    by = lin - bx * gridDim.y;
+  }
+  const int p0 = bx * TP, c0 = by * TC;
+  const int n_img = p0 / GHW, y0 = (p0 - n_img * GHW) / SG.W;
+  const int CB = A.Cin / 64;
+  const int lrow = lane >> 3;
+  const int csrc = (lane & 7) ^ lrow;
+
+#if defined(__HIP_DEVICE_COMPILE__)
+  const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)A.x, (short)0, (int)SG.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)S.w, (short)0, (int)SG.w_bytes, 0x00020000);
+#endif
+  // weight DMA: per-lane row offsets (piece i = rows (wid + NW i) * 8 + lrow); the K offset of a
+  // step is scalar: koff = (ky * 3 + kx) * Cin * 2 + cb * 128
+  unsigned wv[WPW];
+#pragma unroll
+  for (int i = 0; i < WPW; ++i)
+    wv[i] = (unsigned)(((size_t)(c0 + (wid + NW * i) * 8 + lrow) * A.k_pad + csrc * 8) * 2);
+  const int cin2 = A.Cin * 2;
+  // strip DMA: per piece and tap row ky, the lane's source byte offset (chunk 0) or an offset past
+  // the buffer end (zeros) for padding rows / columns; the chunk's cb * 128 goes in the scalar offset
+  const int rowb = A.IW * A.ldx * 2;
+  // pk[i]: the piece's 16-byte-aligned source offset for tap row 0 with a 3-bit "row inside the
+  // image" mask per tap row in the low bits; svn[i]: the offsets for the next strip's tap row,
+  // recomputed (a few VALU per piece) only when that tap row changes, i.e. 3 times per workgroup
+  unsigned pk[SPW], svn[SPW];
+#pragma unroll
+  for (int i = 0; i < SPW; ++i) {
+    const int srow = (wid + 8 * i) * 8 + lrow;
+    const int tr = srow / SG.SW, c = srow - tr * SG.SW;
+    const int ix = c - SG.pad;
+    const bool ok = srow < SG.SR && (unsigned)ix < (unsigned)A.IW;
+    const int sw = (lane & 7) ^ (srow & 7);
+    const int base = (((n_img * A.IH + y0 + tr) * A.IW + ix) * A.ldx + A.cx0 + sw * 8) * 2 + SG.ty0 * rowb;
+    unsigned m = 0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+      m |= (unsigned)(ok && (unsigned)(y0 + SG.ty0 + k * SG.dty + tr) < (unsigned)A.IH) << k;
+    pk[i] = (unsigned)base | m;
+  }
+  const int dtyb = SG.dty * rowb;
+  auto set_svn = [&](int k) {
+#pragma unroll
+    for (int i = 0; i < SPW; ++i)
+      svn[i] = (pk[i] >> k) & 1u ? (pk[i] & ~15u) + (unsigned)(k * dtyb) : 0x80000000u;
+  };
+  const unsigned lds0 = lds_addr(lds);
+  // fragment bases: A (weights) row wc*16*WC + (lane & 15), swizzled chunk; + slot * WSLOT + i * 2048
+  unsigned aoff[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2)
+    aoff[s2] = lds0 + (unsigned)(wc * 16 * WC + (lane & 15)) * 128u + (unsigned)(((s2 * 4 + (lane >> 4)) ^ (lane & 7)) * 16);
+  // B (strip) per tap column PH, half s2, pixel fragment j; + parity * SSLOT
+  unsigned bo[3][2][WP];
+  {
+    const int q0 = wp * 16 * WP;
+    const int tr = q0 / SG.W, x0 = q0 - tr * SG.W;
+    const int bsrow0 = tr * SG.SW + x0 + (lane & 15) + SG.pad;
+    const int jrow = SG.W == 32 ? SG.SW - 32 : 0;
+#pragma unroll
+    for (int ph = 0; ph < 3; ++ph)
+#pragma unroll
+      for (int j = 0; j < WP; ++j) {
+        const int sr = bsrow0 + SG.tx0 + ph * SG.dtx + 16 * j + (j >= 2 ? jrow : 0);
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+          bo[ph][s2][j] = lds0 + 3u * WSLOT + (unsigned)sr * 128u + (unsigned)(((s2 * 4 + (lane >> 4)) ^ (sr & 7)) * 16);
+      }
+  }
+  const bool pingpong = (flags & 8) != 0;
+
+  auto issue_w = [&](int slot, int koff) {
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+    for (int i = 0; i < WPW; ++i) {
+      auto* d = (__attribute__((address_space(3))) void*)&lds[(slot * TC + (wid + NW * i) * 8) * 8];
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrsrc, d, 16, wv[i], koff, 0, 0);
+    }
+#endif
+  };
+  auto issue_s = [&](int slot, int cb) {  // the strip of the group whose tap row svn holds
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+    for (int i = 0; i < SPW; ++i) {
+      auto* d = (__attribute__((address_space(3))) void*)&lds[(3 * TC + slot * SRP + (wid + 8 * i) * 8) * 8];
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrsrc, d, 16, svn[i], cb * 128, 0, 0);
+    }
+#endif
+  };
+
+  f32x4 acc[WC][WP];
+#pragma unroll
+  for (int i = 0; i < WC; ++i)
+#pragma unroll
+    for (int j = 0; j < WP; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // one K step: tap column PH of a group with strip parity GP.  Prefetch (issued first): PH 0 the
+  // weights of (this group, column 2) -> slot 2; PH 1 the weights of (next group, column 0) -> slot 0
+  // and the next group's strip -> slot GP ^ 1; PH 2 the weights of (next group, column 1) -> slot 1.
+  // Waits: what the next step reads must have landed.
+  auto step = [&](auto gp_c, auto ph_c, auto steady_c, int koff_cur, int koff_next, int ncb) {
+    constexpr int GP = decltype(gp_c)::value, PH = decltype(ph_c)::value;
+    constexpr bool STEADY = decltype(steady_c)::value;
+    if constexpr (PH == 0) {
+      issue_w(2, koff_cur + 2 * cin2);
+    } else if constexpr (STEADY && PH == 1) {
+      issue_w(0, koff_next);
+      issue_s(GP ^ 1, ncb);
+    } else if constexpr (STEADY && PH == 2) {
+      issue_w(1, koff_next + cin2);
+    }
+    uint4 af[2][WC], bfr[2][WP];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      static_for<WC>([&](auto i) { af[s2][i] = ds_read16<PH * WSLOT + i * 2048>(aoff[s2]); });
+      static_for<WP>([&](auto j) { bfr[s2][j] = ds_read16<GP * SSLOT>(bo[PH][s2][j]); });
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    auto wait_out = [&]() {
+      if constexpr (PH == 0) vm_wait<WPW>();
+      else if constexpr (STEADY && PH == 1) vm_wait<WPW + SPW>();
+      else if constexpr (STEADY && PH == 2) vm_wait<WPW>();
+      else vm_wait<0>();
+    };
+    if (pingpong) {
+      wait_out();
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __builtin_amdgcn_s_setprio(1);
+    if constexpr (ZP_ABL != 2) {
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int i = 0; i < WC; ++i)
+#pragma unroll
+          for (int j = 0; j < WP; ++j) MfmaTraits<T>::mma(acc[i][j], af[s2][i], bfr[s2][j]);
+    } else {
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int i = 0; i < WC; ++i)
+#pragma unroll
+          for (int j = 0; j < WP; ++j) acc[i][j][0] += __uint_as_float(af[s2][i].x ^ bfr[s2][j].y);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(0);
+    if (!pingpong) wait_out();
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  using P0 = std::integral_constant<int, 0>;
+  using P1 = std::integral_constant<int, 1>;
+  using P2 = std::integral_constant<int, 2>;
+  using G0 = std::integral_constant<int, 0>;
+  using G1 = std::integral_constant<int, 1>;
+  using ST = std::integral_constant<bool, true>;
+  using TL = std::integral_constant<bool, false>;
+  auto group = [&](auto gp_c, auto steady_c, int koff_cur, int koff_next, int ncb) {
+    step(gp_c, P0{}, steady_c, koff_cur, koff_next, ncb);
+    step(gp_c, P1{}, steady_c, koff_cur, koff_next, ncb);
+    step(gp_c, P2{}, steady_c, koff_cur, koff_next, ncb);
+  };
+
+  // groups (ky, cb), cb fastest; koff of (ky, cb, kx = 0) = ky * 3 * Cin * 2 + cb * 128
+  int ky = 0, cb = 0;
+  auto koff_of = [&](int a, int b) { return a * 3 * cin2 + b * 128; };
+  // the next group (its strip is staged during the current one); svn follows its tap row
+  int nky = 0, ncb = 0;
+  auto advance_next = [&]() {
+    if (++ncb == CB) {
+      ncb = 0;
+      ++nky;
+      if (nky < 3) set_svn(nky);
+    }
+  };
+  // prologue: strip of group 0, weights of steps 0 and 1
+  set_svn(0);
+  issue_s(0, 0);
+  issue_w(0, 0);
+  issue_w(1, cin2);
+  vm_wait<WPW>();
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  if (pingpong && wid >= 4) __builtin_amdgcn_s_barrier();
+  const int ng = 3 * CB;
+  advance_next();
+  int g = 0;
+  for (; g + 2 <= ng - 1; g += 2) {
+    group(G0{}, ST{}, koff_of(ky, cb), koff_of(nky, ncb), ncb);
+    ky = nky;
+    cb = ncb;
+    advance_next();
+    group(G1{}, ST{}, koff_of(ky, cb), koff_of(nky, ncb), ncb);
+    ky = nky;
+    cb = ncb;
+    advance_next();
+  }
+  if (g < ng - 1) {
+    group(G0{}, ST{}, koff_of(ky, cb), koff_of(nky, ncb), ncb);
+    ky = nky;
+    cb = ncb;
+    ++g;
+  }
+  if (g & 1) group(G1{}, TL{}, koff_of(ky, cb), 0, 0);
+  else group(G0{}, TL{}, koff_of(ky, cb), 0, 0);
   if (pingpong && wid < 4) __builtin_amdgcn_s_barrier();
   conv_epilogue<T, WC, WP, NWP>(A, S, acc, p0, c0, wc, wp, lane, M, GHW, bx);
 }
@@ -1388,13 +1704,16 @@ static int conv_stages_override() {
   return v;
 }
 
-// k_conv schedule switches: bit 1 XCD-aware tile order, bit 2 s_setprio(1) around the MFMA
+// conv schedule switches: bit 1 XCD-aware tile order, bit 2 s_setprio(1) around the MFMA
 // cluster, bit 3 ping-pong (staggered wave groups), bit 4 tap-row trimming (tap rows that read only
-// padding for a whole tile are skipped).  Default (measured, profiles/r01_conv_sweep.md):
-// setprio + ping-pong + trimming.  ZP_CONV_FLAGS overrides for sweeps.
+// padding for a whole tile are skipped), bit 5 spread strip DMA (k_conv_strip only; slower), bit 6
+// k_conv_strip2 instead of k_conv_strip.  Default (measured, profiles/r01_conv_sweep.md,
+// profiles/r02_conv_ab.md): XCD order + setprio + ping-pong + trimming + k_conv_strip2 (94).
+// ZP_CONV_FLAGS / zp_conv_tuning(1, .) override for sweeps.
+static int g_conv_flags = -1;  // zp_conv_tuning key 1 (runtime A/B in one process); -1 = env / default
 static int conv_flags() {
-  static const int v = getenv("ZP_CONV_FLAGS") ? env_int("ZP_CONV_FLAGS") : 28;
-  return v;
+  static const int v = getenv("ZP_CONV_FLAGS") ? env_int("ZP_CONV_FLAGS") : 94;
+  return g_conv_flags >= 0 ? g_conv_flags : v;
 }
 
 // 3x3 stride-1 same-size bf16 convs on full-width tiles (W 32 / 64 / 128) whose strip of
@@ -1550,12 +1869,21 @@ extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
     ZP_CHECK_ARG(!a.stats || 4 * sgx == zp_conv2d_stat_parts(&a),
                  "zp_conv2d: strip launch emits %d stat parts, zp_conv2d_stat_parts says %d", 4 * sgx,
                  zp_conv2d_stat_parts(&a));
-    if (a.dtype == ZP_F16) {
-      if (tc == 64) hipLaunchKernelGGL((k_conv_strip<f16_t, 2, 3, 5>), grid, dim3(512), 0, st, a, sg, conv_flags());
-      else hipLaunchKernelGGL((k_conv_strip<f16_t, 4, 3, 5>), grid, dim3(512), 0, st, a, sg, conv_flags());
+    const int fl = conv_flags();
+    if (fl & 64) {  // k_conv_strip2 (lean main loop)
+      if (a.dtype == ZP_F16) {
+        if (tc == 64) hipLaunchKernelGGL((k_conv_strip2<f16_t, 2, 5>), grid, dim3(512), 0, st, a, sg, fl);
+        else hipLaunchKernelGGL((k_conv_strip2<f16_t, 4, 5>), grid, dim3(512), 0, st, a, sg, fl);
+      } else {
+        if (tc == 64) hipLaunchKernelGGL((k_conv_strip2<bf16_t, 2, 5>), grid, dim3(512), 0, st, a, sg, fl);
+        else hipLaunchKernelGGL((k_conv_strip2<bf16_t, 4, 5>), grid, dim3(512), 0, st, a, sg, fl);
+      }
+    } else if (a.dtype == ZP_F16) {
+      if (tc == 64) hipLaunchKernelGGL((k_conv_strip<f16_t, 2, 3, 5>), grid, dim3(512), 0, st, a, sg, fl);
+      else hipLaunchKernelGGL((k_conv_strip<f16_t, 4, 3, 5>), grid, dim3(512), 0, st, a, sg, fl);
     } else {
-      if (tc == 64) hipLaunchKernelGGL((k_conv_strip<bf16_t, 2, 3, 5>), grid, dim3(512), 0, st, a, sg, conv_flags());
-      else hipLaunchKernelGGL((k_conv_strip<bf16_t, 4, 3, 5>), grid, dim3(512), 0, st, a, sg, conv_flags());
+      if (tc == 64) hipLaunchKernelGGL((k_conv_strip<bf16_t, 2, 3, 5>), grid, dim3(512), 0, st, a, sg, fl);
+      else hipLaunchKernelGGL((k_conv_strip<bf16_t, 4, 3, 5>), grid, dim3(512), 0, st, a, sg, fl);
     }
     ZP_LAUNCH_CHECK("zp_conv2d strip");
     return ZP_OK;
@@ -1739,16 +2067,22 @@ extern "C" int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* st
   *tc = conv_tc(*a);
   *tp = conv_tp(*a);
   *stages = *tc == 256 ? 2 : conv_stages(*a, *tc);
-  *variant = *tc <= 128 && strip_eligible(*a, nullptr) ? 1 : 0;
+  *variant = *tc <= 128 && strip_eligible(*a, nullptr) ? ((conv_flags() & 64) ? 2 : 1) : 0;
   return ZP_OK;
 }
 
 /* runtime tuning knobs (tests / sweeps).  key 0: minimum workgroups for the 256-channel conv tile
- * (default 1024).  Returns the previous value. */
+ * (default 1024); key 1: conv schedule flags (-1 = ZP_CONV_FLAGS / default).  Returns the previous
+ * value. */
 extern "C" int zp_conv_tuning(int key, int value) {
   if (key == 0) {
     const int old = g_tc256_min_blocks;
     g_tc256_min_blocks = value;
+    return old;
+  }
+  if (key == 1) {
+    const int old = g_conv_flags;
+    g_conv_flags = value;
     return old;
   }
   return -1;
