@@ -112,8 +112,10 @@ int zp_conv2d_stat_parts(const zp_conv_args* a);
  * the same with the lean main loop) */
 int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* stages, int* variant);
 /* runtime tuning knobs (tests / sweeps): key 0 = minimum workgroup count for the 256-channel
- * tile (default 1024); key 1 = conv schedule flags (-1 = ZP_CONV_FLAGS or the default).  Returns
- * the previous value, -1 for an unknown key. */
+ * tile (default 1024); key 1 = conv schedule flags (-1 = ZP_CONV_FLAGS or the default); key 2 =
+ * 64-channel layers on the strip kernel (default 1); key 3 = the lean weight-gradient kernel
+ * (default 1); key 4 = its target workgroup count (default 512).  Returns the previous value, -1
+ * for an unknown key. */
 int zp_conv_tuning(int key, int value);
 
 /* Pack an f32 weight tensor src[d0][d1][kh][kw] into dst[rows_pad][k_pad] (dtype), taps

@@ -6,7 +6,8 @@ variant's (a schedule change must not change a single bit: same K order per outp
 
     python tools/conv_ab.py --layers 256:256:128:1,512:512:32:4 --flags 28,60 [--rounds 7 --iters 10]
 
-layer = cin:cout:hw:dilation[:k]  (3x3 by default; batch --batch)."""
+layer = cin:cout:hw:dilation[:k]  (3x3 by default; batch --batch).  A variant is a flags value,
+optionally with extra knobs: "94+noc64" sets zp_conv_tuning(2, 0) (64-channel layers on k_conv)."""
 import argparse
 import json
 import os
@@ -28,34 +29,67 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--wgrad", action="store_true", help="time the weight gradient (dy = the output buffer)")
     a = ap.parse_args()
     import zebrapose_amd._lib as L
     from zebrapose_amd.engine import Engine, Unit, Act
     from zebrapose_amd.model import layers as LY
     dev = torch.device("cuda", 0)
-    flags = [int(f) for f in a.flags.split(",")]
+    flags = a.flags.split(",")
+
+    def apply(v):
+        parts = v.split("+")
+        L.lib.zp_conv_tuning(1, int(parts[0]))
+        L.lib.zp_conv_tuning(2, 0 if "noc64" in parts[1:] else 1)
+        L.lib.zp_conv_tuning(0, 1 << 30 if "no256" in parts[1:] else (1 if "all256" in parts[1:] else 1024))
+        L.lib.zp_conv_tuning(3, 0 if "now2" in parts[1:] else 1)
+        tg = [int(q[1:]) for q in parts[1:] if q.startswith("t") and q[1:].isdigit()]
+        L.lib.zp_conv_tuning(4, tg[0] if tg else 512)
     rows = []
     for spec in a.layers.split(","):
-        f = [int(v) for v in spec.split(":")]
-        cin, cout, hw, d = f[:4]
+        tr = spec.startswith("T")  # T<cin>:<cout>:<hw>: ConvTranspose2d(3, s2, p1, op1) (aspp.py:60-80)
+        f = [int(v) for v in spec.lstrip("T").split(":")]
+        cin, cout, hw = f[:3]
+        d = f[3] if len(f) > 3 else 1
         k = f[4] if len(f) > 4 else 3
         torch.manual_seed(0)
-        conv = LY.Conv2d(cin, cout, k, 1, d * (k // 2), d, bias=False).to(dev)
+        if tr:
+            conv = LY.ConvTranspose2d(cin, cout, 3, 2, 1, 1, bias=False).to(dev)
+        else:
+            conv = LY.Conv2d(cin, cout, k, 1, d * (k // 2), d, bias=False).to(dev)
         torch.nn.init.normal_(conv.weight, 0, (2.0 / (cin * k * k)) ** 0.5)
         bn = LY.BatchNorm2d(cout).to(dev).eval()
         unit = Unit(conv, bn, relu=True)
         eng = Engine(torch.nn.Module(), torch.bfloat16)
         x = Act(torch.randn(a.batch, hw, hw, cin, device=dev).bfloat16())
-        y = Act(torch.empty(a.batch, hw, hw, cout, device=dev, dtype=torch.bfloat16))
-        fl = 2.0 * a.batch * hw * hw * k * k * cin * cout
+        ohw = 2 * hw if tr else hw
+        y = Act(torch.empty(a.batch, ohw, ohw, cout, device=dev, dtype=torch.bfloat16))
+        fl = 2.0 * a.batch * hw * hw * k * k * cin * cout  # ConvT: 9 taps per input pixel as well
+        dw = torch.empty_like(conv.weight)
+        if a.wgrad:
+            y.buf.copy_(torch.randn(y.buf.shape, device=dev).clamp(min=0).bfloat16())
+        plan = unit.fwd_plan(hw, hw)
+
+        def run():
+            if a.wgrad:
+                eng._wgrad(unit, x, plan, y, dw)
+            else:
+                eng.unit_fwd(unit, x, y, None)
         times = {fv: [] for fv in flags}
         ref = None
         for r in range(a.rounds):
             for fv in flags:
-                L.lib.zp_conv_tuning(1, fv)
-                eng.unit_fwd(unit, x, y, None)
+                apply(fv)
+                run()
                 torch.cuda.synchronize()
-                if r == 0:
+                if r == 0 and a.wgrad:
+                    if ref is None:
+                        ref = dw.clone()
+                    else:
+                        rel = float((dw - ref).norm() / ref.norm())
+                        if not rel < 1e-5:
+                            print(f"!! {spec} flags {fv}: dw rel diff {rel:.3g} vs flags {flags[0]}", flush=True)
+                elif r == 0:
                     if ref is None:
                         ref = y.buf.clone()
                     else:
@@ -67,17 +101,21 @@ def main():
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(a.iters):
-                    eng.unit_fwd(unit, x, y, None)
+                    run()
                 e1.record()
                 torch.cuda.synchronize()
                 times[fv].append(e0.elapsed_time(e1) * 1e3 / a.iters)
         L.lib.zp_conv_tuning(1, -1)
+        L.lib.zp_conv_tuning(2, 1)
+        L.lib.zp_conv_tuning(0, 1024)
+        L.lib.zp_conv_tuning(3, 1)
+        L.lib.zp_conv_tuning(4, 512)
         for fv in flags:
             med, mn = float(np.median(times[fv])), float(np.min(times[fv]))
             row = {"layer": spec, "flags": fv, "us_median": round(med, 2), "us_min": round(mn, 2),
                    "tflops_median": round(fl / med * 1e-6, 1)}
             rows.append(row)
-            print(f"{spec:>16s} flags {fv:4d}: {med:8.1f} us (min {mn:8.1f})  {fl / med * 1e-6:7.1f} TFLOP/s", flush=True)
+            print(f"{spec:>16s} flags {fv:>8s}: {med:8.1f} us (min {mn:8.1f})  {fl / med * 1e-6:7.1f} TFLOP/s", flush=True)
     if a.json:
         with open(a.json, "w") as fh:
             json.dump(rows, fh, indent=0)

@@ -9,7 +9,7 @@ d = sys.argv[1]
 vals = defaultdict(list)
 for f in sorted(glob.glob(f"{d}/**/*counter_collection.csv", recursive=True)):
     for r in csv.DictReader(open(f)):
-        if "k_conv" not in r["Kernel_Name"]:
+        if "k_conv" not in r["Kernel_Name"] and "k_wgrad" not in r["Kernel_Name"]:
             continue
         vals[(r["Kernel_Name"][:60], r["Counter_Name"])].append(float(r["Counter_Value"]))
 for (k, c), v in sorted(vals.items()):

@@ -911,7 +911,7 @@ __global__ void __launch_bounds__(512) k_conv_strip(const zp_conv_args A, const 
 //     row and piece) plus a scalar offset advanced by additions (no divisions);
 //   * one __shared__ array (weights ring, then strip ring).
 // ------------------------------------------------------------------------------------
-template <typename T, int WC, int SPW>
+template <typename T, int WC, int SPW, bool SPREAD>
 __global__ void __launch_bounds__(512) k_conv_strip2(const zp_conv_args A, const strip_geo SG, const int flags) {
   constexpr int WP = 4, NWP = 4, NW = 8;
   constexpr int TC = 32 * WC, TP = 256;
@@ -1014,10 +1014,12 @@ __global__ void __launch_bounds__(512) k_conv_strip2(const zp_conv_args A, const
     }
 #endif
   };
-  auto issue_s = [&](int slot, int cb) {  // the strip of the group whose tap row svn holds
+  constexpr int N0 = (SPW + 2) / 3, N1 = (SPW + 1) / 3;  // SPREAD: pieces per step (PH 0 / 1 / 2 = rest)
+  auto issue_s = [&](int slot, int cb, auto i0_c, auto i1_c) {  // pieces [I0, I1) of the strip svn holds
+    constexpr int I0 = decltype(i0_c)::value, I1 = decltype(i1_c)::value;
 #if defined(__HIP_DEVICE_COMPILE__)
 #pragma unroll
-    for (int i = 0; i < SPW; ++i) {
+    for (int i = I0; i < I1; ++i) {
       auto* d = (__attribute__((address_space(3))) void*)&lds[(3 * TC + slot * SRP + (wid + 8 * i) * 8) * 8];
       __builtin_amdgcn_raw_ptr_buffer_load_lds(xrsrc, d, 16, svn[i], cb * 128, 0, 0);
     }
@@ -1037,13 +1039,32 @@ __global__ void __launch_bounds__(512) k_conv_strip2(const zp_conv_args A, const
   auto step = [&](auto gp_c, auto ph_c, auto steady_c, int koff_cur, int koff_next, int ncb) {
     constexpr int GP = decltype(gp_c)::value, PH = decltype(ph_c)::value;
     constexpr bool STEADY = decltype(steady_c)::value;
-    if constexpr (PH == 0) {
-      issue_w(2, koff_cur + 2 * cin2);
-    } else if constexpr (STEADY && PH == 1) {
-      issue_w(0, koff_next);
-      issue_s(GP ^ 1, ncb);
-    } else if constexpr (STEADY && PH == 2) {
-      issue_w(1, koff_next + cin2);
+    using Z = std::integral_constant<int, 0>;
+    using K0 = std::integral_constant<int, N0>;
+    using K1 = std::integral_constant<int, N0 + N1>;
+    using KS = std::integral_constant<int, SPW>;
+    if constexpr (!SPREAD) {
+      if constexpr (PH == 0) {
+        issue_w(2, koff_cur + 2 * cin2);
+      } else if constexpr (STEADY && PH == 1) {
+        issue_w(0, koff_next);
+        issue_s(GP ^ 1, ncb, Z{}, KS{});
+      } else if constexpr (STEADY && PH == 2) {
+        issue_w(1, koff_next + cin2);
+      }
+    } else {
+      // the next strip in three parts; issue order weights-then-strip (PH 0, 1), strip-then-weights
+      // (PH 2) so each counted wait below retires exactly what the next step reads
+      if constexpr (PH == 0) {
+        issue_w(2, koff_cur + 2 * cin2);
+        if constexpr (STEADY) issue_s(GP ^ 1, ncb, Z{}, K0{});
+      } else if constexpr (STEADY && PH == 1) {
+        issue_w(0, koff_next);
+        issue_s(GP ^ 1, ncb, K0{}, K1{});
+      } else if constexpr (STEADY && PH == 2) {
+        issue_s(GP ^ 1, ncb, K1{}, KS{});
+        issue_w(1, koff_next + cin2);
+      }
     }
     uint4 af[2][WC], bfr[2][WP];
 #pragma unroll
@@ -1054,8 +1075,8 @@ __global__ void __launch_bounds__(512) k_conv_strip2(const zp_conv_args A, const
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     auto wait_out = [&]() {
-      if constexpr (PH == 0) vm_wait<WPW>();
-      else if constexpr (STEADY && PH == 1) vm_wait<WPW + SPW>();
+      if constexpr (PH == 0) vm_wait<WPW + (SPREAD && STEADY ? N0 : 0)>();
+      else if constexpr (STEADY && PH == 1) vm_wait<WPW + (SPREAD ? N0 + N1 : SPW)>();
       else if constexpr (STEADY && PH == 2) vm_wait<WPW>();
       else vm_wait<0>();
     };
@@ -1113,7 +1134,7 @@ __global__ void __launch_bounds__(512) k_conv_strip2(const zp_conv_args A, const
   };
   // prologue: strip of group 0, weights of steps 0 and 1
   set_svn(0);
-  issue_s(0, 0);
+  issue_s(0, 0, std::integral_constant<int, 0>{}, std::integral_constant<int, SPW>{});
   issue_w(0, 0);
   issue_w(1, cin2);
   vm_wait<WPW>();
@@ -1596,6 +1617,219 @@ __global__ void __launch_bounds__(512) k_wgrad_lds(const zp_wgrad_args A, float*
     }
 }
 
+// ------------------------------------------------------------------------------------
+// k_wgrad2: k_wgrad_lds's product (same tiles, same panels, same fragment reads, same partial
+// layout) with a lean issue path for the common geometry: one sub-problem, stride 1, dy on the
+// input grid (same-size convs: every 3x3 d-conv and 1x1 of the network), W in {32, 64, 128},
+// images a multiple of the 64-pixel step, Cin and the dy channel slice 64-aligned.  Then the
+// pixel offset of a lane's row in dy and x is LINEAR in the pixel index: the per-step offset is
+// one scalar (p * ld * 2) added by the buffer unit; per lane only constant row / channel /
+// tap offsets are kept, and a tap's row validity is wave-uniform per step (a 64-pixel step is
+// one image row at W 64, half a row at W 128, two rows at W 32 whose halves are waves 0-3 and
+// 4-7), its column validity a per-lane constant (W 128: one of two).  k_wgrad_lds, profiled on
+// the 256->256 3x3 at 128x128 (bs 32), spent 1.4 VALU + 1.0 SALU per MFMA on per-step pixel
+// arithmetic and ran the MFMA pipe 34% busy.
+// ------------------------------------------------------------------------------------
+template <int NA, int NB, int STAGES, int WN>
+__global__ void __launch_bounds__(512) k_wgrad2(const zp_wgrad_args A, float* __restrict__ ws, int pix_per_split,
+                                                int col_tiles, int tiles_per_sub, int cols_max, const wg_bounds WB) {
+  constexpr int KP = 64;
+  static_assert(NA * NB == 8 * WN, "8 waves of 64 x (64 WN)");
+  constexpr int NBW = NB / WN;
+  constexpr int NP = NA + NB;   // panels per stage; wave w fills rows 8w..8w+7 of every panel
+  constexpr int PB = KP * 128;  // panel bytes
+  constexpr int SB = NP * PB;   // stage bytes
+  static_assert(SB * STAGES <= 160 * 1024, "LDS");
+  __shared__ uint4 lds[STAGES * SB / 16];
+
+  const int total = gridDim.x;
+  const int bid = blockIdx.x;
+  const int lin = (total & 7) ? bid : (bid & 7) * (total >> 3) + (bid >> 3);
+  const int tile = lin % tiles_per_sub;
+  const int split = lin / tiles_per_sub;  // one sub-problem
+  const auto& S = A.sub[0];
+  const int cols = S.ntaps * A.Cin;
+  const int ct = tile % col_tiles, cot = tile / col_tiles;
+  const int col0 = ct * 64 * NB, co0 = cot * 64 * NA;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wa = wid / NBW, wb = wid % NBW;
+  const int W = A.GW, GHW = A.GH * A.GW;
+  const int M = A.N * GHW;
+  const int pbeg = split * pix_per_split;
+  const int pend = min(M, pbeg + pix_per_split);
+  const int nK = pend > pbeg ? (pend - pbeg) / KP : 0;
+
+  const int R = wid * 8 + (lane >> 3);  // this lane's pixel row within a step
+  const int lchunk = (lane & 7) ^ wg_swz(R);
+  const int cout8 = (A.Cout + 7) & ~7;
+  const int rh = W == 32 ? (wid >> 2) : 0;  // image-row offset of this wave's rows (wave-uniform)
+  const int gxl = W == 32 ? (R & 31) : R;   // column (W 128: + 64 * xh)
+  // per panel: lane offsets (dy: row + channel; x: row + tap + channel, with column validity folded
+  // in as an out-of-range offset), tap row of x panels (wave-uniform)
+  unsigned vdy[NA];
+  int vx[NB];                // x: row + tap + channel offset (bytes; may be negative, the step adds p)
+  bool okx0[NB], okx1[NB];   // column validity (W 128: column half 0 / 1)
+  int tyP[NB];
+#pragma unroll
+  for (int P = 0; P < NA; ++P) {
+    const int ch = co0 + 64 * P + 8 * lchunk;
+    vdy[P] = ch < cout8 ? (unsigned)((R * S.lddy + S.cdy0 + ch) * 2) : 0x80000000u;
+  }
+#pragma unroll
+  for (int P = 0; P < NB; ++P) {
+    const int col = col0 + 64 * P + 8 * lchunk;
+    const bool ok = col < cols;
+    const int t = ok ? col / A.Cin : 0;
+    const int ci = col - t * A.Cin;
+    const int ty = S.ty[t], tx = S.tx[t];
+    tyP[P] = __builtin_amdgcn_readfirstlane(S.ty[(col0 + 64 * P) / A.Cin < S.ntaps ? (col0 + 64 * P) / A.Cin : 0]);
+    vx[P] = (R + ty * A.IW + tx) * A.ldx * 2 + (A.cx0 + ci) * 2;
+    okx0[P] = ok && (unsigned)(gxl + tx) < (unsigned)W;
+    okx1[P] = ok && (unsigned)(gxl + 64 + tx) < (unsigned)W;
+  }
+#if defined(__HIP_DEVICE_COMPILE__)
+  const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)A.x, (short)0, (int)WB.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t drsrc = __builtin_amdgcn_make_buffer_rsrc((void*)S.dy, (short)0, (int)WB.dy_bytes[0], 0x00020000);
+#endif
+  // scalar walk: pixel p of the next step to issue, its image row gy and (W 128) column half xh
+  int p_is = pbeg;
+  int gy_is, xh_is;
+  {
+    const int r = pbeg % GHW;
+    gy_is = r / W;
+    xh_is = W == 128 ? (r / 64) & 1 : 0;
+  }
+  const int ldy2 = S.lddy * 2, ldx2 = A.ldx * 2;
+  auto issue = [&](auto slot_c) {
+    constexpr int SL = decltype(slot_c)::value;
+    const int sdy = p_is * ldy2, sx = p_is * ldx2;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+    for (int P = 0; P < NA; ++P) {
+      auto* d = (__attribute__((address_space(3))) void*)((unsigned char*)lds + SL * SB + P * PB + wid * 1024);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(drsrc, d, 16, vdy[P], sdy, 0, 0);
+    }
+#pragma unroll
+    for (int P = 0; P < NB; ++P) {
+      // the full (non-negative when valid) offset in the VGPR: a lane offset below zero is never
+      // handed to the buffer unit, whatever its range check does with the scalar part
+      const bool rowok = (unsigned)(gy_is + rh + tyP[P]) < (unsigned)A.IH;  // wave-uniform
+      const bool ok = rowok && (xh_is ? okx1[P] : okx0[P]);
+      const unsigned v = ok ? (unsigned)(vx[P] + sx) : 0x80000000u;
+      auto* d = (__attribute__((address_space(3))) void*)((unsigned char*)lds + SL * SB + (NA + P) * PB + wid * 1024);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrsrc, d, 16, v, 0, 0, 0);
+    }
+#endif
+    // advance one 64-pixel step (images are whole steps: GHW % 64 == 0)
+    p_is += KP;
+    if (W == 128) {
+      xh_is ^= 1;
+      if (xh_is == 0) ++gy_is;
+    } else {
+      gy_is += KP / W;
+    }
+    if (gy_is >= A.GH) gy_is = 0;
+  };
+
+  f32x4 acc[4][4 * WN];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4 * WN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+  const int sh = (((q4 >> 1) & 1) | ((g & 1) << 1));
+  const unsigned l0 = lds_addr(lds);
+  unsigned pa[STAGES][4], pb[STAGES][4];  // per ring slot (slot offsets exceed the ds immediate)
+#pragma unroll
+  for (int sl = 0; sl < STAGES; ++sl)
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) {
+      pa[sl][ii] = l0 + (unsigned)(sl * SB + wa * PB) + (unsigned)(128 * (8 * g + q4) + 8 * p4 + 32 * (ii ^ sh));
+      pb[sl][ii] = pa[sl][ii] + (unsigned)((NA + wb * WN - wa) * PB);
+    }
+  auto step = [&](auto cur_c, auto nxt_c, int ks) {
+    constexpr int CUR = decltype(cur_c)::value;
+    const bool more = ks + (STAGES - 1) < nK;
+    if constexpr (ZP_ABL != 1) {
+      if (more) issue(nxt_c);
+    }
+    static_for<KP / 32>([&](auto s2) {
+      uint4 af[4], bfr[4 * WN];
+      static_for<4>([&](auto ii) {
+        const uint2 a0 = ds_read_tr8<s2 * 4096>(pa[CUR][ii]);
+        const uint2 a1 = ds_read_tr8<s2 * 4096 + 512>(pa[CUR][ii]);
+        af[ii] = make_uint4(a0.x, a0.y, a1.x, a1.y);
+        static_for<WN>([&](auto w) {
+          const uint2 b0 = ds_read_tr8<w * PB + s2 * 4096>(pb[CUR][ii]);
+          const uint2 b1 = ds_read_tr8<w * PB + s2 * 4096 + 512>(pb[CUR][ii]);
+          bfr[w * 4 + ii] = make_uint4(b0.x, b0.y, b1.x, b1.y);
+        });
+      });
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+      if constexpr (ZP_ABL != 2) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4 * WN; ++j) MfmaTraits<bf16_t>::mma(acc[i][j], af[i], bfr[j]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i][0][0] += __uint_as_float(af[i].x ^ bfr[i].y);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(0);
+    });
+    if (more) vm_wait<NP * (STAGES - 2)>();
+    else vm_wait<0>();
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  if (nK > 0) {
+    issue(I0{});
+    if (STAGES == 3 && nK > 1) {
+      issue(I1{});
+      vm_wait<NP * (STAGES - 2)>();
+    } else {
+      vm_wait<0>();
+    }
+  }
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  if constexpr (STAGES == 3) {
+    for (int ks = 0; ks < nK; ks += 3) {
+      step(I0{}, I2{}, ks);
+      if (ks + 1 >= nK) break;
+      step(I1{}, I0{}, ks + 1);
+      if (ks + 2 >= nK) break;
+      step(I2{}, I1{}, ks + 2);
+    }
+  } else {
+    for (int ks = 0; ks < nK; ks += 2) {
+      step(I0{}, I1{}, ks);
+      if (ks + 1 >= nK) break;
+      step(I1{}, I0{}, ks + 1);
+    }
+  }
+  float* Wp = ws + (size_t)split * (size_t)A.Cout * cols_max;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4 * WN; ++j) {
+      const int col = col0 + wb * WN * 64 + j * 16 + (lane & 15);
+      if (col >= cols) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + wa * 64 + i * 16 + g * 4 + r;
+        if (co < A.Cout) Wp[(size_t)co * cols_max + col] = acc[i][j][r];
+      }
+    }
+}
+
 // ws (summed over splits) -> dw in the weight's own layout
 __global__ void k_wgrad_reduce(const zp_wgrad_args A, const float* __restrict__ ws, int splits, int cols_max) {
   const int sub = blockIdx.y;
@@ -1669,11 +1903,13 @@ static int g_tc256_min_blocks = 1024;
 // workgroups: 78.7 us vs 70.7 us on the 128-channel tile) and on the ASPP launch, whose four
 // sub-problems (1 vs 9 taps) are too unbalanced for 512 large tiles.
 static bool strip_eligible(const zp_conv_args& a, strip_geo* sg);
+static int g_strip_c64 = 1;  // zp_conv_tuning key 2: 64-channel layers on the strip kernel (TC 64; 27.5 -> 22.2 us at 64x64)
 // strip tile width: 128 channels, or 64 when 128-channel tiles would leave part of the 256 CUs
 // idle (128 -> 128 at 32x32, bs 32: 128 workgroups; 24.2 -> 22.7 us).  64-channel layers stay on
 // k_conv's 128-pixel tiles (27.5 us there vs 29.2 us as a 64-channel strip).
 static int strip_tc(const zp_conv_args& a) {
   static const int en64 = getenv("ZP_STRIP_TC64") ? env_int("ZP_STRIP_TC64") : 1;
+  if (a.Cout <= 64) return 64;
   if (!en64) return 128;
   const long tiles = (long)a.N * a.GH * a.GW / 256;
   if (tiles * ((a.Cout + 127) / 128) < 256) return 64;
@@ -1721,7 +1957,8 @@ static int conv_flags() {
 // ZP_CONV_STRIP=0 disables.
 static bool strip_eligible(const zp_conv_args& a, strip_geo* sg) {
   static const int en = getenv("ZP_CONV_STRIP") ? env_int("ZP_CONV_STRIP") : 1;
-  if (!en || a.dtype == ZP_F32 || a.nsub != 1 || a.Cin % 64 != 0 || a.Cout % 64 != 0 || a.Cout <= 64) return false;
+  if (!en || a.dtype == ZP_F32 || a.nsub != 1 || a.Cin % 64 != 0 || a.Cout % 64 != 0) return false;
+  if (a.Cout <= 64 && !g_strip_c64) return false;
   if (a.sy != 1 || a.sx != 1 || a.GH != a.IH || a.GW != a.IW) return false;
   const zp_conv_sub& S = a.sub[0];
   if (S.ntaps != 9 || S.oys != 1 || S.oxs != 1 || S.oyo != 0 || S.oxo != 0 || S.OH != a.GH || S.OW != a.GW)
@@ -1870,14 +2107,16 @@ extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
                  "zp_conv2d: strip launch emits %d stat parts, zp_conv2d_stat_parts says %d", 4 * sgx,
                  zp_conv2d_stat_parts(&a));
     const int fl = conv_flags();
-    if (fl & 64) {  // k_conv_strip2 (lean main loop)
+    if (fl & 64) {  // k_conv_strip2 (lean main loop); flags & 32: strip DMA spread over the group
+#define ZP_STRIP2(T, WC)                                                                              \
+  if (fl & 32) hipLaunchKernelGGL((k_conv_strip2<T, WC, 5, true>), grid, dim3(512), 0, st, a, sg, fl); \
+  else hipLaunchKernelGGL((k_conv_strip2<T, WC, 5, false>), grid, dim3(512), 0, st, a, sg, fl);
       if (a.dtype == ZP_F16) {
-        if (tc == 64) hipLaunchKernelGGL((k_conv_strip2<f16_t, 2, 5>), grid, dim3(512), 0, st, a, sg, fl);
-        else hipLaunchKernelGGL((k_conv_strip2<f16_t, 4, 5>), grid, dim3(512), 0, st, a, sg, fl);
+        if (tc == 64) { ZP_STRIP2(f16_t, 2) } else { ZP_STRIP2(f16_t, 4) }
       } else {
-        if (tc == 64) hipLaunchKernelGGL((k_conv_strip2<bf16_t, 2, 5>), grid, dim3(512), 0, st, a, sg, fl);
-        else hipLaunchKernelGGL((k_conv_strip2<bf16_t, 4, 5>), grid, dim3(512), 0, st, a, sg, fl);
+        if (tc == 64) { ZP_STRIP2(bf16_t, 2) } else { ZP_STRIP2(bf16_t, 4) }
       }
+#undef ZP_STRIP2
     } else if (a.dtype == ZP_F16) {
       if (tc == 64) hipLaunchKernelGGL((k_conv_strip<f16_t, 2, 3, 5>), grid, dim3(512), 0, st, a, sg, fl);
       else hipLaunchKernelGGL((k_conv_strip<f16_t, 4, 3, 5>), grid, dim3(512), 0, st, a, sg, fl);
@@ -1962,6 +2201,17 @@ static int wgrad_cfg(const zp_wgrad_args& a) {
   if (a.Cout >= 256 && big) return 2;
   return 1;
 }
+// k_wgrad2 (lean issue path) for the common geometry -- see the kernel's header comment.
+// zp_conv_tuning key 3: 0 disables it; key 4: its target workgroup count (fewer, longer
+// workgroups than k_wgrad_lds's 1024: the split-K partial slabs are written and re-read in full).
+static int g_wgrad2 = 1, g_wgrad2_target = 512;
+static bool wgrad2_eligible(const zp_wgrad_args& a) {
+  if (!g_wgrad2 || a.dtype != ZP_BF16 || a.nsub != 1 || a.sy != 1 || a.sx != 1) return false;
+  if (a.IH != a.GH || a.IW != a.GW || (a.GW != 32 && a.GW != 64 && a.GW != 128)) return false;
+  if (((long)a.GH * a.GW) % 64 != 0 || a.Cin % 64 != 0) return false;
+  const auto& S = a.sub[0];
+  return S.oys == 1 && S.oxs == 1 && S.oyo == 0 && S.oxo == 0 && S.OH == a.GH && S.OW == a.GW;
+}
 static void wgrad_plan_lds(const zp_wgrad_args& a, int* splits, int* col_tiles, int* cols_max, int* pix_per) {
   long M = (long)a.N * a.GH * a.GW;
   int cm = 0;
@@ -1972,7 +2222,8 @@ static void wgrad_plan_lds(const zp_wgrad_args& a, int* splits, int* col_tiles, 
   int tiles = ct * ceil_div(a.Cout, tco) * a.nsub;
   // target workgroup count: 1024 (R34 bs 32 train step 19.93 -> 19.71 ms vs 512; 2048: 19.81).
   // ZP_WGRAD_WG overrides for sweeps (read once, so the workspace size query agrees)
-  static const int target = getenv("ZP_WGRAD_WG") ? env_int("ZP_WGRAD_WG") : 1024;
+  static const int target_lds = getenv("ZP_WGRAD_WG") ? env_int("ZP_WGRAD_WG") : 1024;
+  const int target = wgrad2_eligible(a) ? g_wgrad2_target : target_lds;
   long sp = (target + tiles - 1) / tiles;
   long maxsp = M / (16 * KP);
   if (maxsp < 1) maxsp = 1;
@@ -2026,7 +2277,15 @@ extern "C" int zp_conv2d_wgrad(const zp_wgrad_args* ap, void* ws, void* stream) 
       wb.dy_bytes[s] = (unsigned)db;
     }
     const int cfg = wgrad_cfg(a);
-    if (cfg == 0) {
+    if (wgrad2_eligible(a)) {
+      const int tiles = ct * ceil_div(a.Cout, cfg == 0 ? 64 : (cfg == 1 ? 128 : 256));
+      if (cfg == 0)
+        hipLaunchKernelGGL((k_wgrad2<1, 8, 2, 1>), dim3(sp * tiles), dim3(512), 0, st, a, (float*)ws, pp, ct, tiles, cm, wb);
+      else if (cfg == 1)
+        hipLaunchKernelGGL((k_wgrad2<2, 4, 3, 1>), dim3(sp * tiles), dim3(512), 0, st, a, (float*)ws, pp, ct, tiles, cm, wb);
+      else
+        hipLaunchKernelGGL((k_wgrad2<4, 4, 2, 2>), dim3(sp * tiles), dim3(512), 0, st, a, (float*)ws, pp, ct, tiles, cm, wb);
+    } else if (cfg == 0) {
       const int tiles = ct * ceil_div(a.Cout, 64);
       hipLaunchKernelGGL((k_wgrad_lds<64, 1, 8, 2, 1>), dim3(sp * a.nsub * tiles), dim3(512), 0, st, a, (float*)ws,
                          pp, ct, tiles, cm, wb);
@@ -2072,8 +2331,9 @@ extern "C" int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* st
 }
 
 /* runtime tuning knobs (tests / sweeps).  key 0: minimum workgroups for the 256-channel conv tile
- * (default 1024); key 1: conv schedule flags (-1 = ZP_CONV_FLAGS / default).  Returns the previous
- * value. */
+ * (default 1024); key 1: conv schedule flags (-1 = ZP_CONV_FLAGS / default); key 2: 64-channel
+ * layers on the strip kernel (default 1); key 3: k_wgrad2 (default 1); key 4: k_wgrad2's target
+ * workgroup count (default 512).  Returns the previous value. */
 extern "C" int zp_conv_tuning(int key, int value) {
   if (key == 0) {
     const int old = g_tc256_min_blocks;
@@ -2083,6 +2343,21 @@ extern "C" int zp_conv_tuning(int key, int value) {
   if (key == 1) {
     const int old = g_conv_flags;
     g_conv_flags = value;
+    return old;
+  }
+  if (key == 2) {
+    const int old = g_strip_c64;
+    g_strip_c64 = value;
+    return old;
+  }
+  if (key == 3) {
+    const int old = g_wgrad2;
+    g_wgrad2 = value;
+    return old;
+  }
+  if (key == 4) {
+    const int old = g_wgrad2_target;
+    g_wgrad2_target = value > 0 ? value : 512;
     return old;
   }
   return -1;
