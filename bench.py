@@ -414,14 +414,15 @@ def run(args):
     eng.timing = None
     # group launches by kernel instantiation (the names rocprofv3 reports)
     for rec in eng_t:
-        label, e0, e1, flops, kname = rec
-        d = per.setdefault(kname, [0.0, 0.0, 0])
+        label, e0, e1, flops, kname, nbytes = rec
+        d = per.setdefault(kname, [0.0, 0.0, 0, 0.0])
         d[0] += flops
         d[1] += e0.elapsed_time(e1) * 1e-3
         d[2] += 1
+        d[3] += nbytes
     if args.layer_report and rank == 0:
         lay = {}
-        for label, e0, e1, flops, kname in eng_t:
+        for label, e0, e1, flops, kname, _ in eng_t:
             d = lay.setdefault(label, [kname, 0.0, 0.0, 0])
             d[1] += e0.elapsed_time(e1) * 1e3
             d[2] += flops
@@ -431,19 +432,25 @@ def run(args):
         with open(args.layer_report, "w") as f:
             json.dump(rows, f, indent=0)
     dom = max(per.items(), key=lambda kv: kv[1][1])
-    kname, (fl, tsec, nl) = dom
+    kname, (fl, tsec, nl, algo_bytes) = dom
     achieved = fl / tsec / 1e12
     traffic = None
     # HBM bytes per launch of this kernel instance from the committed PMC passes (rocprofv3 cannot
     # run inside this process): tools/prof_round.sh + tools/prof_summary.py -> profiles/<tag>_pmc_traffic.json
-    pmc = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
-    if pmc:
-        with open(pmc[-1]) as fh:
+    traffic_src = None
+    for pf in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")), reverse=True):
+        with open(pf) as fh:
             traffic = json.load(fh).get("by_label", {}).get(kname)
-    all_conv_flops = sum(v[0] for v in per.values())
+        if traffic is not None:
+            traffic_src = os.path.relpath(pf, ROOT)
+            break
+    all_conv_flops = sum(v[0] for v in per.values())  # noqa
     all_conv_time = sum(v[1] for v in per.values())
+    algo_per_launch = algo_bytes / nl
     roofline = {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 2), "peak": PEAK[args.precision],
                 "unit": "TFLOP/s", "frac": round(achieved / PEAK[args.precision], 4), "traffic": traffic,
+                "traffic_source": traffic_src, "algorithmic_bytes_per_launch": round(algo_per_launch),
+                "traffic_over_algorithmic": None if traffic is None else round(traffic / algo_per_launch, 3),
                 "launches_per_step": nl // args.steps, "avg_launch_us": round(tsec / nl * 1e6, 2),
                 "all_conv_tflops": round(all_conv_flops / all_conv_time / 1e12, 2),
                 "whole_step_tflops": round(FWD_GFLOP_PER_CROP * 1e9 * B / (ms_per_step * 1e-3) / 1e12, 2)}

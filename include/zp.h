@@ -114,7 +114,7 @@ int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* stages, int* 
 /* runtime tuning knobs (tests / sweeps): key 0 = minimum workgroup count for the 256-channel
  * tile (default 1024); key 1 = conv schedule flags (-1 = ZP_CONV_FLAGS or the default); key 2 =
  * 64-channel layers on the strip kernel (default 1); key 3 = the lean weight-gradient kernel
- * (default 1); key 4 = its target workgroup count (default 512).  Returns the previous value, -1
+ * (default 1); key 4 = its workgroup rounds over the CUs (default 1).  Returns the previous value, -1
  * for an unknown key. */
 int zp_conv_tuning(int key, int value);
 

@@ -43,8 +43,8 @@ def main():
         L.lib.zp_conv_tuning(2, 0 if "noc64" in parts[1:] else 1)
         L.lib.zp_conv_tuning(0, 1 << 30 if "no256" in parts[1:] else (1 if "all256" in parts[1:] else 1024))
         L.lib.zp_conv_tuning(3, 0 if "now2" in parts[1:] else 1)
-        tg = [int(q[1:]) for q in parts[1:] if q.startswith("t") and q[1:].isdigit()]
-        L.lib.zp_conv_tuning(4, tg[0] if tg else 512)
+        tg = [int(q[1:]) for q in parts[1:] if q.startswith("r") and q[1:].isdigit()]
+        L.lib.zp_conv_tuning(4, tg[0] if tg else 1)
     rows = []
     for spec in a.layers.split(","):
         tr = spec.startswith("T")  # T<cin>:<cout>:<hw>: ConvTranspose2d(3, s2, p1, op1) (aspp.py:60-80)
@@ -109,7 +109,7 @@ def main():
         L.lib.zp_conv_tuning(2, 1)
         L.lib.zp_conv_tuning(0, 1024)
         L.lib.zp_conv_tuning(3, 1)
-        L.lib.zp_conv_tuning(4, 512)
+        L.lib.zp_conv_tuning(4, 1)
         for fv in flags:
             med, mn = float(np.median(times[fv])), float(np.min(times[fv]))
             row = {"layer": spec, "flags": fv, "us_median": round(med, 2), "us_min": round(mn, 2),

@@ -71,7 +71,7 @@ def main():
         ts(x, gt_code, gt_mask)
         torch.cuda.synchronize()
         lay = {}
-        for label, e0, e1, flops, kname in eng.timing:
+        for label, e0, e1, flops, kname, _ in eng.timing:
             d = lay.setdefault(label, [kname, 0.0, 0.0, 0])
             d[1] += e0.elapsed_time(e1) * 1e3
             d[2] += flops

@@ -1642,9 +1642,12 @@ __global__ void __launch_bounds__(512) k_wgrad2(const zp_wgrad_args A, float* __
   static_assert(SB * STAGES <= 160 * 1024, "LDS");
   __shared__ uint4 lds[STAGES * SB / 16];
 
+  // XCD-aware order (bijective for any total): each XCD walks a contiguous run of (split, tile),
+  // tiles fastest, so the tiles of one split (same dy / x pixel rows) share an L2
   const int total = gridDim.x;
   const int bid = blockIdx.x;
-  const int lin = (total & 7) ? bid : (bid & 7) * (total >> 3) + (bid >> 3);
+  const int xcd = bid & 7, pos = bid >> 3, q8 = total >> 3, r8 = total & 7;
+  const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + pos;
   const int tile = lin % tiles_per_sub;
   const int split = lin / tiles_per_sub;  // one sub-problem
   const auto& S = A.sub[0];
@@ -2202,9 +2205,20 @@ static int wgrad_cfg(const zp_wgrad_args& a) {
   return 1;
 }
 // k_wgrad2 (lean issue path) for the common geometry -- see the kernel's header comment.
-// zp_conv_tuning key 3: 0 disables it; key 4: its target workgroup count (fewer, longer
-// workgroups than k_wgrad_lds's 1024: the split-K partial slabs are written and re-read in full).
-static int g_wgrad2 = 1, g_wgrad2_target = 512;
+// zp_conv_tuning key 3: 0 disables it; key 4: its workgroup rounds over the CUs (default 1: fewer,
+// longer workgroups than k_wgrad_lds's 1024 -- the split-K partial slabs are written and re-read
+// in full -- and never a partial extra round; one round measured fastest).
+static int g_wgrad2 = 1, g_wgrad2_rounds = 1;
+static int num_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n <= 0)
+      n = 256;
+  }
+  return n;
+}
 static bool wgrad2_eligible(const zp_wgrad_args& a) {
   if (!g_wgrad2 || a.dtype != ZP_BF16 || a.nsub != 1 || a.sy != 1 || a.sx != 1) return false;
   if (a.IH != a.GH || a.IW != a.GW || (a.GW != 32 && a.GW != 64 && a.GW != 128)) return false;
@@ -2223,18 +2237,22 @@ static void wgrad_plan_lds(const zp_wgrad_args& a, int* splits, int* col_tiles, 
   // target workgroup count: 1024 (R34 bs 32 train step 19.93 -> 19.71 ms vs 512; 2048: 19.81).
   // ZP_WGRAD_WG overrides for sweeps (read once, so the workspace size query agrees)
   static const int target_lds = getenv("ZP_WGRAD_WG") ? env_int("ZP_WGRAD_WG") : 1024;
-  const int target = wgrad2_eligible(a) ? g_wgrad2_target : target_lds;
-  long sp = (target + tiles - 1) / tiles;
+  const bool lean = wgrad2_eligible(a);
+  // k_wgrad2: workgroups (one per CU at a time: 96-144 KB of LDS) in whole rounds over the CUs --
+  // a grid one workgroup past a round costs a full extra workgroup lifetime (513 vs 512 ran 1.6x)
+  long sp = lean ? (long)g_wgrad2_rounds * num_cus() / tiles : (target_lds + tiles - 1) / tiles;
+  if (sp < 1) sp = 1;
   long maxsp = M / (16 * KP);
   if (maxsp < 1) maxsp = 1;
   if (sp > maxsp) sp = maxsp;
   if (sp > 256) sp = 256;
   long pp = (M + sp - 1) / sp;
   pp = (pp + KP - 1) / KP * KP;
-  sp = (M + pp - 1) / pp;
-  // pad the split count so the launch is a multiple of 8 workgroups (the XCD-aware order
-  // needs it); padding splits have an empty pixel range and write zero partials
-  while ((sp * tiles) % 8) ++sp;
+  sp = (M + pp - 1) / pp;  // never more than requested: pp only grew
+  // k_wgrad_lds: pad the split count so the launch is a multiple of 8 workgroups (its XCD-aware
+  // order needs it); padding splits have an empty pixel range and write zero partials
+  if (!lean)
+    while ((sp * tiles) % 8) ++sp;
   *splits = (int)sp;
   *col_tiles = ct;
   *cols_max = cm;
@@ -2332,8 +2350,8 @@ extern "C" int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* st
 
 /* runtime tuning knobs (tests / sweeps).  key 0: minimum workgroups for the 256-channel conv tile
  * (default 1024); key 1: conv schedule flags (-1 = ZP_CONV_FLAGS / default); key 2: 64-channel
- * layers on the strip kernel (default 1); key 3: k_wgrad2 (default 1); key 4: k_wgrad2's target
- * workgroup count (default 512).  Returns the previous value. */
+ * layers on the strip kernel (default 1); key 3: k_wgrad2 (default 1); key 4: k_wgrad2's
+ * workgroup rounds over the CUs (default 1).  Returns the previous value. */
 extern "C" int zp_conv_tuning(int key, int value) {
   if (key == 0) {
     const int old = g_tc256_min_blocks;
@@ -2356,8 +2374,8 @@ extern "C" int zp_conv_tuning(int key, int value) {
     return old;
   }
   if (key == 4) {
-    const int old = g_wgrad2_target;
-    g_wgrad2_target = value > 0 ? value : 512;
+    const int old = g_wgrad2_rounds;
+    g_wgrad2_rounds = value > 0 ? value : 1;
     return old;
   }
   return -1;

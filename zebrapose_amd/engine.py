@@ -242,7 +242,14 @@ class Engine:
                          f"NWP={tp.value // 64},ST={stages.value},smallC={int(x.C < _KE[self.dt])}>")
             geo = (f"{label}:{x.C}->{cout} taps{max(len(sb.taps) for sb in plan.subs)} "
                    f"{x.H}x{x.W}->{plan.GH}x{plan.GW}x{a.nsub}")
-            self.timing.append((geo, e0, e1, flops, kname))
+            # algorithmic HBM bytes: the input slice and every output read / written once, the
+            # packed weights of each sub-problem once (the residual, when fused, read once)
+            es = 4 if self.dt == L.ZP_F32 else 2
+            osz = 4 if out_mode == L.ZP_OUT_HEAD_NCHW else es
+            mgrid = x.B * plan.GH * plan.GW
+            nbytes = (x.P * x.C * es + len(plan.subs) * mgrid * cout * osz
+                      + sum(w.numel() * w.element_size() for w in weights) + (0 if res is None else mgrid * cout * es))
+            self.timing.append((geo, e0, e1, flops, kname, nbytes))
         else:
             L.check(L.lib.zp_conv2d(C.byref(a), st), "zp_conv2d")
         return stats, parts
@@ -402,7 +409,7 @@ class Engine:
             flops = 2.0 * x.B * plan.GH * plan.GW * sum(len(sb.taps) for sb in plan.subs) * x.C * unit.cout
             geo = (f"wgrad:{x.C}->{unit.cout} taps{max(len(sb.taps) for sb in plan.subs)} "
                    f"{x.H}x{x.W}->{plan.GH}x{plan.GW}x{a.nsub}")
-            self.timing.append((geo, e0, e1, flops, "k_wgrad+reduce"))
+            self.timing.append((geo, e0, e1, flops, "k_wgrad+reduce", 0))
             return
         L.check(L.lib.zp_conv2d_wgrad(C.byref(a), ws.data_ptr(), L.stream_ptr()), "zp_conv2d_wgrad")
 
