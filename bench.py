@@ -439,6 +439,8 @@ def run(args):
     # run inside this process): tools/prof_round.sh + tools/prof_summary.py -> profiles/<tag>_pmc_traffic.json
     traffic_src = None
     for pf in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")), reverse=True):
+        if "_train_" in os.path.basename(pf):  # the eval (folded-BN) launches are the ones timed here
+            continue
         with open(pf) as fh:
             traffic = json.load(fh).get("by_label", {}).get(kname)
         if traffic is not None:

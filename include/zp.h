@@ -114,7 +114,8 @@ int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* stages, int* 
 /* runtime tuning knobs (tests / sweeps): key 0 = minimum workgroup count for the 256-channel
  * tile (default 1024); key 1 = conv schedule flags (-1 = ZP_CONV_FLAGS or the default); key 2 =
  * 64-channel layers on the strip kernel (default 1); key 3 = the lean weight-gradient kernel
- * (default 1); key 4 = its workgroup rounds over the CUs (default 1).  Returns the previous value, -1
+ * (default 1); key 4 = its workgroup rounds over the CUs (default 1); key 5 = the general
+ * weight-gradient kernel's workgroup rounds (default 1; 0 = a ~1024-workgroup target).  Returns the previous value, -1
  * for an unknown key. */
 int zp_conv_tuning(int key, int value);
 
@@ -171,26 +172,30 @@ int zp_bn_fold(const float* gamma, const float* beta, const float* mean, const f
                const float* conv_bias, float eps, int C, float* scale, float* shift, void* stream);
 /* train: merge the [3][parts][C] partial statistics of zp_conv2d(stats) (count = P, checked),
  * update running stats (momentum, unbiased var; the conv bias, if any, is added to the mean)
- * and emit scale/shift for the apply pass, plus save[2][C] = (mean, invstd) of the raw values.
+ * and emit scale/shift for the apply pass, plus save[4][C] = (mean, invstd, scale, shift) of the
+ * raw values (shift = fma(-mean, scale, beta)).
  * partials is scratch: a first merge level overwrites it in place (every 64th part). */
 int zp_bn_train_finalize(float* partials, int parts, int C, long long count, float eps,
                          float momentum, const float* gamma, const float* beta, const float* conv_bias,
                          float* running_mean, float* running_var, int64_t* num_batches_tracked,
                          float* scale, float* shift, float* save, void* stream);
-/* y[p, cy0+c] = act(x[p, c]*scale[c] + shift[c] (+ res[p, cr0+c])), x: raw conv output [P][C] */
+/* y[p, cy0+c] = act(fma(x[p, c], scale[c], shift[c]) (+ res[p, cr0+c])), x: raw conv output [P][C] */
 int zp_bn_apply(const void* x, int P, int C, const float* scale, const float* shift,
                 const void* res, int ldr, int cr0, int relu, int dtype, void* y, int ldy, int cy0,
                 void* stream);
 /* number of partial slots zp_bn_bwd_reduce uses for P pixels (partials needs [2][parts+1][C]) */
 int zp_bn_bwd_parts(int P, int C);
-/* backward of y = act(bn(x) (+res)):  g = dy * (y > 0 if relu);  xhat = (x - mean) * invstd;
+/* backward of y = act(bn(x) (+res)):  g = dy * mask;  xhat = (x - mean) * invstd;
+ * relu 0: no mask; 1: mask = y > 0 (y read); 2: mask = fma(x, save scale, save shift) > 0, recomputed
+ * from the raw x exactly as zp_bn_apply formed y (no residual) -- y is not read and may be NULL;
  * partials[0][k][c] = sum g, partials[1][k][c] = sum g*xhat over pixel block k (x == NULL: only sum g);
  * then totals into partials[.][parts][c] and (optional) dgamma = sum g*xhat, dbeta = sum g
  * (written, or added if accumulate). */
 int zp_bn_bwd_reduce(const void* dy, int lddy, int cdy0, const void* y, int ldy, int cy0,
                      const void* x, int P, int C, const float* save, int relu, int dtype,
                      float* partials, float* dgamma, float* dbeta, int accumulate, void* stream);
-/* dx[p][c] = gamma*invstd*(g - sum_g/P - xhat*sum_gx/P)  (dx dtype, [P][C]);
+/* dx[p][c] = gamma*invstd*(g - sum_g/P - xhat*sum_gx/P)  (dx dtype, [P][C]); relu as for the
+ * reduce (mode 2 needs dx);
  * dres (optional) [p, cdres0+c] = g, or += g if res_accumulate */
 int zp_bn_bwd_apply(const void* dy, int lddy, int cdy0, const void* y, int ldy, int cy0,
                     const void* x, int P, int C, const float* save, const float* partials,

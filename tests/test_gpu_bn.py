@@ -1,0 +1,67 @@
+"""Train-mode BatchNorm backward through the C-ABI (zp_bn_apply / zp_bn_bwd_reduce / zp_bn_bwd_apply):
+the ReLU mask recomputed from the raw conv output (relu mode 2) must give bit-identical results to
+the mask read from the stored activation (mode 1), and both match a torch fp32 restatement of
+nn.BatchNorm2d + ReLU backward (torch/nn/modules/batchnorm.py semantics: batch statistics,
+biased variance) within bf16 storage tolerance."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f32"])
+@pytest.mark.parametrize("P,Cc", [(4096, 64), (2048, 256), (1000, 512), (37, 8)])
+def test_bn_backward_mask_from_raw_matches_stored_mask(dt, P, Cc):
+    import zebrapose_amd._lib as L
+    dev = torch.device("cuda", 0)
+    tdt = torch.bfloat16 if dt == "bf16" else torch.float32
+    code = L.dtype_code(tdt)
+    g = torch.Generator(device="cpu").manual_seed(P + Cc)
+    raw = (torch.randn(P, Cc, generator=g) * 2 + 0.3).to(tdt).to(dev)
+    gout = torch.randn(P, Cc, generator=g).to(tdt).to(dev)
+    gamma = (torch.rand(Cc, generator=g) + 0.5).to(dev)
+    beta = (torch.randn(Cc, generator=g) * 0.5).to(dev)
+    rf = raw.float()
+    mean = rf.mean(0)
+    invstd = torch.rsqrt(rf.var(0, unbiased=False) + 1e-5)
+    scale = gamma * invstd
+    shift = torch.addcmul(beta, -mean, scale)  # fma(-mean, scale, beta) up to rounding; kernel reads save
+    save = torch.cat([mean, invstd, scale, shift]).contiguous()
+    y = torch.empty_like(raw)
+    st = L.stream_ptr()
+    L.call("zp_bn_apply", raw.data_ptr(), P, Cc, scale.data_ptr(), shift.data_ptr(), None, 0, 0, 1, code, y.data_ptr(),
+           Cc, 0, st)
+    parts = L.lib.zp_bn_bwd_parts(P, Cc)
+    outs = {}
+    for mode in (1, 2):
+        partials = torch.empty(2 * (parts + 1) * Cc, dtype=torch.float32, device=dev)
+        dgamma = torch.empty(Cc, device=dev)
+        dbeta = torch.empty(Cc, device=dev)
+        yp = y.data_ptr() if mode == 1 else None
+        L.call("zp_bn_bwd_reduce", gout.data_ptr(), Cc, 0, yp, Cc, 0, raw.data_ptr(), P, Cc, save.data_ptr(), mode,
+               code, partials.data_ptr(), dgamma.data_ptr(), dbeta.data_ptr(), 0, st)
+        dx = torch.empty_like(raw)
+        L.call("zp_bn_bwd_apply", gout.data_ptr(), Cc, 0, yp, Cc, 0, raw.data_ptr(), P, Cc, save.data_ptr(),
+               partials.data_ptr(), gamma.data_ptr(), mode, code, dx.data_ptr(), None, 0, 0, 0, st)
+        torch.cuda.synchronize()
+        outs[mode] = (dgamma.cpu(), dbeta.cpu(), dx.float().cpu())
+    for a, b in zip(outs[1], outs[2]):
+        assert torch.equal(a, b)
+    # fp32 restatement: y = relu(xhat*gamma + beta); dL/dx through batch statistics
+    xhat = (rf - mean) * invstd
+    m = ((rf * scale + shift) > 0).float()
+    gm = gout.float() * m
+    db = gm.sum(0)
+    dg = (gm * xhat).sum(0)
+    dx_ref = gamma * invstd * (gm - db / P - xhat * dg / P)
+    dgamma, dbeta, dx = outs[2]
+    tol = 2e-2 if dt == "bf16" else 1e-4
+    assert torch.allclose(dbeta, db.cpu(), rtol=1e-4, atol=1e-3)
+    assert torch.allclose(dgamma, dg.cpu(), rtol=1e-4, atol=1e-3)
+    err = float((dx - dx_ref.cpu()).norm() / dx_ref.norm())
+    assert err < tol, err
+    # the mask the kernel forms agrees with y > 0 wherever y is stored nonzero
+    yk = y.float().cpu() > 0
+    mk = (torch.addcmul(shift, rf, scale) > 0).cpu()  # fma form
+    assert float((yk != mk).float().mean()) < 1e-3

@@ -6,7 +6,9 @@ variant's (a schedule change must not change a single bit: same K order per outp
 
     python tools/conv_ab.py --layers 256:256:128:1,512:512:32:4 --flags 28,60 [--rounds 7 --iters 10]
 
-layer = cin:cout:hw:dilation[:k]  (3x3 by default; batch --batch).  A variant is a flags value,
+layer = cin:cout:hw:dilation[:k]  (3x3 by default; batch --batch); T<cin>:<cout>:<hw> a ConvTranspose2d
+(3, s2) and S<cin>:<cout>:<hw>[:1:k] a stride-2 conv of an hw input.  Variant knobs: r<N> = k_wgrad2
+rounds (key 4), l<N> = k_wgrad_lds rounds (key 5; l0 = the 1024-workgroup target).  A variant is a flags value,
 optionally with extra knobs: "94+noc64" sets zp_conv_tuning(2, 0) (64-channel layers on k_conv)."""
 import argparse
 import json
@@ -45,10 +47,13 @@ def main():
         L.lib.zp_conv_tuning(3, 0 if "now2" in parts[1:] else 1)
         tg = [int(q[1:]) for q in parts[1:] if q.startswith("r") and q[1:].isdigit()]
         L.lib.zp_conv_tuning(4, tg[0] if tg else 1)
+        lg = [int(q[1:]) for q in parts[1:] if q.startswith("l") and q[1:].isdigit()]
+        L.lib.zp_conv_tuning(5, lg[0] if lg else 1)
     rows = []
     for spec in a.layers.split(","):
         tr = spec.startswith("T")  # T<cin>:<cout>:<hw>: ConvTranspose2d(3, s2, p1, op1) (aspp.py:60-80)
-        f = [int(v) for v in spec.lstrip("T").split(":")]
+        s2 = spec.startswith("S")  # S<cin>:<cout>:<hw>[:1:k]: stride-2 conv, hw = input size
+        f = [int(v) for v in spec.lstrip("TS").split(":")]
         cin, cout, hw = f[:3]
         d = f[3] if len(f) > 3 else 1
         k = f[4] if len(f) > 4 else 3
@@ -56,15 +61,17 @@ def main():
         if tr:
             conv = LY.ConvTranspose2d(cin, cout, 3, 2, 1, 1, bias=False).to(dev)
         else:
-            conv = LY.Conv2d(cin, cout, k, 1, d * (k // 2), d, bias=False).to(dev)
+            conv = LY.Conv2d(cin, cout, k, 2 if s2 else 1, d * (k // 2), d, bias=False).to(dev)
         torch.nn.init.normal_(conv.weight, 0, (2.0 / (cin * k * k)) ** 0.5)
         bn = LY.BatchNorm2d(cout).to(dev).eval()
         unit = Unit(conv, bn, relu=True)
         eng = Engine(torch.nn.Module(), torch.bfloat16)
         x = Act(torch.randn(a.batch, hw, hw, cin, device=dev).bfloat16())
-        ohw = 2 * hw if tr else hw
+        ohw = 2 * hw if tr else (hw // 2 if s2 else hw)
         y = Act(torch.empty(a.batch, ohw, ohw, cout, device=dev, dtype=torch.bfloat16))
         fl = 2.0 * a.batch * hw * hw * k * k * cin * cout  # ConvT: 9 taps per input pixel as well
+        if s2:
+            fl /= 4
         dw = torch.empty_like(conv.weight)
         if a.wgrad:
             y.buf.copy_(torch.randn(y.buf.shape, device=dev).clamp(min=0).bfloat16())
@@ -110,6 +117,7 @@ def main():
         L.lib.zp_conv_tuning(0, 1024)
         L.lib.zp_conv_tuning(3, 1)
         L.lib.zp_conv_tuning(4, 1)
+        L.lib.zp_conv_tuning(5, 1)
         for fv in flags:
             med, mn = float(np.median(times[fv])), float(np.min(times[fv]))
             row = {"layer": spec, "flags": fv, "us_median": round(med, 2), "us_min": round(mn, 2),

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Runs on the GPU box (gpurun): kernel-trace stats for inference and training, then the two PMC
-# passes (FETCH_SIZE, WRITE_SIZE -- separate runs, TCC slots) over the inference step.
+# passes (FETCH_SIZE, WRITE_SIZE -- separate runs, TCC slots) over the inference step, then the same
+# two passes over the training step.
 # Output under gpurun_out/prof_<tag>/ ; summarise with tools/prof_summary.py.
 set -e -o pipefail
 TAG=${1:-r02}
@@ -15,4 +16,8 @@ timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format cs
     python3 tools/prof_driver.py --mode infer --steps 3 --warmup 1 > $O/pmc_fetch.log 2>&1
 timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/pmc_write -o run -- \
     python3 tools/prof_driver.py --mode infer --steps 3 --warmup 1 > $O/pmc_write.log 2>&1
+timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/tpmc_fetch -o run -- \
+    python3 tools/prof_driver.py --mode train --steps 2 --warmup 1 > $O/tpmc_fetch.log 2>&1
+timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/tpmc_write -o run -- \
+    python3 tools/prof_driver.py --mode train --steps 2 --warmup 1 > $O/tpmc_write.log 2>&1
 echo done

@@ -3,6 +3,7 @@
 
   profiles/<tag>_infer_kernel_stats.csv   rocprofv3 --kernel-trace --stats, inference (bench.py)
   profiles/<tag>_train_kernel_stats.csv   same, training step (tools/prof_driver.py --mode train)
+  profiles/<tag>_train_pmc_traffic.json   same two passes over training steps
   profiles/<tag>_pmc_traffic.json         HBM bytes per launch per kernel instantiation, from two
                                           separate --pmc passes (FETCH_SIZE, WRITE_SIZE) over eval
                                           inference steps, corrected as MI355X_MICROARCH.md §HBM
@@ -66,14 +67,22 @@ def main(tag="r01"):
         if f:
             shutil.copy(f, os.path.join(dst, f"{tag}_{leg}_kernel_stats.csv"))
             print("copied", f)
-    ff = one(os.path.join(src, "pmc_fetch", "**", "*counter_collection.csv"))
-    fw = one(os.path.join(src, "pmc_write", "**", "*counter_collection.csv"))
+    for pre, leg, what in (("pmc", "", "eval inference steps (--mode infer --steps 3 --warmup 1: R34 bs=32 bf16 "
+                                         "eval + decode)"),
+                           ("tpmc", "train_", "training steps (--mode train --steps 2 --warmup 1: R34 bs=32 bf16 "
+                                              "forward + loss + backward + Adam)")):
+        traffic(src, dst, tag, pre, leg, what)
+
+
+def traffic(src, dst, tag, pre, leg, what):
+    ff = one(os.path.join(src, f"{pre}_fetch", "**", "*counter_collection.csv"))
+    fw = one(os.path.join(src, f"{pre}_write", "**", "*counter_collection.csv"))
     if not (ff and fw):
-        print("no PMC passes found")
+        print(f"no {pre} PMC passes found")
         return
     fetch, write = counters(ff, "FETCH_SIZE"), counters(fw, "WRITE_SIZE")
-    out = {"source": "tools/prof_round.sh: rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate runs) over "
-                     "tools/prof_driver.py --mode infer --steps 3 --warmup 1 (R34 bs=32 bf16 eval + decode)",
+    out = {"source": f"tools/prof_round.sh: rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate runs) over "
+                     f"tools/prof_driver.py {what}",
            "correction": "bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024 (FETCH_SIZE halves wide coalesced "
                          "reads on gfx950, MI355X_MICROARCH.md HBM section)",
            "kernels": {}, "by_label": {}}
@@ -86,11 +95,11 @@ def main(tag="r01"):
         lab = bench_label(k)
         if lab:
             out["by_label"][lab] = round(rd + wr)
-    with open(os.path.join(dst, f"{tag}_pmc_traffic.json"), "w") as fh:
+    with open(os.path.join(dst, f"{tag}_{leg}pmc_traffic.json"), "w") as fh:
         json.dump(out, fh, indent=1)
+    print(f"== {tag}_{leg}pmc_traffic.json")
     for k, v in sorted(out["kernels"].items(), key=lambda kv: -kv[1]["hbm_bytes_per_launch"] * kv[1]["launches"])[:12]:
         print(f"{v['launches']:5d} {v['hbm_bytes_per_launch'] / 1e6:10.2f} MB/launch  {k[:100]}")
-
 
 if __name__ == "__main__":
     main(*sys.argv[1:])

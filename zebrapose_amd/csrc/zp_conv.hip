@@ -1399,7 +1399,8 @@ __global__ void __launch_bounds__(512) k_wgrad_lds(const zp_wgrad_args A, float*
   // L2 instead of being fetched by all eight.
   const int total = gridDim.x;
   const int bid = blockIdx.x;
-  const int lin = (total & 7) ? bid : (bid & 7) * (total >> 3) + (bid >> 3);
+  const int xcd = bid & 7, pos = bid >> 3, q8 = total >> 3, r8 = total & 7;  // bijective for any total
+  const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + pos;
   const int tiles = tiles_per_sub;
   const int tile = lin % tiles;
   const int rest = lin / tiles;
@@ -2208,7 +2209,7 @@ static int wgrad_cfg(const zp_wgrad_args& a) {
 // zp_conv_tuning key 3: 0 disables it; key 4: its workgroup rounds over the CUs (default 1: fewer,
 // longer workgroups than k_wgrad_lds's 1024 -- the split-K partial slabs are written and re-read
 // in full -- and never a partial extra round; one round measured fastest).
-static int g_wgrad2 = 1, g_wgrad2_rounds = 1;
+static int g_wgrad2 = 1, g_wgrad2_rounds = 1, g_wgrad_lds_rounds = 1;
 static int num_cus() {
   static int n = 0;
   if (!n) {
@@ -2240,7 +2241,10 @@ static void wgrad_plan_lds(const zp_wgrad_args& a, int* splits, int* col_tiles, 
   const bool lean = wgrad2_eligible(a);
   // k_wgrad2: workgroups (one per CU at a time: 96-144 KB of LDS) in whole rounds over the CUs --
   // a grid one workgroup past a round costs a full extra workgroup lifetime (513 vs 512 ran 1.6x)
-  long sp = lean ? (long)g_wgrad2_rounds * num_cus() / tiles : (target_lds + tiles - 1) / tiles;
+  // k_wgrad_lds: the same whole-round plan when zp_conv_tuning key 5 > 0, else ~target_lds workgroups
+  long sp = lean ? (long)g_wgrad2_rounds * num_cus() / tiles
+                 : g_wgrad_lds_rounds > 0 ? (long)g_wgrad_lds_rounds * num_cus() / tiles
+                                          : (target_lds + tiles - 1) / tiles;
   if (sp < 1) sp = 1;
   long maxsp = M / (16 * KP);
   if (maxsp < 1) maxsp = 1;
@@ -2251,7 +2255,7 @@ static void wgrad_plan_lds(const zp_wgrad_args& a, int* splits, int* col_tiles, 
   sp = (M + pp - 1) / pp;  // never more than requested: pp only grew
   // k_wgrad_lds: pad the split count so the launch is a multiple of 8 workgroups (its XCD-aware
   // order needs it); padding splits have an empty pixel range and write zero partials
-  if (!lean)
+  if (!lean && g_wgrad_lds_rounds <= 0)
     while ((sp * tiles) % 8) ++sp;
   *splits = (int)sp;
   *col_tiles = ct;
@@ -2351,7 +2355,8 @@ extern "C" int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* st
 /* runtime tuning knobs (tests / sweeps).  key 0: minimum workgroups for the 256-channel conv tile
  * (default 1024); key 1: conv schedule flags (-1 = ZP_CONV_FLAGS / default); key 2: 64-channel
  * layers on the strip kernel (default 1); key 3: k_wgrad2 (default 1); key 4: k_wgrad2's
- * workgroup rounds over the CUs (default 1).  Returns the previous value. */
+ * workgroup rounds over the CUs (default 1); key 5: k_wgrad_lds's workgroup rounds (default 1; 0 =
+ * the older ~1024-workgroup target padded to a multiple of 8).  Returns the previous value. */
 extern "C" int zp_conv_tuning(int key, int value) {
   if (key == 0) {
     const int old = g_tc256_min_blocks;
@@ -2371,6 +2376,11 @@ extern "C" int zp_conv_tuning(int key, int value) {
   if (key == 3) {
     const int old = g_wgrad2;
     g_wgrad2 = value;
+    return old;
+  }
+  if (key == 5) {
+    const int old = g_wgrad_lds_rounds;
+    g_wgrad_lds_rounds = value >= 0 ? value : 1;
     return old;
   }
   if (key == 4) {

@@ -232,10 +232,13 @@ __global__ void k_bn_train_finalize(const float* __restrict__ part, int parts, i
   if (var < 0) var = 0;
   float invstd = (float)(1.0 / sqrt(var + (double)eps));
   float sc = gamma[c] * invstd;
+  const float shv = __builtin_fmaf(-(float)mean, sc, beta[c]);
   scale[c] = sc;
-  shift[c] = beta[c] - (float)mean * sc;
+  shift[c] = shv;
   save[c] = (float)mean;
   save[C + c] = invstd;
+  save[2 * C + c] = sc;  // the backward recomputes the ReLU mask from the raw conv output
+  save[3 * C + c] = shv;
   double mt = mean + (bias ? (double)bias[c] : 0.0);
   double unb = cntd > 1 ? var * cntd / (cntd - 1.0) : var;
   rm[c] = (float)((1.0 - mom) * rm[c] + mom * mt);
@@ -256,10 +259,31 @@ __device__ __forceinline__ void load_chan(const float* __restrict__ p, float* v)
   }
 }
 
+// Pixel-row tiling of the per-pixel BN passes: block = 256 threads = lanes (16-byte channel chunks,
+// at most 256) x R pixel rows; blockIdx.y = channel group.  A thread keeps one channel chunk, so its
+// per-channel terms are loaded once, and walks K = pix / R pixels in batches of 4 with every load
+// of a batch issued before any use.
+struct BnTile {
+  int lanes, R, cgroups, pix, blocks;
+};
+static inline BnTile bn_tile(long P, int C, int N, long min_blocks = 2048) {  // k_bn_bwd_apply
+  BnTile t;
+  const int CV = C / N;
+  t.lanes = CV < 256 ? CV : 256;
+  t.R = 256 / t.lanes;
+  t.cgroups = CV > 256 ? CV / 256 : 1;
+  int K = 16;  // pixels per thread: fewer (down to 4) while that leaves fewer than min_blocks blocks
+  while (K > 4 && ((P + (long)t.R * K - 1) / ((long)t.R * K)) * t.cgroups < min_blocks) K >>= 1;
+  t.pix = t.R * K;
+  t.blocks = (int)((P + t.pix - 1) / t.pix);
+  return t;
+}
+
 template <typename T>
 __global__ void k_bn_apply(const T* __restrict__ x, long P, int C, const float* __restrict__ scale,
                            const float* __restrict__ shift, const T* __restrict__ res, int ldr, int cr0, int relu,
                            T* __restrict__ y, int ldy, int cy0) {
+  // grid-stride over 16-byte chunks (measured faster here than bn_tile's pixel-row tiling)
   constexpr int N = V16<T>::N;
   const int CV = C / N;
   const long total = P * CV;
@@ -278,7 +302,7 @@ __global__ void k_bn_apply(const T* __restrict__ x, long P, int C, const float* 
     }
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-      float o = v[i] * sc[i] + sh[i];
+      float o = __builtin_fmaf(v[i], sc[i], sh[i]);  // the backward's mask (relu mode 2) repeats this
       if (res) o += r[i];
       if (relu) o = fmaxf(o, 0.f);
       v[i] = o;
@@ -299,12 +323,17 @@ static inline int bn_bwd_pix(int P, int C) {
   return R * rows;
 }
 
-// block: 256 threads = (C/N) chunk lanes x R rows
-template <typename T>
-__global__ void k_bn_bwd_reduce(const T* __restrict__ dy, int lddy, int cdy0, const T* __restrict__ y, int ldy, int cy0,
-                                const T* __restrict__ x, long P, int C, const float* __restrict__ save, int relu,
-                                float* __restrict__ part, int parts, int pix) {
+// block: 256 threads = (C/N) chunk lanes x R rows.  MODE: ReLU mask source (0 none, 1 the stored
+// activation y, 2 recomputed from the raw x); HX: x given (sum g*xhat as well).  Templated so each
+// instance holds only the registers its streams need (the runtime-mode kernel spilled at 128 VGPRs).
+template <typename T, int MODE, bool HX>
+__global__ void __launch_bounds__(256) k_bn_bwd_reduce(const T* __restrict__ dy, int lddy, int cdy0,
+                                                       const T* __restrict__ y, int ldy, int cy0,
+                                                       const T* __restrict__ x, long P, int C,
+                                                       const float* __restrict__ save, float* __restrict__ part,
+                                                       int parts, int pix) {
   constexpr int N = V16<T>::N;
+  static_assert(MODE != 2 || HX, "mask from raw needs x");
   __shared__ float red[2][256][N];
   const int CV = C / N;
   const int lanes = CV < 256 ? CV : 256;  // chunk lanes per row
@@ -314,51 +343,54 @@ __global__ void k_bn_bwd_reduce(const T* __restrict__ dy, int lddy, int cdy0, co
   const int c = (cgi * lanes + cl) * N;
   const long p0 = (long)blockIdx.x * pix;
   const long p1 = min(P, p0 + pix);
-  float sg[N], sgx[N], mean[N], inv[N];
+  float sg[N], sgx[N], mean[N], inv[N], msc[N], msh[N];
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     sg[i] = sgx[i] = 0.f;
-    mean[i] = (x && c < C) ? save[c + i] : 0.f;
-    inv[i] = (x && c < C) ? save[C + c + i] : 0.f;
+    mean[i] = (HX && c < C) ? save[c + i] : 0.f;
+    inv[i] = (HX && c < C) ? save[C + c + i] : 0.f;
+    msc[i] = (MODE == 2 && c < C) ? save[2 * C + c + i] : 0.f;
+    msh[i] = (MODE == 2 && c < C) ? save[3 * C + c + i] : 0.f;
   }
   if (row < R && c < C) {
-    // U pixels per iteration with all 3U loads issued before any use: the loop is otherwise
+    // U pixels per iteration with all loads issued before any use: the loop is otherwise
     // latency-bound (one dependent HBM round trip per pixel row)
-    constexpr int U = 4;
-    auto body = [&](long p, const uint4& gd, const uint4& yd, const uint4& xd) {
+    constexpr int U = 4;  // pixels in flight per thread (the pixel count per thread, pix / R, is 4, 8 or 16)
+    auto body = [&](const uint4& gd, const uint4& yd, const uint4& xd, bool ok) {
       float g[N], yy[N], xx[N];
       V16<T>::load((const T*)&gd, g);
-      if (relu) {
+#pragma unroll
+      for (int i = 0; i < N; ++i) g[i] = ok ? g[i] : 0.f;
+      if (MODE == 1) {
         V16<T>::load((const T*)&yd, yy);
 #pragma unroll
         for (int i = 0; i < N; ++i) g[i] = yy[i] > 0.f ? g[i] : 0.f;
       }
-      if (x) {
+      if (HX) {
         V16<T>::load((const T*)&xd, xx);
+        if (MODE == 2)
+#pragma unroll
+          for (int i = 0; i < N; ++i) g[i] = __builtin_fmaf(xx[i], msc[i], msh[i]) > 0.f ? g[i] : 0.f;
 #pragma unroll
         for (int i = 0; i < N; ++i) sgx[i] += g[i] * (xx[i] - mean[i]) * inv[i];
       }
 #pragma unroll
       for (int i = 0; i < N; ++i) sg[i] += g[i];
     };
-    long p = p0 + row;
-    for (; p + (U - 1) * R < p1; p += U * R) {
+    // batches of U rows with every load issued before any use; rows past the end load the last
+    // row again (clamped address) and contribute zero
+    const uint4 z = make_uint4(0, 0, 0, 0);
+    for (long pb = p0 + row; pb < p1; pb += U * R) {
       uint4 gd[U], yd[U], xd[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const long pp = p + u * R;
+        const long pp = min(pb + u * R, p1 - 1);
         gd[u] = *(const uint4*)(dy + pp * lddy + cdy0 + c);
-        yd[u] = relu ? *(const uint4*)(y + pp * ldy + cy0 + c) : make_uint4(0, 0, 0, 0);
-        xd[u] = x ? *(const uint4*)(x + pp * C + c) : make_uint4(0, 0, 0, 0);
+        yd[u] = MODE == 1 ? *(const uint4*)(y + pp * ldy + cy0 + c) : z;
+        xd[u] = HX ? *(const uint4*)(x + pp * C + c) : z;
       }
 #pragma unroll
-      for (int u = 0; u < U; ++u) body(p + u * R, gd[u], yd[u], xd[u]);
-    }
-    for (; p < p1; p += R) {
-      const uint4 gd = *(const uint4*)(dy + p * lddy + cdy0 + c);
-      const uint4 yd = relu ? *(const uint4*)(y + p * ldy + cy0 + c) : make_uint4(0, 0, 0, 0);
-      const uint4 xd = x ? *(const uint4*)(x + p * C + c) : make_uint4(0, 0, 0, 0);
-      body(p, gd, yd, xd);
+      for (int u = 0; u < U; ++u) body(gd[u], yd[u], xd[u], pb + u * R < p1);
     }
   }
 #pragma unroll
@@ -422,60 +454,87 @@ __global__ void __launch_bounds__(1024) k_bn_bwd_totals(float* __restrict__ part
   if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)s : (float)s;
 }
 
-template <typename T>
-__global__ void k_bn_bwd_apply(const T* __restrict__ dy, int lddy, int cdy0, const T* __restrict__ y, int ldy, int cy0,
-                               const T* __restrict__ x, long P, int C, const float* __restrict__ save,
-                               const float* __restrict__ part, int parts, const float* __restrict__ gamma, int relu,
-                               T* __restrict__ dx, T* __restrict__ dres, int lddres, int cdres0, int racc) {
+template <typename T, int relu>
+__global__ void __launch_bounds__(256) k_bn_bwd_apply(const T* __restrict__ dy, int lddy, int cdy0,
+                                                      const T* __restrict__ y, int ldy, int cy0,
+                                                      const T* __restrict__ x, long P, int C,
+                                                      const float* __restrict__ save, const float* __restrict__ part,
+                                                      int parts, const float* __restrict__ gamma, T* __restrict__ dx,
+                                                      T* __restrict__ dres, int lddres, int cdres0, int racc, int pix) {
+  // pixel-row tiling (bn_tile)
   constexpr int N = V16<T>::N;
+  constexpr int U = 4;
   const int CV = C / N;
-  const long total = P * CV;
+  const int lanes = CV < 256 ? CV : 256;
+  const int R = 256 / lanes;
+  const int cl = threadIdx.x % lanes, row = threadIdx.x / lanes;
+  const int c = (blockIdx.y * lanes + cl) * N;
+  if (row >= R || c >= C) return;
+  const long p0 = (long)blockIdx.x * pix;
+  const long p1 = min(P, p0 + pix);
   const float invP = 1.f / (float)P;
-  // per-channel terms of the current chunk (the grid stride usually keeps a thread on one chunk)
-  int cur = -1;
-  float mean[N], inv[N], sg[N], sgx[N], gm[N];
-  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    long p = e / CV;
-    int c = (int)(e - p * CV) * N;
-    float g[N], yy[N], xx[N], o[N];
-    V16<T>::load(dy + p * lddy + cdy0 + c, g);
-    if (relu) {
-      V16<T>::load(y + p * ldy + cy0 + c, yy);
-#pragma unroll
-      for (int i = 0; i < N; ++i) g[i] = yy[i] > 0.f ? g[i] : 0.f;
+  float mean[N], inv[N], sg[N], sgx[N], gm[N], msc[N], msh[N];
+  if (dx) {
+    load_chan<N>(save + c, mean);
+    load_chan<N>(save + C + c, inv);
+    if (relu == 2) {
+      load_chan<N>(save + 2 * C + c, msc);
+      load_chan<N>(save + 3 * C + c, msh);
     }
-    if (dx) {
-      V16<T>::load(x + p * C + c, xx);
-      if (c != cur) {
-        cur = c;
-        load_chan<N>(save + c, mean);
-        load_chan<N>(save + C + c, inv);
-        load_chan<N>(part + (size_t)parts * C + c, sg);
-        load_chan<N>(part + ((size_t)parts + 1 + parts) * C + c, sgx);
-        load_chan<N>(gamma + c, gm);
+    load_chan<N>(part + (size_t)parts * C + c, sg);
+    load_chan<N>(part + ((size_t)parts + 1 + parts) * C + c, sgx);
+    load_chan<N>(gamma + c, gm);
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      sg[i] *= invP;
+      sgx[i] *= invP;
+    }
+  }
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  for (long pb = p0 + row; pb < p1; pb += U * R) {
+    uint4 gd[U], yd[U], xd[U], rd[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long pp = min(pb + u * R, p1 - 1);
+      gd[u] = *(const uint4*)(dy + pp * lddy + cdy0 + c);
+      yd[u] = relu == 1 ? *(const uint4*)(y + pp * ldy + cy0 + c) : z;
+      xd[u] = dx ? *(const uint4*)(x + pp * C + c) : z;
+      rd[u] = (dres && racc) ? *(const uint4*)(dres + pp * lddres + cdres0 + c) : z;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long p = pb + u * R;
+      if (p >= p1) break;
+      float g[N], yy[N], xx[N], o[N];
+      V16<T>::load((const T*)&gd[u], g);
+      if (relu == 1) {
+        V16<T>::load((const T*)&yd[u], yy);
+#pragma unroll
+        for (int i = 0; i < N; ++i) g[i] = yy[i] > 0.f ? g[i] : 0.f;
+      }
+      if (dx) {
+        V16<T>::load((const T*)&xd[u], xx);
+        if (relu == 2)
+#pragma unroll
+          for (int i = 0; i < N; ++i) g[i] = __builtin_fmaf(xx[i], msc[i], msh[i]) > 0.f ? g[i] : 0.f;
 #pragma unroll
         for (int i = 0; i < N; ++i) {
-          sg[i] *= invP;
-          sgx[i] *= invP;
+          float xh = (xx[i] - mean[i]) * inv[i];
+          o[i] = gm[i] * inv[i] * (g[i] - sg[i] - xh * sgx[i]);
         }
+        V16<T>::store(dx + p * C + c, o);
       }
+      if (dres) {
+        T* d = dres + p * lddres + cdres0 + c;
+        if (racc) {
+          float r[N];
+          V16<T>::load((const T*)&rd[u], r);
 #pragma unroll
-      for (int i = 0; i < N; ++i) {
-        float xh = (xx[i] - mean[i]) * inv[i];
-        o[i] = gm[i] * inv[i] * (g[i] - sg[i] - xh * sgx[i]);
-      }
-      V16<T>::store(dx + p * C + c, o);
-    }
-    if (dres) {
-      T* d = dres + p * lddres + cdres0 + c;
-      if (racc) {
-        float r[N];
-        V16<T>::load(d, r);
-#pragma unroll
-        for (int i = 0; i < N; ++i) r[i] += g[i];
-        V16<T>::store(d, r);
-      } else {
-        V16<T>::store(d, g);
+          for (int i = 0; i < N; ++i) r[i] += g[i];
+          V16<T>::store(d, r);
+        } else {
+          V16<T>::store(d, g);
+        }
       }
     }
   }
@@ -1050,7 +1109,9 @@ extern "C" int zp_bn_bwd_reduce(const void* dy, int lddy, int cdy0, const void* 
                                 float* dbeta, int accumulate, void* stream) {
   ZP_DTYPE_CHECK_TRAIN("zp_bn_bwd_reduce", dtype);
   const int N = dtype == ZP_F32 ? 4 : 8;
-  ZP_CHECK_ARG(dy && partials && P > 0 && C % N == 0 && (!relu || y) && (!x || save), "zp_bn_bwd_reduce: bad args");
+  ZP_CHECK_ARG(dy && partials && P > 0 && C % N == 0 && relu >= 0 && relu <= 2 && (relu != 1 || y) &&
+                   (relu != 2 || x) && (!x || save),
+               "zp_bn_bwd_reduce: bad args");
   ZP_CHECK_ARG(C / N <= 256 || (C / N) % 256 == 0, "zp_bn_bwd_reduce: C %d", C);
   const int parts = zp_bn_bwd_parts(P, C);
   const int CV = C / N;
@@ -1058,12 +1119,28 @@ extern "C" int zp_bn_bwd_reduce(const void* dy, int lddy, int cdy0, const void* 
   const int pix = bn_bwd_pix(P, C);
   hipStream_t st = (hipStream_t)stream;
   dim3 grid(parts, cgroups);
+#define ZP_BNR(T, M, HX)                                                                                           \
+  hipLaunchKernelGGL((k_bn_bwd_reduce<T, M, HX>), grid, dim3(256), 0, st, (const T*)dy, lddy, cdy0, (const T*)y, ldy, \
+                     cy0, (const T*)x, (long)P, C, save, partials, parts, pix)
+#define ZP_BNR_T(T)             \
+  do {                          \
+    if (relu == 2)              \
+      ZP_BNR(T, 2, true);       \
+    else if (relu == 1 && x)    \
+      ZP_BNR(T, 1, true);       \
+    else if (relu == 1)         \
+      ZP_BNR(T, 1, false);      \
+    else if (x)                 \
+      ZP_BNR(T, 0, true);       \
+    else                        \
+      ZP_BNR(T, 0, false);      \
+  } while (0)
   if (dtype == ZP_BF16)
-    hipLaunchKernelGGL(k_bn_bwd_reduce<bf16_t>, grid, dim3(256), 0, st, (const bf16_t*)dy, lddy, cdy0, (const bf16_t*)y,
-                       ldy, cy0, (const bf16_t*)x, (long)P, C, save, relu, partials, parts, pix);
+    ZP_BNR_T(bf16_t);
   else
-    hipLaunchKernelGGL(k_bn_bwd_reduce<float>, grid, dim3(256), 0, st, (const float*)dy, lddy, cdy0, (const float*)y,
-                       ldy, cy0, (const float*)x, (long)P, C, save, relu, partials, parts, pix);
+    ZP_BNR_T(float);
+#undef ZP_BNR_T
+#undef ZP_BNR
   ZP_LAUNCH_CHECK("zp_bn_bwd_reduce");
   hipLaunchKernelGGL(k_bn_bwd_totals, dim3((C + 31) / 32), dim3(1024), 0, st, partials, parts, C, dgamma, dbeta,
                      accumulate);
@@ -1076,19 +1153,33 @@ extern "C" int zp_bn_bwd_apply(const void* dy, int lddy, int cdy0, const void* y
                                void* dx, void* dres, int lddres, int cdres0, int res_accumulate, void* stream) {
   ZP_DTYPE_CHECK_TRAIN("zp_bn_bwd_apply", dtype);
   const int N = dtype == ZP_F32 ? 4 : 8;
-  ZP_CHECK_ARG(dy && P > 0 && C % N == 0 && (!relu || y) && (!dx || (x && save && partials && gamma)),
+  ZP_CHECK_ARG(dy && P > 0 && C % N == 0 && relu >= 0 && relu <= 2 && (relu != 1 || y) && (relu != 2 || dx) &&
+                   (!dx || (x && save && partials && gamma)),
                "zp_bn_bwd_apply: bad args");
+  ZP_CHECK_ARG(C / N <= 256 || (C / N) % 256 == 0, "zp_bn_bwd_apply: C %d", C);
   const int parts = zp_bn_bwd_parts(P, C);
-  long total = (long)P * (C / N);
+  const BnTile t = bn_tile(P, C, N);
+  const dim3 grid(t.blocks, t.cgroups);
   hipStream_t st = (hipStream_t)stream;
+#define ZP_BNA(T, M)                                                                                             \
+  hipLaunchKernelGGL((k_bn_bwd_apply<T, M>), grid, dim3(256), 0, st, (const T*)dy, lddy, cdy0, (const T*)y, ldy,  \
+                     cy0, (const T*)x, (long)P, C, save, partials, parts, gamma, (T*)dx, (T*)dres, lddres, cdres0, \
+                     res_accumulate, t.pix)
+#define ZP_BNA_T(T)     \
+  do {                  \
+    if (relu == 2)      \
+      ZP_BNA(T, 2);     \
+    else if (relu == 1) \
+      ZP_BNA(T, 1);     \
+    else                \
+      ZP_BNA(T, 0);     \
+  } while (0)
   if (dtype == ZP_BF16)
-    hipLaunchKernelGGL(k_bn_bwd_apply<bf16_t>, dim3(grid_for(total)), dim3(256), 0, st, (const bf16_t*)dy, lddy, cdy0,
-                       (const bf16_t*)y, ldy, cy0, (const bf16_t*)x, (long)P, C, save, partials, parts, gamma, relu,
-                       (bf16_t*)dx, (bf16_t*)dres, lddres, cdres0, res_accumulate);
+    ZP_BNA_T(bf16_t);
   else
-    hipLaunchKernelGGL(k_bn_bwd_apply<float>, dim3(grid_for(total)), dim3(256), 0, st, (const float*)dy, lddy, cdy0,
-                       (const float*)y, ldy, cy0, (const float*)x, (long)P, C, save, partials, parts, gamma, relu,
-                       (float*)dx, (float*)dres, lddres, cdres0, res_accumulate);
+    ZP_BNA_T(float);
+#undef ZP_BNA_T
+#undef ZP_BNA
   ZP_LAUNCH_CHECK("zp_bn_bwd_apply");
   return ZP_OK;
 }

@@ -22,6 +22,7 @@ input's gradient buffer).
 """
 from __future__ import annotations
 
+import os
 import ctypes as C
 import weakref
 
@@ -108,6 +109,14 @@ class Engine:
         # read and wrote (kept alive by the list) -- the teacher-forced layer parity tests replay
         # each op on the host from the device's own stored inputs (tests/test_gpu_bench_geometry.py)
         self.trace = None
+        # training backward: each unit's weight gradient runs on a second HIP stream, concurrently
+        # with its input gradient and the next unit's BN backward on the main stream (the wgrad
+        # kernel is L2/MFMA-bound, the BN passes HBM-bound; both fill the other's tail).  The
+        # streams join at the end of backward().  ZP_SIDE_WGRAD=0 keeps everything on one stream.
+        self.side_wgrad = os.environ.get("ZP_SIDE_WGRAD", "1") != "0"
+        self._side = None
+        self._side_used = False
+        self.bn_mask_from_raw = True  # BN+ReLU backward without residual: mask from raw (A/B knob)
 
     # ------------------------------------------------------------------ weight / BN caches
     def invalidate(self):
@@ -298,7 +307,7 @@ class Engine:
         dev = x.buf.device
         scale = torch.empty(unit.cout, dtype=torch.float32, device=dev)
         shift = torch.empty_like(scale)
-        save = torch.empty(2 * unit.cout, dtype=torch.float32, device=dev)
+        save = torch.empty(4 * unit.cout, dtype=torch.float32, device=dev)  # mean, invstd, scale, shift
         L.call("zp_bn_train_finalize", stats.data_ptr(), parts, unit.cout, P, C.c_float(bn.eps),
                C.c_float(bn.momentum), bn.weight.data_ptr(), bn.bias.data_ptr(), L.ptr(unit.conv.bias),
                bn.running_mean.data_ptr(), bn.running_var.data_ptr(), bn.num_batches_tracked.data_ptr(),
@@ -413,6 +422,18 @@ class Engine:
             return
         L.check(L.lib.zp_conv2d_wgrad(C.byref(a), ws.data_ptr(), L.stream_ptr()), "zp_conv2d_wgrad")
 
+    def _side_stream(self, dev):
+        if not self.side_wgrad or dev.type != "cuda" or self.timing is not None:
+            return None  # the per-launch timing (bench breakdown) wants the serial order
+        if self._side is None:
+            self._side = torch.cuda.Stream(dev)
+        return self._side
+
+    def _side_join(self, dev):
+        if self._side is not None and self._side_used:
+            torch.cuda.current_stream(dev).wait_stream(self._side)
+        self._side_used = False
+
     def _dgrad(self, unit, gy: Act, gx: Act, accumulate=True):
         """gx (+)= dgrad(gy): accumulate into the input gradient slice (residual = itself), or
         overwrite it (accumulate False: its first writer, see _grad_out)."""
@@ -443,6 +464,7 @@ class Engine:
         dev = x.buf.device
         st = L.stream_ptr()
         plan = unit.fwd_plan(x.H, x.W)
+        pending = {}  # this unit's gradients, handed over with the weight gradient
         if kind == "head":
             gy = gmap[out]
         else:
@@ -453,20 +475,22 @@ class Engine:
                 partials = torch.empty(2 * (parts + 1) * unit.cout, dtype=torch.float32, device=dev)
                 dgamma = torch.empty_like(bn.weight)
                 dbeta = torch.empty_like(bn.bias)
+                # ReLU without a residual: the mask is recomputed from raw (mode 2), out is not read
+                rm = (2 if res is None and self.bn_mask_from_raw else 1) if unit.relu else 0
                 L.call("zp_bn_bwd_reduce", gout.ptr, gout.ld, gout.c0, out.ptr, out.ld, out.c0, raw.data_ptr(), P,
-                       unit.cout, save.data_ptr(), int(unit.relu), self.dt, partials.data_ptr(), dgamma.data_ptr(),
+                       unit.cout, save.data_ptr(), rm, self.dt, partials.data_ptr(), dgamma.data_ptr(),
                        dbeta.data_ptr(), 0, st)
                 graw = torch.empty_like(raw)
                 gres, racc = self._grad_out(gmap, res, True) if res is not None else (None, True)
                 L.call("zp_bn_bwd_apply", gout.ptr, gout.ld, gout.c0, out.ptr, out.ld, out.c0, raw.data_ptr(), P,
-                       unit.cout, save.data_ptr(), partials.data_ptr(), bn.weight.data_ptr(), int(unit.relu),
+                       unit.cout, save.data_ptr(), partials.data_ptr(), bn.weight.data_ptr(), rm,
                        self.dt, graw.data_ptr(), None if gres is None else gres.ptr,
                        0 if gres is None else gres.ld, 0 if gres is None else gres.c0, int(racc), st)
-                grads[bn.weight] = dgamma
-                grads[bn.bias] = dbeta
+                pending[bn.weight] = dgamma
+                pending[bn.bias] = dbeta
                 if conv.bias is not None:
                     # train-mode BN removes the per-channel mean: d loss / d conv bias == 0 exactly
-                    grads[conv.bias] = torch.zeros_like(conv.bias)
+                    pending[conv.bias] = torch.zeros_like(conv.bias)
                 gy = Act(graw)
             else:
                 raise NotImplementedError("eval-mode backward")
@@ -476,11 +500,27 @@ class Engine:
             db = torch.empty(gy.ld, dtype=torch.float32, device=dev)
             L.call("zp_bn_bwd_reduce", gy.ptr, gy.ld, 0, None, 0, 0, None, gy.P, gy.ld, None, 0, self.dt,
                    partials.data_ptr(), None, db.data_ptr(), 0, st)
-            grads[conv.bias] = db[:unit.cout]
-        dw = torch.empty_like(conv.weight)
+            pending[conv.bias] = db[:unit.cout]
         wdy = Act(gy.buf, 0, unit.cout) if kind == "head" else gy
-        self._wgrad(unit, x, plan, wdy, dw)
-        grads[conv.weight] = dw
+        side = self._side_stream(dev)
+        if side is None:
+            dw = torch.empty_like(conv.weight)
+            self._wgrad(unit, x, plan, wdy, dw)
+            grads.update(pending)
+            grads[conv.weight] = dw
+        else:
+            # the side stream starts after everything enqueued so far (gy, dgamma / dbeta, the head
+            # bias); the gradients are handed over (grads / GradBuckets.ready copies) from the side
+            # stream too, so a bucket's all-reduce is ordered after its weight gradients
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                dw = torch.empty_like(conv.weight)
+                self._wgrad(unit, x, plan, wdy, dw)
+                for k, v in pending.items():
+                    grads[k] = v
+                grads[conv.weight] = dw
+            gy.buf.record_stream(side)  # freed below on the main stream; reused only after the wgrad
+            self._side_used = True  # x (the tape's activation) and the gradients outlive the join
         if need_dx:
             gx, acc = self._grad_out(gmap, x, self._dgrad_whole(unit, x))
             self._dgrad(unit, gy, gx, accumulate=acc)
@@ -761,5 +801,6 @@ class Engine:
                 gx = self._grad(gmap, xa)
                 L.call("zp_add_broadcast_hw", gp.ptr, C.c_float(1.0 / (xa.H * xa.W)), xa.B, xa.C, self.dt, gx.ptr,
                        xa.H, xa.W, gx.ld, gx.c0, 1, st)
+        self._side_join(dev)
         return grads
 
