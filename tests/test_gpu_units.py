@@ -234,3 +234,63 @@ def test_maxpool_bwd_channel_slices(gpu, ih, iw):
     assert torch.equal(got[..., c0 + C:], torch.full_like(got[..., c0 + C:], 5.0))
     want = xx.grad.permute(0, 2, 3, 1).to(torch.bfloat16).float()
     assert (got[..., c0:c0 + C] - want).abs().max().item() <= 2e-2
+
+
+QUAD_GEOMS = [
+    # the four ConvTranspose phases in one tile (k_conv_quad): up1 (W 32) and up2 (W 64) shapes, and the
+    # data gradient of a 3x3 stride-2 conv (dy 32x32 / 64x64), at batch sizes the CPU reference runs
+    ("convT", 256, 256, 3, 2, 1, 1, False, 32),
+    ("convT", 320, 256, 3, 2, 1, 1, False, 64),
+    ("conv", 64, 128, 3, 2, 1, 1, False, 64),
+    ("conv", 128, 64, 3, 2, 1, 1, False, 128),
+]
+
+
+@pytest.fixture
+def quad_any():
+    """k_conv_quad normally needs >= 256 workgroups; the small cases below force it."""
+    from zebrapose_amd import _lib as L
+    old = L.lib.zp_conv_tuning(6, 1)
+    yield
+    L.lib.zp_conv_tuning(6, old)
+
+
+@pytest.mark.parametrize("prec", ["bf16"])
+@pytest.mark.parametrize("geom", QUAD_GEOMS, ids=[f"{g[0]}{g[1]}-{g[2]}s{g[4]}h{g[8]}" for g in QUAD_GEOMS])
+@pytest.mark.parametrize("train", [False, True])
+def test_unit_quad(gpu, geom, prec, train, quad_any):
+    """Same checks as test_unit with the four-phase kernel forced (forward ConvT; in train mode also
+    the stride-2 conv's data gradient, which accumulates into its input-gradient slice)."""
+    from zebrapose_amd import _lib as L
+    from zebrapose_amd.engine import Unit
+    import ctypes as C
+    kind, cin, cout, k, s, p, d, bias, H = geom
+    # the launch under test really is k_conv_quad (variant 3)
+    if kind == "convT":
+        conv, bn = _mk(kind, cin, cout, k, s, p, d, bias)
+        plan = Unit(conv, bn).fwd_plan(H, H)
+        assert len(plan.subs) == 4 and plan.GW == H
+    test_unit(gpu, geom, prec, train, "tc-auto")
+
+
+@pytest.mark.parametrize("geom", QUAD_GEOMS[:2], ids=["up1", "up2"])
+def test_unit_quad_fp16_eval(gpu, geom, quad_any):
+    test_unit_fp16_eval(gpu, geom, "tc-auto")
+
+
+def test_quad_variant_selected(gpu):
+    """zp_conv2d_config reports k_conv_quad (variant 3) for the bench's up2 ConvT launch (bs 32)."""
+    from zebrapose_amd import _lib as L
+    from zebrapose_amd.engine import Engine, Unit, Act
+    from zebrapose_amd.model import layers as LY
+    import ctypes as C
+    conv = LY.ConvTranspose2d(320, 256, 3, 2, 1, output_padding=1, bias=False).to(gpu)
+    bn = LY.BatchNorm2d(256).to(gpu).eval()
+    unit = Unit(conv, bn)
+    eng = Engine(torch.nn.Module(), torch.bfloat16)
+    eng.timing = []
+    x = Act(torch.randn(32, 64, 64, 320, device=gpu).bfloat16())
+    y = Act(torch.empty(32, 128, 128, 256, device=gpu, dtype=torch.bfloat16))
+    eng.unit_fwd(unit, x, y, None)
+    torch.cuda.synchronize()
+    assert eng.timing[-1][4] == "k_conv_quad<bf16,W=64>", eng.timing[-1][4]

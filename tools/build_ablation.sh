@@ -1,6 +1,6 @@
 #!/bin/bash
 # Diagnostic builds of libzp with conv / wgrad ablations (ZP_ABL=1: no LDS-DMA in the loop, 2: no
-# MFMA, 3: weights only, 4: strips only; results are wrong): zebrapose_amd/libzp_abl<N>.so.  Only
+# MFMA, 3: weights only, 4: strips only, 5: no epilogue (k_conv_quad); results are wrong): zebrapose_amd/libzp_abl<N>.so.  Only
 # zp_conv.hip is rebuilt; the other objects come from the product build (make first).
 # Use with ZP_LIB=zebrapose_amd/libzp_abl<N>.so python tools/conv_ab.py ...
 set -e

@@ -99,8 +99,11 @@ __device__ __forceinline__ void static_for(F&& f) {
 template <typename T, int WC, int WP, int NWP>
 __device__ __forceinline__ void conv_epilogue(const zp_conv_args& A, const zp_conv_sub& S, f32x4 (&acc)[WC][WP],
                                               const int p0, const int c0, const int wc, const int wp, const int lane,
-                                              const int M, const int GHW, const int bx) {
+                                              const int M, const int GHW, const int bx, const int zi,
+                                              const int nz) {
   // ---------------- epilogue ----------------
+  // (zi, nz): this tile's sub-problem and the sub-problem count, for the statistics part index
+  // (blockIdx.z / gridDim.z, except in k_conv_quad, whose tiles hold all four sub-pixel phases)
   // output pixel of (lane, j): one division for j = 0, then +16 pixels per j
   int pn[WP], poy[WP], pox[WP];
   bool pok[WP];
@@ -271,8 +274,8 @@ __device__ __forceinline__ void conv_epilogue(const zp_conv_args& A, const zp_co
     // Train-mode BatchNorm statistics of the raw (stored) conv output, per wave half:
     // (count, mean, M2) with M2 centred on the local mean (two passes over the registers, no
     // E[x^2] - E[x]^2 cancellation); zp_bn_train_finalize merges the parts (Chan et al.).
-    const int parts = gridDim.x * gridDim.z * NWP;
-    const int part = (blockIdx.z * gridDim.x + bx) * NWP + wp;
+    const int parts = gridDim.x * nz * NWP;
+    const int part = (zi * gridDim.x + bx) * NWP + wp;
     float cnt = 0.f;
 #pragma unroll
     for (int j = 0; j < WP; ++j) cnt += (p0 + wp * 16 * WP + j * 16 + (lane & 15) < M) ? 1.f : 0.f;
@@ -633,7 +636,7 @@ __global__ void __launch_bounds__(128 * NWP) k_conv(const zp_conv_args A, const 
 
   if (pingpong && wid < 4) __builtin_amdgcn_s_barrier();  // same barrier count for both groups
 
-  conv_epilogue<T, WC, WP, NWP>(A, S, acc, p0, c0, wc, wp, lane, M, GHW, bx);
+  conv_epilogue<T, WC, WP, NWP>(A, S, acc, p0, c0, wc, wp, lane, M, GHW, bx, blockIdx.z, gridDim.z);
 }
 
 // ------------------------------------------------------------------------------------
@@ -892,7 +895,7 @@ __global__ void __launch_bounds__(512) k_conv_strip(const zp_conv_args A, const 
     step(P2{}, ks + 2);
   }
   if (pingpong && wid < 4) __builtin_amdgcn_s_barrier();
-  conv_epilogue<T, WC, WP, NWP>(A, S, acc, p0, c0, wc, wp, lane, M, GHW, bx);
+  conv_epilogue<T, WC, WP, NWP>(A, S, acc, p0, c0, wc, wp, lane, M, GHW, bx, blockIdx.z, gridDim.z);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1163,7 +1166,262 @@ __global__ void __launch_bounds__(512) k_conv_strip2(const zp_conv_args A, const
   if (g & 1) group(G1{}, TL{}, koff_of(ky, cb), 0, 0);
   else group(G0{}, TL{}, koff_of(ky, cb), 0, 0);
   if (pingpong && wid < 4) __builtin_amdgcn_s_barrier();
-  conv_epilogue<T, WC, WP, NWP>(A, S, acc, p0, c0, wc, wp, lane, M, GHW, bx);
+  conv_epilogue<T, WC, WP, NWP>(A, S, acc, p0, c0, wc, wp, lane, M, GHW, bx, blockIdx.z, gridDim.z);
+}
+
+// ------------------------------------------------------------------------------------
+// k_conv_quad: the four sub-pixel phases of a stride-2 transposed structure in ONE tile.
+// ConvTranspose2d(3, s2, p1, op1) (model/aspp.py:60-80) -- and the data gradient of a 3x3 stride-2
+// conv, which geometry.py plans the same way -- is four stride-1 sub-problems over the same input
+// grid, output phase (py, px) at (2 gy + py, 2 gx + px), with 1 / 2 / 2 / 4 taps whose input offsets
+// (dy, dx) all lie in {0, 1}^2.  k_conv runs them as four independent tiles (blockIdx.z) that each
+// stage their own shifted copies of the input: 9 activation tiles per 64-channel chunk for the 9
+// (phase, tap) pairs, and the four phases of one pixel tile land on different XCDs, so the re-staging
+// goes to HBM (r01 PMC: 761 MB read per up2 launch against 85 MB algorithmic).
+// Here a workgroup owns 256 grid points (TR = 256 / W full rows) x 64 output channels x ALL FOUR
+// phases: per chunk it stages ONE strip of (TR + 1) x W input pixels (the +1 row / column of the
+// (dy, dx) = 1 taps; column W is outside the image, so the lane that would read it gets zeros by a
+// register select instead of a staged padding column) and the 9 weight taps, and every (phase, tap)
+// reads its operand from the strip at offset dy * W + dx.
+// Per chunk, 5 K steps grouped by input shift (B fragments read once per step):
+//   step 0: shift 00, phases 0, 1   step 1: shift 00, phases 2, 3   step 2: shift 01, phases 1, 3
+//   step 3: shift 10, phases 2, 3   step 4: shift 11, phase 3
+// Weights: one 8 KB LDS slot per (phase, tap) (9 slots, 72 KB); at the start of step s the slots of
+// step s - 1 are refilled with the next chunk's taps (4 steps of lead).  Strips: 2-slot ring, the
+// next chunk's strip issued at step 0.  8 waves = 2 (32 channels) x 4 (64 grid points), each holding
+// 4 phases x 2 x 4 MFMA tiles (128 accumulator registers).  Schedule (ping-pong wave groups, setprio,
+// counted vmcnt waits, XCD-aware order) as k_conv_strip2.  Epilogue: k_conv's, once per phase.
+// ------------------------------------------------------------------------------------
+struct quad_geo {
+  unsigned x_bytes, w_bytes;
+  int koff[9];  // byte offset of the slot's tap in a packed weight row: local tap index * Cin * 2
+};
+// slot -> phase (sub-problem) and input shift (host table: quad_plan)
+__host__ __device__ constexpr int quad_phase(int slot) { return slot == 0 ? 0 : slot == 1 || slot == 4 ? 1 : slot == 2 || slot == 6 ? 2 : 3; }
+
+template <typename T, int W>
+__global__ void __launch_bounds__(512) k_conv_quad(const zp_conv_args A, const quad_geo QG, const int flags) {
+  constexpr int WC = 2, WP = 4, NWP = 4;
+  constexpr int TC = 64, TP = 256, TR = TP / W;
+  constexpr int SROWS = (TR + 1) * W;    // strip rows: TR + 1 image rows of W pixels
+  constexpr int SPW = (SROWS + 63) / 64;  // strip DMA instructions per wave (8 waves x 8 rows each)
+  constexpr int SRP = 64 * SPW;
+  constexpr int WSLOT = TC * 128;         // bytes per weight slot (one tap)
+  constexpr int SBASE = 9 * WSLOT;        // strip ring after the 9 weight slots
+  constexpr int SSLOT = SRP * 128;
+  static_assert(SPW == 5, "strip of 5 DMA instructions per wave (W 32 / 64)");
+  static_assert(7 * WSLOT + 2048 < 65536 && SSLOT + W * 128 < 65536, "ds_read immediate range");
+  __shared__ uint4 lds[(9 * TC + 2 * SRP) * 8];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wid / NWP, wp = wid % NWP;
+  const int GHW = A.GH * A.GW;
+  const int M = A.N * GHW;
+  int bx = blockIdx.x, by = blockIdx.y;
+  if (flags & 2) {  // XCD-aware order: the cout tiles of one pixel tile (same strip) on one L2
+    const int total = gridDim.x * gridDim.y;
+    const int bid = blockIdx.x + gridDim.x * blockIdx.y;
+    const int xcd = bid & 7, pos = bid >> 3, q = total >> 3, r = total & 7;
+    const int lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
+    bx = lin / gridDim.y;
+    by = lin - bx * gridDim.y;
+  }
+  const int p0 = bx * TP, c0 = by * TC;
+  const int n_img = p0 / GHW, y0 = (p0 - n_img * GHW) / W;
+  const int CB = A.Cin / 64;
+  const int lrow = lane >> 3;
+
+#if defined(__HIP_DEVICE_COMPILE__)
+  const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)A.x, (short)0, (int)QG.x_bytes, 0x00020000);
+  __amdgpu_buffer_rsrc_t wrsrc[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+    wrsrc[s] = __builtin_amdgcn_make_buffer_rsrc((void*)A.sub[s].w, (short)0, (int)QG.w_bytes, 0x00020000);
+#endif
+  // weight DMA: row c0 + wid * 8 + lrow of the slot, source chunk swizzled by the row (lrow)
+  const unsigned wv = (unsigned)(((size_t)(c0 + wid * 8 + lrow) * A.k_pad + ((lane & 7) ^ lrow) * 8) * 2);
+  // strip DMA: piece i = strip rows (wid + 8 i) * 8 + lrow = (tr, x); rows past the strip or below the
+  // image read past the buffer end (zeros)
+  unsigned sv[SPW];
+#pragma unroll
+  for (int i = 0; i < SPW; ++i) {
+    const int srow = (wid + 8 * i) * 8 + lrow;
+    const int tr = srow / W, x = srow - tr * W;
+    const bool ok = srow < SROWS && y0 + tr < A.IH;
+    const int sw = (lane & 7) ^ (srow & 7);
+    sv[i] = ok ? (unsigned)((((n_img * A.IH + y0 + tr) * A.IW + x) * A.ldx + A.cx0 + sw * 8) * 2) : 0x80000000u;
+  }
+  const unsigned lds0 = lds_addr(lds);
+  unsigned aoff[2], aoff8[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    aoff[s2] = lds0 + (unsigned)(wc * 16 * WC + (lane & 15)) * 128u + (unsigned)(((s2 * 4 + (lane >> 4)) ^ (lane & 7)) * 16);
+    aoff8[s2] = aoff[s2] + 8u * WSLOT;
+  }
+  // B fragment j of the wave: grid point q = wp * 64 + 16 j + (lane & 15) -> strip row tr * W + x + dx
+  // (+ dy * W through the immediate offset, which keeps the row's swizzle); the lane at x = W - 1
+  // reads garbage for dx = 1 and is zeroed after the read
+  unsigned bo[2][2][WP];
+#pragma unroll
+  for (int dx = 0; dx < 2; ++dx)
+#pragma unroll
+    for (int j = 0; j < WP; ++j) {
+      const int q = wp * 64 + 16 * j + (lane & 15);
+      const int sr = (q / W) * W + (q % W) + dx;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+        bo[dx][s2][j] = lds0 + (unsigned)SBASE + (unsigned)sr * 128u + (unsigned)((((s2 * 4 + (lane >> 4)) ^ (sr & 7))) * 16);
+    }
+  const bool edge = (lane & 15) == 15;  // x = W - 1 in fragments j = 3 (W 64) / j odd (W 32)
+  // the strip slot of the current chunk alternates: bo moves between the two slots once per chunk
+  // (a runtime parity keeps ONE loop body and one tail, so the 128 accumulators stay in place)
+  int sdelta = SSLOT;
+  auto flip = [&]() {
+#pragma unroll
+    for (int dx = 0; dx < 2; ++dx)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int j = 0; j < WP; ++j) bo[dx][s2][j] += (unsigned)sdelta;
+    sdelta = -sdelta;
+  };
+
+  auto issue_w = [&](int slot, int cb) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    auto* d = (__attribute__((address_space(3))) void*)&lds[(slot * TC + wid * 8) * 8];
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(wrsrc[quad_phase(slot)], d, 16, wv, QG.koff[slot] + cb * 128, 0, 0);
+#endif
+  };
+  auto issue_s = [&](int gslot, int cb) {
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+    for (int i = 0; i < SPW; ++i) {
+      auto* d = (__attribute__((address_space(3))) void*)&lds[(9 * TC + gslot * SRP + (wid + 8 * i) * 8) * 8];
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrsrc, d, 16, sv[i], cb * 128, 0, 0);
+    }
+#endif
+  };
+
+  f32x4 acc[4][WC][WP];
+#pragma unroll
+  for (int ph = 0; ph < 4; ++ph)
+#pragma unroll
+    for (int i = 0; i < WC; ++i)
+#pragma unroll
+      for (int j = 0; j < WP; ++j) acc[ph][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // one K step S of chunk cb (strip slot gp); STEADY: a next chunk exists (prefetches issued)
+  auto step = [&](auto s_c, auto steady_c, int cb, int gp) {
+    constexpr int S = decltype(s_c)::value;
+    constexpr bool STEADY = decltype(steady_c)::value;
+    constexpr int NT = S == 4 ? 1 : 2;
+    constexpr int DY = (S == 3 || S == 4) ? 1 : 0, DX = (S == 2 || S == 4) ? 1 : 0;
+    if constexpr (ZP_ABL == 1) {  // diagnostic build: no DMA in the loop
+    } else if constexpr (S == 0) {
+      issue_w(8, cb);
+      if constexpr (STEADY) issue_s(gp ^ 1, cb + 1);
+    } else if constexpr (STEADY) {
+      issue_w(2 * (S - 1), cb + 1);
+      issue_w(2 * (S - 1) + 1, cb + 1);
+    }
+    uint4 af[NT][2][WC], bfr[2][WP];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      static_for<NT>([&](auto t) {
+        constexpr int SL = 2 * S + decltype(t)::value;
+        static_for<WC>([&](auto i) {
+          if constexpr (SL < 8) af[t][s2][i] = ds_read16<SL * WSLOT + i * 2048>(aoff[s2]);
+          else af[t][s2][i] = ds_read16<i * 2048>(aoff8[s2]);
+        });
+      });
+      static_for<WP>([&](auto j) { bfr[s2][j] = ds_read16<DY * W * 128>(bo[DX][s2][j]); });
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (DX == 1) {
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int j = 0; j < WP; ++j)
+          if (W == 32 ? (j & 1) : (j == 3)) {
+            bfr[s2][j].x = edge ? 0u : bfr[s2][j].x;
+            bfr[s2][j].y = edge ? 0u : bfr[s2][j].y;
+            bfr[s2][j].z = edge ? 0u : bfr[s2][j].z;
+            bfr[s2][j].w = edge ? 0u : bfr[s2][j].w;
+          }
+    }
+    // loads allowed in flight at the end of this step (issued after what the next step reads)
+    auto wait_out = [&]() {
+      if constexpr (STEADY) {
+        if constexpr (S <= 2) vm_wait<5 + SPW>();
+        else if constexpr (S == 3) vm_wait<6 + SPW>();
+        else vm_wait<6>();
+      } else {
+        if constexpr (S == 0) vm_wait<5>();
+        else if constexpr (S == 1) vm_wait<3>();
+        else if constexpr (S == 2) vm_wait<1>();
+        else vm_wait<0>();
+      }
+    };
+    // ping-pong: the two wave groups run one barrier apart (the second group's extra prologue
+    // barrier), so one group's MFMAs overlap the other's LDS reads
+    wait_out();
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    static_for<NT>([&](auto t) {
+      constexpr int PH = quad_phase(2 * S + decltype(t)::value);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int i = 0; i < WC; ++i)
+#pragma unroll
+          for (int j = 0; j < WP; ++j) {
+            if constexpr (ZP_ABL != 2) MfmaTraits<T>::mma(acc[PH][i][j], af[t][s2][i], bfr[s2][j]);
+            else acc[PH][i][j][0] += __uint_as_float(af[t][s2][i].x ^ bfr[s2][j].y);  // diagnostic: no MFMA
+          }
+    });
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  using ST = std::integral_constant<bool, true>;
+  using TL = std::integral_constant<bool, false>;
+  auto chunk = [&](auto steady_c, int cb) {
+    const int gp = cb & 1;
+    step(std::integral_constant<int, 0>{}, steady_c, cb, gp);
+    step(std::integral_constant<int, 1>{}, steady_c, cb, gp);
+    step(std::integral_constant<int, 2>{}, steady_c, cb, gp);
+    step(std::integral_constant<int, 3>{}, steady_c, cb, gp);
+    step(std::integral_constant<int, 4>{}, steady_c, cb, gp);
+    flip();
+  };
+  // prologue: strip of chunk 0, then the weights of slots 0..7 (slot 8 is issued by step 0)
+  issue_s(0, 0);
+#pragma unroll
+  for (int sl = 0; sl < 8; ++sl) issue_w(sl, 0);
+  vm_wait<6>();  // strip(0) and slots 0, 1 landed
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  if (wid >= 4) __builtin_amdgcn_s_barrier();
+  for (int cb = 0; cb < CB - 1; ++cb) chunk(ST{}, cb);
+  chunk(TL{}, CB - 1);
+  if (wid < 4) __builtin_amdgcn_s_barrier();
+  if constexpr (ZP_ABL == 5) {  // diagnostic build: no epilogue (one store only if a sum is exactly 1)
+    float sm = 0.f;
+    static_for<4>([&](auto ph) {
+#pragma unroll
+      for (int i = 0; i < WC; ++i)
+#pragma unroll
+        for (int j = 0; j < WP; ++j) sm += acc[ph][i][j][0] + acc[ph][i][j][1] + acc[ph][i][j][2] + acc[ph][i][j][3];
+    });
+    if (sm == 1.f) ((float*)A.sub[0].y)[tid] = sm;
+  } else {
+    static_for<4>([&](auto ph) {
+      conv_epilogue<T, WC, WP, NWP>(A, A.sub[ph], acc[ph], p0, c0, wc, wp, lane, M, GHW, bx, ph, 4);
+    });
+  }
 }
 
 // ------------------------------------------------------------------------------------
@@ -1907,6 +2165,8 @@ static int g_tc256_min_blocks = 1024;
 // workgroups: 78.7 us vs 70.7 us on the 128-channel tile) and on the ASPP launch, whose four
 // sub-problems (1 vs 9 taps) are too unbalanced for 512 large tiles.
 static bool strip_eligible(const zp_conv_args& a, strip_geo* sg);
+static bool quad_plan(const zp_conv_args& a, quad_geo* qg);
+static int g_quad_min_blocks = 256;  // zp_conv_tuning key 6: fewest workgroups k_conv_quad runs with
 static int g_strip_c64 = 1;  // zp_conv_tuning key 2: 64-channel layers on the strip kernel (TC 64; 27.5 -> 22.2 us at 64x64)
 // strip tile width: 128 channels, or 64 when 128-channel tiles would leave part of the 256 CUs
 // idle (128 -> 128 at 32x32, bs 32: 128 workgroups; 24.2 -> 22.7 us).  64-channel layers stay on
@@ -1920,6 +2180,7 @@ static int strip_tc(const zp_conv_args& a) {
   return 128;
 }
 static int conv_tc(const zp_conv_args& a) {
+  if (quad_plan(a, nullptr)) return 64;  // k_conv_quad: 64 channels x 4 phases
   // strip-eligible layers take k_conv_strip's 128-channel tile: it stages fewer bytes per FLOP than
   // the 256-channel k_conv tile, and a 256-channel strip tile does not fit the register file
   // (35 spilled VGPRs)
@@ -1947,12 +2208,13 @@ static int conv_stages_override() {
 // conv schedule switches: bit 1 XCD-aware tile order, bit 2 s_setprio(1) around the MFMA
 // cluster, bit 3 ping-pong (staggered wave groups), bit 4 tap-row trimming (tap rows that read only
 // padding for a whole tile are skipped), bit 5 spread strip DMA (k_conv_strip only; slower), bit 6
-// k_conv_strip2 instead of k_conv_strip.  Default (measured, profiles/r01_conv_sweep.md,
+// k_conv_strip2 instead of k_conv_strip, bit 7 k_conv_quad for the four phases of stride-2 transposed
+// structures (ConvTranspose2d forward, stride-2 conv data gradient).  Default (measured, profiles/r01_conv_sweep.md,
 // profiles/r02_conv_ab.md): XCD order + setprio + ping-pong + trimming + k_conv_strip2 (94).
 // ZP_CONV_FLAGS / zp_conv_tuning(1, .) override for sweeps.
 static int g_conv_flags = -1;  // zp_conv_tuning key 1 (runtime A/B in one process); -1 = env / default
 static int conv_flags() {
-  static const int v = getenv("ZP_CONV_FLAGS") ? env_int("ZP_CONV_FLAGS") : 94;
+  static const int v = getenv("ZP_CONV_FLAGS") ? env_int("ZP_CONV_FLAGS") : 94 + 128;
   return g_conv_flags >= 0 ? g_conv_flags : v;
 }
 
@@ -1995,6 +2257,38 @@ static bool strip_eligible(const zp_conv_args& a, strip_geo* sg) {
   return true;
 }
 
+// k_conv_quad eligibility: 16-bit, the four phases (py, px) = (0,0), (0,1), (1,0), (1,1) of a
+// stride-2 transposed structure over an input the size of the grid (W 32 / 64), 1 / 2 / 2 / 4 taps
+// at input offsets in {0,1}^2 (geometry.py _phases with k = 3, p = 1), channels in whole chunks, and
+// enough workgroups to cover the CUs.  qg: the byte offset of each schedule slot's tap.
+static bool quad_plan(const zp_conv_args& a, quad_geo* qg) {
+  if (!(conv_flags() & 128)) return false;
+  if (a.dtype == ZP_F32 || a.nsub != 4 || a.Cin % 64 != 0 || a.Cout % 64 != 0) return false;
+  if (a.sy != 1 || a.sx != 1 || a.GH != a.IH || a.GW != a.IW) return false;
+  if (a.GW != 32 && a.GW != 64) return false;
+  if (((long)a.GH * a.GW) % 256 != 0) return false;
+  if ((long)a.N * a.GH * a.GW / 256 * (a.Cout / 64) < g_quad_min_blocks) return false;
+  static const int ntap[4] = {1, 2, 2, 4};
+  for (int s = 0; s < 4; ++s) {
+    const zp_conv_sub& S = a.sub[s];
+    if (S.oys != 2 || S.oxs != 2 || S.oyo != s / 2 || S.oxo != s % 2 || S.ntaps != ntap[s]) return false;
+    if (S.OH < 2 * a.GH || S.OW < 2 * a.GW) return false;
+  }
+  // slot -> (ty, tx) (the sub is quad_phase(slot))
+  static const int shift[9][2] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 1}, {0, 1}, {1, 0}, {1, 0}, {1, 1}};
+  int used[4] = {0, 0, 0, 0};
+  for (int k = 0; k < 9; ++k) {
+    const int ph = quad_phase(k);
+    const zp_conv_sub& S = a.sub[ph];
+    int t = 0;
+    while (t < S.ntaps && !(S.ty[t] == shift[k][0] && S.tx[t] == shift[k][1])) ++t;
+    if (t == S.ntaps || (used[ph] >> t) & 1) return false;
+    used[ph] |= 1 << t;
+    if (qg) qg->koff[k] = t * a.Cin * 2;
+  }
+  return true;
+}
+
 // pixel tile: 256 (8 waves) whenever the cout tile allows it.  Measured on MI355X (R34 bs32,
 // profiles/r01_conv_sweep.md): the 8-wave 3-stage tile beats the 4-wave tiles even on the
 // 32x32 layers where it leaves part of the chip idle (fewer workgroups, but 2x the MFMA work
@@ -2002,7 +2296,7 @@ static bool strip_eligible(const zp_conv_args& a, strip_geo* sg) {
 static int conv_tp(const zp_conv_args& a) {
   int tc = a.Cout > 64 ? 128 : (a.Cout > 32 ? 64 : 32);
   if (tc == 32) return 128;  // 32 + 256 rows do not split over 8 waves in 8-row groups
-  if (strip_eligible(a, nullptr)) return 256;
+  if (strip_eligible(a, nullptr) || quad_plan(a, nullptr)) return 256;
   if (conv_tc(a) == 256) return 256;  // the 256-channel tile exists only with 256-pixel tiles
   const int ov = conv_tp_override();
   if (ov == 128 || ov == 256) return ov;
@@ -2129,6 +2423,24 @@ extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
       else hipLaunchKernelGGL((k_conv_strip<bf16_t, 4, 3, 5>), grid, dim3(512), 0, st, a, sg, fl);
     }
     ZP_LAUNCH_CHECK("zp_conv2d strip");
+    return ZP_OK;
+  }
+  quad_geo qg{};
+  if (quad_plan(a, &qg)) {
+    qg.x_bytes = tg.x_bytes;
+    qg.w_bytes = tg.w_bytes[0];
+    const int qgx = (int)(((long)a.N * a.GH * a.GW) / 256);
+    const dim3 grid(qgx, gy, 1);
+    ZP_CHECK_ARG(!a.stats || 4 * 4 * qgx == zp_conv2d_stat_parts(&a),
+                 "zp_conv2d: quad launch emits %d stat parts, zp_conv2d_stat_parts says %d", 16 * qgx,
+                 zp_conv2d_stat_parts(&a));
+    const int fl = conv_flags();
+#define ZP_QUAD(T)                                                                             \
+  if (a.GW == 32) hipLaunchKernelGGL((k_conv_quad<T, 32>), grid, dim3(512), 0, st, a, qg, fl); \
+  else hipLaunchKernelGGL((k_conv_quad<T, 64>), grid, dim3(512), 0, st, a, qg, fl);
+    if (a.dtype == ZP_F16) { ZP_QUAD(f16_t) } else { ZP_QUAD(bf16_t) }
+#undef ZP_QUAD
+    ZP_LAUNCH_CHECK("zp_conv2d quad");
     return ZP_OK;
   }
   const int nwp = conv_tp(a) / 64;
@@ -2348,7 +2660,7 @@ extern "C" int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* st
   *tc = conv_tc(*a);
   *tp = conv_tp(*a);
   *stages = *tc == 256 ? 2 : conv_stages(*a, *tc);
-  *variant = *tc <= 128 && strip_eligible(*a, nullptr) ? ((conv_flags() & 64) ? 2 : 1) : 0;
+  *variant = quad_plan(*a, nullptr) ? 3 : *tc <= 128 && strip_eligible(*a, nullptr) ? ((conv_flags() & 64) ? 2 : 1) : 0;
   return ZP_OK;
 }
 
@@ -2356,7 +2668,8 @@ extern "C" int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* st
  * (default 1024); key 1: conv schedule flags (-1 = ZP_CONV_FLAGS / default); key 2: 64-channel
  * layers on the strip kernel (default 1); key 3: k_wgrad2 (default 1); key 4: k_wgrad2's
  * workgroup rounds over the CUs (default 1); key 5: k_wgrad_lds's workgroup rounds (default 1; 0 =
- * the older ~1024-workgroup target padded to a multiple of 8).  Returns the previous value. */
+ * the older ~1024-workgroup target padded to a multiple of 8); key 6: the fewest workgroups
+ * k_conv_quad runs with (default 256).  Returns the previous value. */
 extern "C" int zp_conv_tuning(int key, int value) {
   if (key == 0) {
     const int old = g_tc256_min_blocks;
@@ -2381,6 +2694,11 @@ extern "C" int zp_conv_tuning(int key, int value) {
   if (key == 5) {
     const int old = g_wgrad_lds_rounds;
     g_wgrad_lds_rounds = value >= 0 ? value : 1;
+    return old;
+  }
+  if (key == 6) {
+    const int old = g_quad_min_blocks;
+    g_quad_min_blocks = value;
     return old;
   }
   if (key == 4) {

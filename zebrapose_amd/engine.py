@@ -244,6 +244,8 @@ class Engine:
             tn = {L.ZP_F32: "f32", L.ZP_BF16: "bf16", L.ZP_F16: "f16"}[self.dt]
             if var.value == 1:  # rocprofv3 name: k_conv_strip<T, WC, STAGES, SPW = 5>
                 kname = f"k_conv_strip<{tn},WC={tc.value // 32},ST=3>"
+            elif var.value == 3:  # rocprofv3 name: k_conv_quad<T, W>
+                kname = f"k_conv_quad<{tn},W={plan.GW}>"
             elif var.value == 2:  # rocprofv3 name: k_conv_strip2<T, WC, SPW = 5>
                 kname = f"k_conv_strip2<{tn},WC={tc.value // 32}>"
             else:  # rocprofv3 name: k_conv<T, WC = tc / 32, WP = 4, NWP = tp / 64, STAGES, smallC>
