@@ -1046,7 +1046,8 @@ __global__ void __launch_bounds__(512) k_conv_strip2(const zp_conv_args A, const
     using K0 = std::integral_constant<int, N0>;
     using K1 = std::integral_constant<int, N0 + N1>;
     using KS = std::integral_constant<int, SPW>;
-    if constexpr (!SPREAD) {
+    if constexpr (ZP_ABL == 1) {  // diagnostic build: no DMA in the loop
+    } else if constexpr (!SPREAD) {
       if constexpr (PH == 0) {
         issue_w(2, koff_cur + 2 * cin2);
       } else if constexpr (STEADY && PH == 1) {
@@ -1166,7 +1167,16 @@ __global__ void __launch_bounds__(512) k_conv_strip2(const zp_conv_args A, const
   if (g & 1) group(G1{}, TL{}, koff_of(ky, cb), 0, 0);
   else group(G0{}, TL{}, koff_of(ky, cb), 0, 0);
   if (pingpong && wid < 4) __builtin_amdgcn_s_barrier();
-  conv_epilogue<T, WC, WP, NWP>(A, S, acc, p0, c0, wc, wp, lane, M, GHW, bx, blockIdx.z, gridDim.z);
+  if constexpr (ZP_ABL == 5) {  // diagnostic build: no epilogue (one store only if a sum is exactly 1)
+    float sm = 0.f;
+#pragma unroll
+    for (int i = 0; i < WC; ++i)
+#pragma unroll
+      for (int j = 0; j < WP; ++j) sm += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+    if (sm == 1.f) ((float*)S.y)[tid] = sm;
+  } else {
+    conv_epilogue<T, WC, WP, NWP>(A, S, acc, p0, c0, wc, wp, lane, M, GHW, bx, blockIdx.z, gridDim.z);
+  }
 }
 
 // ------------------------------------------------------------------------------------
