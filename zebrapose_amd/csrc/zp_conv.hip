@@ -94,6 +94,18 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
+// Sum over the 16 lanes of each DPP row (lanes 16k .. 16k + 15), the total in every lane of the row:
+// quad_perm xor 1, xor 2, then row_half_mirror and row_mirror -- the same pairing tree as
+// __shfl_xor over 1, 2, 4, 8 (bit-identical sums) as four DPP adds instead of four ds_bpermute
+// round trips through the LDS crossbar.
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));  // row_half_mirror
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false));  // row_mirror
+  return v;
+}
+
 // Conv epilogue shared by k_conv and k_conv_strip: BN scale/shift (+bias), residual, ReLU,
 // NHWC (channel slice) / NCHW-head / f32 stores, or train-mode BN partial statistics.
 template <typename T, int WC, int WP, int NWP>
@@ -279,8 +291,7 @@ __device__ __forceinline__ void conv_epilogue(const zp_conv_args& A, const zp_co
     float cnt = 0.f;
 #pragma unroll
     for (int j = 0; j < WP; ++j) cnt += (p0 + wp * 16 * WP + j * 16 + (lane & 15) < M) ? 1.f : 0.f;
-#pragma unroll
-    for (int off = 1; off < 16; off <<= 1) cnt += __shfl_xor(cnt, off);
+    cnt = row16_sum(cnt);
 #pragma unroll
     for (int i = 0; i < WC; ++i)
 #pragma unroll
@@ -295,8 +306,7 @@ __device__ __forceinline__ void conv_epilogue(const zp_conv_args& A, const zp_co
           vv[j] = ok ? v : 0.f;
           sm += vv[j];
         }
-#pragma unroll
-        for (int off = 1; off < 16; off <<= 1) sm += __shfl_xor(sm, off);
+        sm = row16_sum(sm);
         const float mean = cnt > 0.f ? sm / cnt : 0.f;
         float m2 = 0.f;
 #pragma unroll
@@ -305,8 +315,7 @@ __device__ __forceinline__ void conv_epilogue(const zp_conv_args& A, const zp_co
           const float dlt = vv[j] - mean;
           m2 += ok ? dlt * dlt : 0.f;
         }
-#pragma unroll
-        for (int off = 1; off < 16; off <<= 1) m2 += __shfl_xor(m2, off);
+        m2 = row16_sum(m2);
         const int c = cbase + i * 16 + r;
         if ((lane & 15) == 0 && c < A.Cout) {
           A.stats[(size_t)part * A.Cout + c] = cnt;
