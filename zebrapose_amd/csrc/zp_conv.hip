@@ -291,7 +291,12 @@ __device__ __forceinline__ void conv_epilogue(const zp_conv_args& A, const zp_co
     float cnt = 0.f;
 #pragma unroll
     for (int j = 0; j < WP; ++j) cnt += (p0 + wp * 16 * WP + j * 16 + (lane & 15) < M) ? 1.f : 0.f;
-    cnt = row16_sum(cnt);
+    if constexpr (sizeof(T) == 2) {
+          cnt = row16_sum(cnt);
+        } else {  // f32 parity mode: DPP temporaries pushed this 128-accumulator tile past 256 VGPRs
+#pragma unroll
+          for (int off = 1; off < 16; off <<= 1) cnt += __shfl_xor(cnt, off);
+        }
 #pragma unroll
     for (int i = 0; i < WC; ++i)
 #pragma unroll
@@ -306,7 +311,12 @@ __device__ __forceinline__ void conv_epilogue(const zp_conv_args& A, const zp_co
           vv[j] = ok ? v : 0.f;
           sm += vv[j];
         }
-        sm = row16_sum(sm);
+        if constexpr (sizeof(T) == 2) {
+          sm = row16_sum(sm);
+        } else {  // f32 parity mode: DPP temporaries pushed this 128-accumulator tile past 256 VGPRs
+#pragma unroll
+          for (int off = 1; off < 16; off <<= 1) sm += __shfl_xor(sm, off);
+        }
         const float mean = cnt > 0.f ? sm / cnt : 0.f;
         float m2 = 0.f;
 #pragma unroll
@@ -315,7 +325,12 @@ __device__ __forceinline__ void conv_epilogue(const zp_conv_args& A, const zp_co
           const float dlt = vv[j] - mean;
           m2 += ok ? dlt * dlt : 0.f;
         }
-        m2 = row16_sum(m2);
+        if constexpr (sizeof(T) == 2) {
+          m2 = row16_sum(m2);
+        } else {  // f32 parity mode: DPP temporaries pushed this 128-accumulator tile past 256 VGPRs
+#pragma unroll
+          for (int off = 1; off < 16; off <<= 1) m2 += __shfl_xor(m2, off);
+        }
         const int c = cbase + i * 16 + r;
         if ((lane & 15) == 0 && c < A.Cout) {
           A.stats[(size_t)part * A.Cout + c] = cnt;
