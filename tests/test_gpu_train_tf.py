@@ -1,0 +1,369 @@
+"""Teacher-forced parity of one bf16 TRAINING step (BASELINE.json configs[2]: train_v6.py:319-338,
+ResNet34 + DeepLabv3, bs=32, 256x256) through TrainStep and libzp.so, and of the same step at
+64x64, B=2.
+
+Why teacher-forced.  The random-weight network amplifies a 1-ulp bf16 difference anywhere into
+percent-level gradient differences at the far end (tests/test_gpu_bench_geometry.py measures the
+forward; the backward chain is longer), so an end-to-end comparison of a bf16 step against any
+oracle is a norm band that cannot tell a kernel bug from rounding.  Instead every op of the step
+is replayed on the host from the device's OWN stored 16-bit inputs, with the device's storage
+roundings (oracle/ref_cpu.py lp_conv for the convs), and its stored output must agree:
+
+  forward, per train-mode conv + BatchNorm unit (engine tape):
+    raw conv output  (bf16)    within 1 bf16 ulp (+ 2^-12 of the layer rms for cancelling sums)
+    batch mean / invstd        within 1e-4 (relative to the channel std) of the f64 statistics of
+                               the stored raw values over ALL crops
+    running mean / var         momentum update of those statistics (train_v6.py / torch BN), 1e-4
+    BN+residual+ReLU output    fma(raw, scale, shift) [+ res] [relu] from the device's own
+                               scale / shift: within 1 ulp
+    maxpool / avgpool / image-pool broadcast / head   as tests/test_gpu_bench_geometry.py
+  loss (BinaryCodeNet.py:8-93 on the device's logits):  loss_b 1e-12, loss_m 1e-6, histogram
+    exact, d loss / d logits to 1e-5 (f64 oracle, ref_cpu.binary_code_loss / mask_loss)
+  backward, per unit (engine.bwd_trace, reverse order):
+    head gradient NHWC bf16     exact conversion of d loss / d logits
+    BN backward sums (dbeta = sum g, dgamma = sum g xhat)  within 1e-5 of the f64 sums' absolute
+                                mass, over ALL crops (ReLU mask from the raw output / the stored
+                                activation, as the device picks)
+    d raw (bf16)                gamma invstd (g - mean g - xhat mean(g xhat)): within 1 ulp
+    residual gradient (bf16)    before + g: within 1 ulp
+    weight gradient (f32)       sum over ALL crops of x (x) d raw, 8 output channels per layer:
+                                within 2e-5 of the absolute mass |x| (x) |d raw|
+    input gradient (bf16)       (accumulated) data gradient: within 1 ulp
+    maxpool / avgpool / broadcast backward: within 1 ulp (maxpool: first maximum, as torch)
+  optimizer: the parameters after FusedAdam = torch.optim.Adam's first step from the device's
+    gradients, 1e-5.
+
+Per-crop ops are replayed for sampled crops (all crops at B=2); batch-wide sums use every crop.
+Reference anchors: model/BinaryCodeNet.py:8-93, 161-174, resnet.py:20-51, aspp.py:60-114,
+train_v6.py:319-338.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+THR = np.float32(8.940696716308594e-08)
+GEOMS = [(2, 64, (0, 1), "r34_bn_buffers.npz"), (32, 256, (0, 13, 31), "r34_bn_buffers256.npz")]
+
+
+def _ulp(v):
+    a = v.abs().clamp_min(2.0 ** -126)
+    return torch.pow(2.0, torch.floor(torch.log2(a)) - 7)
+
+
+def _q(t):
+    return t.to(torch.bfloat16).to(torch.float32)
+
+
+def _h(a, b=None):
+    """Act (or [B,H,W,C] tensor) -> f32 NCHW host tensor, crop b or all crops."""
+    t = a.buf[..., a.c0:a.c0 + a.C] if hasattr(a, "buf") else a
+    t = t if b is None else t[b:b + 1]
+    return t.permute(0, 3, 1, 2).float().cpu()
+
+
+class Checker:
+    def __init__(self):
+        self.worst_frac, self.worst_ulp, self.n = 0.0, 0.0, 0
+
+    def bf16(self, label, exp, got, max_frac=0.005):
+        assert exp.shape == got.shape, (label, exp.shape, got.shape)
+        d = (got - exp).abs()
+        rms = float(exp.pow(2).mean().sqrt()) if exp.numel() else 0.0
+        ulp = _ulp(torch.maximum(exp.abs(), got.abs()))
+        bad = d > ulp + 2.0 ** -12 * rms
+        frac = float((d > 0).float().mean()) if d.numel() else 0.0
+        self.worst_frac = max(self.worst_frac, frac)
+        if d.numel():
+            self.worst_ulp = max(self.worst_ulp, float((d / ulp).max()))
+        self.n += 1
+        assert not bool(bad.any()), f"{label}: {int(bad.sum())} elements beyond 1 ulp, max |d| {float(d.max()):.3g} rms {rms:.3g}"
+        assert frac <= max_frac, (label, frac)
+
+    def sums(self, label, got, exp, mass, rel=1e-5):
+        got, exp, mass = got.double().cpu(), exp.double().cpu(), mass.double().cpu()
+        d = (got - exp).abs()
+        ok = d <= rel * mass + 1e-30
+        assert bool(ok.all()), f"{label}: max |d|/mass {float((d / mass.clamp_min(1e-30)).max()):.3g}"
+
+
+def _conv_fwd(unit, x, w, transposed):
+    if transposed:
+        return F.conv_transpose2d(x, w, None, 2, 1, 1)
+    return F.conv2d(x, w, None, unit.s, unit.p, unit.d)
+
+
+def _conv_dgrad(unit, xshape, w, g):
+    if unit.kind == "convT":  # adjoint of conv_transpose2d(stride 2, padding 1) is conv2d(stride 2, padding 1)
+        return F.conv2d(g, w, None, 2, 1)
+    return torch.nn.grad.conv2d_input(xshape, w, g, unit.s, unit.p, unit.d)
+
+
+def _conv_wgrad(unit, x, g, sel):
+    """weight gradient of the output channels ``sel`` (f32, host), summed over the crops of x / g."""
+    w = torch.zeros(unit.conv.weight.shape)  # values do not enter the weight gradient
+    ws = (w[:, sel] if unit.kind == "convT" else w[sel]).clone().requires_grad_(True)
+    y = _conv_fwd(unit, x, ws, unit.kind == "convT")
+    y.backward(g[:, sel])
+    return ws.grad
+
+
+def _mask_mode(unit, res):
+    return (2 if res is None else 1) if unit.relu else 0
+
+
+@pytest.fixture(scope="module", params=GEOMS, ids=["b2_64", "b32_256"])
+def step(request, golden):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from oracle import ref_cpu
+    from zebrapose_amd.model.BinaryCodeNet import BinaryCodeNet_Deeplab
+    from zebrapose_amd.train import TrainStep
+    B, S, sample, bnfile = request.param
+    sd = ref_cpu.synthetic_state(34, 16, 0, dict(golden(bnfile)))
+    net = BinaryCodeNet_Deeplab(34, 16, 2, concat=True, output_kernel_size=1, precision="bf16")
+    net.load_state_dict(sd)
+    net = net.cuda().train()
+    g = torch.Generator().manual_seed(7)
+    u8 = torch.randint(0, 256, (B, 3, S, S), generator=g, dtype=torch.uint8)
+    mean = torch.tensor([0.485, 0.456, 0.406]).view(1, 3, 1, 1)
+    std = torch.tensor([0.229, 0.224, 0.225]).view(1, 3, 1, 1)
+    x = ((u8.float() / 255.0 - mean) / std).cuda()
+    gt_code = torch.randint(0, 2, (B, 16, S // 2, S // 2), generator=g, dtype=torch.uint8).cuda()
+    gt_mask = torch.randint(0, 2, (B, S // 2, S // 2), generator=g).float().cuda()
+    params0 = {k: v.detach().float().cpu().clone() for k, v in net.named_parameters()}
+    # the step's forward and backward ran on these (Adam has updated the parameters since)
+    w0 = {id(v): params0[k] for k, v in net.named_parameters()}
+    buffers0 = {k: v.detach().cpu().clone() for k, v in net.named_buffers()}
+    ts = TrainStep(net, learning_rate=2e-4)
+    eng = net.net._engine
+    eng.bwd_trace = []
+    try:
+        loss, loss_b, loss_m = ts(x, gt_code, gt_mask)
+        torch.cuda.synchronize()
+        rec = dict(net=net, ts=ts, x=x, gt_code=gt_code, gt_mask=gt_mask, params0=params0, buffers0=buffers0,
+                   loss=(loss, loss_b, loss_m), w0=w0, fwd=eng.last_fwd, head_grads=eng.last_head_grads,
+                   bwd=list(eng.bwd_trace), B=B, S=S, sample=sample)
+    finally:
+        eng.bwd_trace = None
+    yield rec
+    eng.last_fwd = eng.last_head_grads = None
+
+
+def test_train_forward_teacher_forced(step):
+    from oracle import ref_cpu
+    net, fwd, sample, B = step["net"], step["fwd"], step["sample"], step["B"]
+    named_buf = dict(net.named_buffers())
+    buffers0 = step["buffers0"]
+    name_of = {id(m): n for n, m in net.named_modules()}
+    ck = Checker()
+    n_bn = 0
+    for i, rec in enumerate(fwd["tape"].recs):
+        kind = rec[0]
+        if kind == "bn":
+            _, unit, x, out, res, raw, save = rec
+            n_bn += 1
+            lab = f"{i}:{unit.kind} k{unit.k} s{unit.s} d{unit.d} {unit.cin_w}->{unit.cout} {x.H}x{x.W}"
+            w = step["w0"][id(unit.conv.weight)]
+            C = unit.cout
+            sv = save.detach().cpu()
+            mean_d, inv_d, sc, sh = sv[:C], sv[C:2 * C], sv[2 * C:3 * C], sv[3 * C:]
+            # batch statistics over all crops (f64 of the stored raw values)
+            r64 = raw.double()
+            m64 = r64.mean((0, 1, 2))
+            v64 = (r64 - m64).pow(2).mean((0, 1, 2))
+            sd64 = v64.sqrt().clamp_min(1e-12)
+            assert float(((mean_d.double() - m64.cpu()).abs() / sd64.cpu()).max()) <= 1e-4, (lab, "mean")
+            inv_ref = 1.0 / torch.sqrt(v64.cpu() + unit.bn.eps)
+            assert float(((inv_d.double() - inv_ref).abs() / inv_ref).max()) <= 1e-4, (lab, "invstd")
+            # running statistics (momentum 0.1, unbiased variance; the conv bias sits in the mean)
+            bname = name_of[id(unit.bn)]
+            P = raw.shape[0] * raw.shape[1] * raw.shape[2]
+            mt = m64.cpu() + (0 if unit.conv.bias is None else unit.conv.bias.detach().double().cpu())
+            rm_exp = 0.9 * buffers0[bname + ".running_mean"].double() + 0.1 * mt
+            rv_exp = 0.9 * buffers0[bname + ".running_var"].double() + 0.1 * v64.cpu() * P / (P - 1)
+            rm = named_buf[bname + ".running_mean"].detach().double().cpu()
+            rv = named_buf[bname + ".running_var"].detach().double().cpu()
+            # (+ the f32 rounding of the stored running mean itself)
+            rm_tol = 1e-4 * 0.1 * sd64.cpu() + 1e-6 * rm_exp.abs() + 1e-7
+            assert bool(((rm - rm_exp).abs() <= rm_tol).all()), (lab, "running_mean", float((rm - rm_exp).abs().max()))
+            assert float(((rv - rv_exp).abs() / rv_exp.abs().clamp_min(1e-6)).max()) <= 1e-4, (lab, "running_var")
+            assert int(named_buf[bname + ".num_batches_tracked"]) == int(buffers0[bname + ".num_batches_tracked"]) + 1
+            for b in sample:
+                xin = _h(x, b)[:, :unit.cin_w]
+                exp_raw = ref_cpu.lp_conv(xin, w, None, None, None, False, stride=unit.s, pad=unit.p, dil=unit.d,
+                                          transposed=unit.kind == "convT")
+                got_raw = _h(raw, b)
+                ck.bf16(f"crop {b} {lab} raw", exp_raw, got_raw)
+                # BN apply from the device's own raw values and scale / shift
+                y = (got_raw.double() * sc.double().view(1, -1, 1, 1) + sh.double().view(1, -1, 1, 1)).float()
+                if res is not None:
+                    y = y + _h(res, b)
+                if unit.relu:
+                    y = F.relu(y)
+                ck.bf16(f"crop {b} {lab} bn-apply", _q(y), _h(out, b), max_frac=1e-4)
+        elif kind == "maxpool":
+            _, xa, pa = rec
+            for b in sample:
+                ck.bf16(f"crop {b} maxpool", F.max_pool2d(_h(xa, b), 3, 2, 1), _h(pa, b), max_frac=0.0)
+        elif kind == "avgpool":
+            _, xa, pa = rec
+            for b in sample:
+                m = _h(xa, b).double().mean((2, 3), keepdim=True).float()
+                ck.bf16(f"crop {b} avgpool", _q(m), _h(pa, b), max_frac=0.0)
+        elif kind == "broadcast":
+            _, src, dst = rec
+            for b in sample:
+                ck.bf16(f"crop {b} broadcast", _h(src, b).expand(-1, -1, dst.H, dst.W), _h(dst, b), max_frac=0.0)
+        elif kind == "head":
+            _, unit, x, key, _, _, _ = rec
+            w = step["w0"][id(unit.conv.weight)]
+            bias = step["w0"][id(unit.conv.bias)]
+            for b in sample:
+                exp = ref_cpu.lp_conv(_h(x, b), w, None, bias, None, False, out_f32=True)
+                got = torch.cat([fwd["mask"][b:b + 1].detach().cpu(), fwd["code"][b:b + 1].detach().cpu()], 1)
+                scale = float(exp.abs().max())
+                assert float((got - exp).abs().max()) <= 2e-5 * max(scale, 1.0), ("head", b)
+        else:
+            raise AssertionError(f"unexpected tape record {kind}")
+    # stem 1 + layer1 6 + layer2 9 + layer4 13 + layer5 7 + ASPP 6 (4 branches, image pool, projection)
+    # + decoder 2 x 3
+    assert n_bn == 48, n_bn
+    print(f"train forward teacher-forced: {len(fwd['tape'].recs)} ops; worst not-bit-identical {ck.worst_frac:.4f}, "
+          f"worst {ck.worst_ulp:.2f} ulp")
+
+
+def test_train_loss_matches_oracle_on_device_logits(step):
+    from oracle import ref_cpu
+    fwd, (loss, loss_b, loss_m) = step["fwd"], step["loss"]
+    ml = fwd["mask"].detach().cpu()
+    cl = fwd["code"].detach().cpu()
+    mask01 = torch.from_numpy(ref_cpu.threshold_np(ml.numpy()))
+    c2 = cl.clone().requires_grad_(True)
+    m2 = ml.clone().requires_grad_(True)
+    st = ref_cpu.HistLossState()
+    gt = step["gt_code"].double().cpu()
+    lb2 = ref_cpu.binary_code_loss(st, c2, mask01, gt)
+    lm2 = ref_cpu.mask_loss(m2, step["gt_mask"].cpu())
+    np.testing.assert_allclose(loss_b.item(), lb2.item(), rtol=1e-12)
+    np.testing.assert_allclose(loss_m.item(), lm2.item(), rtol=1e-6)
+    np.testing.assert_allclose(step["ts"].code_loss.histogram.cpu().numpy(), st.histogram.numpy(), atol=1e-15)
+    (3 * lb2 + lm2).backward()
+    dmask, dcode = step["head_grads"]
+    np.testing.assert_allclose(dcode.cpu().numpy(), c2.grad.numpy(), rtol=1e-5, atol=1e-12)
+    np.testing.assert_allclose(dmask.cpu().numpy(), m2.grad.numpy(), rtol=1e-4, atol=1e-10)
+
+
+def test_train_backward_teacher_forced(step):
+    net, bwd, sample, B = step["net"], step["bwd"], step["sample"], step["B"]
+    dmask, dcode = step["head_grads"]
+    ck = Checker()
+    kinds = [r["kind"] for r in bwd]
+    assert kinds.count("bn") == 48 and kinds.count("head") == 1 and kinds.count("maxpool") == 1
+    named_grad = {id(p): p.grad for p in net.parameters()}
+    sel = slice(0, 8)
+    for i, r in enumerate(bwd):
+        kind = r["kind"]
+        if kind in ("bn", "head"):
+            unit = r["unit"]
+            x = r["x"]
+            lab = f"{i}:{kind} {unit.kind} k{unit.k} s{unit.s} d{unit.d} {unit.cin_w}->{unit.cout} {x.H}x{x.W}"
+            wq = _q(step["w0"][id(unit.conv.weight)])
+            if kind == "head":
+                gy = r["gy"].buf
+                L = dcode.shape[1]
+                want = torch.zeros_like(gy)
+                want[..., 0] = dmask[:, 0].to(gy.dtype)
+                want[..., 1:1 + L] = dcode.permute(0, 2, 3, 1).to(gy.dtype)
+                assert torch.equal(gy, want), "head gradient conversion"
+                g_all = gy[..., :unit.cout]
+                db = g_all.double().sum((0, 1, 2))
+                ck.sums(lab + " dbias", r["dbias"], db, g_all.double().abs().sum((0, 1, 2)))
+                graw_dev = g_all
+            else:
+                gout, raw, save, out, res = r["gout"], r["raw"], r["save"], r["out"], r["res"]
+                C = unit.cout
+                mean, inv = save[:C], save[C:2 * C]
+                sc, sh = save[2 * C:3 * C], save[3 * C:]
+                g = gout.buf[..., gout.c0:gout.c0 + C].float()
+                mode = _mask_mode(unit, res)
+                if mode == 2:
+                    # the sign of the device's single-rounded fma(raw, scale, shift) is the exact one
+                    g = torch.where(raw.double() * sc.double() + sh.double() > 0, g, torch.zeros_like(g))
+                elif mode == 1:
+                    g = torch.where(out.buf[..., out.c0:out.c0 + C].float() > 0, g, torch.zeros_like(g))
+                xh = (raw.float() - mean) * inv
+                sg = g.double().sum((0, 1, 2))
+                sgx = (g.double() * xh.double()).sum((0, 1, 2))
+                ck.sums(lab + " dbeta", r["dbeta"], sg, g.double().abs().sum((0, 1, 2)))
+                ck.sums(lab + " dgamma", r["dgamma"], sgx, (g.double() * xh.double()).abs().sum((0, 1, 2)))
+                P = raw.shape[0] * raw.shape[1] * raw.shape[2]
+                gm = step["w0"][id(unit.bn.weight)].cuda()
+                sgP, sgxP = (sg / P).float(), (sgx / P).float()
+                for b in sample:
+                    exp = (gm * inv) * (g[b] - sgP - xh[b] * sgxP)
+                    ck.bf16(f"crop {b} {lab} d raw", _h(_q(exp.unsqueeze(0).cpu())), _h(r["graw"], b))
+                    if r["gres"] is not None:
+                        before, after = r["gres"]
+                        e = g[b:b + 1].cpu()
+                        if before is not None:
+                            e = before[b:b + 1].float().cpu() + e
+                        ck.bf16(f"crop {b} {lab} d residual", _h(_q(e)), _h(after, b), max_frac=0.0)
+                graw_dev = r["graw"]
+            # weight gradient: 8 output channels, all crops
+            xs = _h(x)[:, :unit.cin_w]
+            gs = _h(graw_dev)
+            exp_w = _conv_wgrad(unit, xs, gs, sel)
+            mass_w = _conv_wgrad(unit, xs.abs(), gs.abs(), sel)
+            dw = r["dw"].detach().float().cpu()
+            got_w = dw[:, sel] if unit.kind == "convT" else dw[sel]
+            ck.sums(lab + " dW", got_w, exp_w, mass_w, rel=2e-5)
+            assert torch.equal(named_grad[id(unit.conv.weight)], r["dw"]), lab + " .grad is the traced dW"
+            if "gx" in r:
+                before, after = r["gx"]
+                for b in sample:
+                    e = _conv_dgrad(unit, (1, unit.cin_w, x.H, x.W), wq, _h(graw_dev, b))
+                    if before is not None:
+                        e = e + _h(before, b)[:, :unit.cin_w]
+                    ck.bf16(f"crop {b} {lab} dx", _q(e), _h(after, b)[:, :unit.cin_w])
+            else:
+                assert x.ld == 8, lab + ": only the image input goes without an input gradient"
+        elif kind == "maxpool":
+            before, after = r["gx"]
+            for b in sample:
+                xx = _h(r["x"], b).requires_grad_(True)
+                F.max_pool2d(xx, 3, 2, 1).backward(_h(r["gp"], b))
+                ck.bf16(f"crop {b} maxpool bwd", _q(xx.grad + _h(before, b)), _h(after, b), max_frac=0.0)
+        elif kind == "avgpool":
+            before, after = r["gx"]
+            gp = r["gp"]
+            for b in sample:
+                H, W = after.shape[1], after.shape[2]
+                e = (_h(gp, b) * np.float32(1.0 / (H * W))).expand(-1, -1, H, W) + _h(before, b)
+                ck.bf16(f"crop {b} avgpool bwd", _q(e), _h(after, b), max_frac=0.0)
+        elif kind == "broadcast":
+            before, after = r["gx"]
+            for b in sample:
+                e = _h(r["gd"], b).double().sum((2, 3), keepdim=True).float()
+                ck.bf16(f"crop {b} broadcast bwd", _q(e), _h(after, b), max_frac=0.5)
+        else:
+            raise AssertionError(kind)
+    print(f"train backward teacher-forced: {len(bwd)} ops; worst not-bit-identical {ck.worst_frac:.4f}, "
+          f"worst {ck.worst_ulp:.2f} ulp")
+
+
+def test_train_adam_step_from_device_gradients(step):
+    """FusedAdam's first step (train_v6.py:335-336, torch.optim.Adam lr 2e-4, betas (0.9, 0.999),
+    eps 1e-8) applied on the host to the pre-step parameters and the device's gradients."""
+    net, p0 = step["net"], step["params0"]
+    lr, b1, b2, eps = 2e-4, 0.9, 0.999, 1e-8
+    n = 0
+    for name, p in net.named_parameters():
+        g = p.grad.detach().float().cpu()
+        m = (1 - b1) * g
+        v = (1 - b2) * g * g
+        exp = p0[name] - (lr / (1 - b1)) * m / ((v / (1 - b2)).sqrt() + eps)
+        np.testing.assert_allclose(p.detach().float().cpu().numpy(), exp.numpy(), rtol=1e-5, atol=1e-7, err_msg=name)
+        n += 1
+    assert n == len(list(net.parameters()))

@@ -109,6 +109,10 @@ class Engine:
         # read and wrote (kept alive by the list) -- the teacher-forced layer parity tests replay
         # each op on the host from the device's own stored inputs (tests/test_gpu_bench_geometry.py)
         self.trace = None
+        # optional list: every training-backward op appends a dict with the buffers it read and the
+        # gradients it wrote (accumulated gradient slices as (before, after) copies) -- the
+        # teacher-forced train-step parity test replays each one on the host (tests/test_gpu_train_tf.py)
+        self.bwd_trace = None
         # training backward: each unit's weight gradient runs on a second HIP stream, concurrently
         # with its input gradient and the next unit's BN backward on the main stream (the wgrad
         # kernel is L2/MFMA-bound, the BN passes HBM-bound; both fill the other's tail).  The
@@ -425,7 +429,7 @@ class Engine:
         L.check(L.lib.zp_conv2d_wgrad(C.byref(a), ws.data_ptr(), L.stream_ptr()), "zp_conv2d_wgrad")
 
     def _side_stream(self, dev):
-        if not self.side_wgrad or dev.type != "cuda" or self.timing is not None:
+        if not self.side_wgrad or dev.type != "cuda" or self.timing is not None or self.bwd_trace is not None:
             return None  # the per-launch timing (bench breakdown) wants the serial order
         if self._side is None:
             self._side = torch.cuda.Stream(dev)
@@ -452,6 +456,11 @@ class Engine:
         self._conv(gy, plan, unit.cin, ws, kp, rows, outs, res=gx if accumulate else None, relu=False, small=small,
                    label="dgrad")
 
+    @staticmethod
+    def _snap(a: Act):
+        """copy of a gradient slice (bwd_trace): [B, H, W, C]"""
+        return a.buf[..., a.c0:a.c0 + a.C].clone()
+
     def _dgrad_whole(self, unit, x: Act):
         """True when the dgrad launch writes every input pixel (one sub whose grid is x's pixels)."""
         plan = unit.dgrad_plan(x.H, x.W)
@@ -467,6 +476,8 @@ class Engine:
         st = L.stream_ptr()
         plan = unit.fwd_plan(x.H, x.W)
         pending = {}  # this unit's gradients, handed over with the weight gradient
+        tr = None if self.bwd_trace is None else {"kind": kind, "unit": unit, "x": x, "out": out, "res": res,
+                                                   "raw": raw, "save": save}
         if kind == "head":
             gy = gmap[out]
         else:
@@ -484,12 +495,16 @@ class Engine:
                        dbeta.data_ptr(), 0, st)
                 graw = torch.empty_like(raw)
                 gres, racc = self._grad_out(gmap, res, True) if res is not None else (None, True)
+                gres_before = self._snap(gres) if tr is not None and gres is not None and racc else None
                 L.call("zp_bn_bwd_apply", gout.ptr, gout.ld, gout.c0, out.ptr, out.ld, out.c0, raw.data_ptr(), P,
                        unit.cout, save.data_ptr(), partials.data_ptr(), bn.weight.data_ptr(), rm,
                        self.dt, graw.data_ptr(), None if gres is None else gres.ptr,
                        0 if gres is None else gres.ld, 0 if gres is None else gres.c0, int(racc), st)
                 pending[bn.weight] = dgamma
                 pending[bn.bias] = dbeta
+                if tr is not None:
+                    tr.update(gout=gout, graw=graw, dgamma=dgamma, dbeta=dbeta,
+                              gres=None if gres is None else (gres_before, self._snap(gres)))
                 if conv.bias is not None:
                     # train-mode BN removes the per-channel mean: d loss / d conv bias == 0 exactly
                     pending[conv.bias] = torch.zeros_like(conv.bias)
@@ -503,6 +518,8 @@ class Engine:
             L.call("zp_bn_bwd_reduce", gy.ptr, gy.ld, 0, None, 0, 0, None, gy.P, gy.ld, None, 0, self.dt,
                    partials.data_ptr(), None, db.data_ptr(), 0, st)
             pending[conv.bias] = db[:unit.cout]
+        if tr is not None and kind == "head":
+            tr.update(gy=gy, dbias=pending.get(conv.bias))
         wdy = Act(gy.buf, 0, unit.cout) if kind == "head" else gy
         side = self._side_stream(dev)
         if side is None:
@@ -523,9 +540,16 @@ class Engine:
                 grads[conv.weight] = dw
             gy.buf.record_stream(side)  # freed below on the main stream; reused only after the wgrad
             self._side_used = True  # x (the tape's activation) and the gradients outlive the join
+        if tr is not None:
+            tr["dw"] = dw
         if need_dx:
             gx, acc = self._grad_out(gmap, x, self._dgrad_whole(unit, x))
+            before = self._snap(gx) if tr is not None and acc else None
             self._dgrad(unit, gy, gx, accumulate=acc)
+            if tr is not None:
+                tr["gx"] = (before, self._snap(gx))
+        if tr is not None:
+            self.bwd_trace.append(tr)
 
     # ------------------------------------------------------------------ network
     def forward(self, x, train):
@@ -613,7 +637,10 @@ class Engine:
         mask = torch.empty((B, 1, H2, W2), dtype=torch.float32, device=dev)
         code = torch.empty((B, ncls - 1, H2, W2), dtype=torch.float32, device=dev)
         self.head_fwd(self._u(aspp.conv_1x1_4, None, False), Act(head_in), mask, code, tape)
-        return {"mask": mask, "code": code, "tape": tape, "xh": xh, "x64": x64, "x128": x128}
+        r = {"mask": mask, "code": code, "tape": tape, "xh": xh, "x64": x64, "x128": x128}
+        if tape is not None and self.bwd_trace is not None:
+            self.last_fwd = r  # the traced training step's outputs and tape (teacher-forced tests)
+        return r
 
     def _aspp_v3(self, r):
         """ASPP_v3.forward (aspp_v3.py:78-102).  The concats are channel slices of three buffers
@@ -749,6 +776,8 @@ class Engine:
         if dcode is None:
             dcode = torch.zeros((B, ncls - 1, H2, W2), dtype=torch.float32, device=dev)
         dmask, dcode = dmask.contiguous().float(), dcode.contiguous().float()
+        if self.bwd_trace is not None:
+            self.last_head_grads = (dmask, dcode)
         ldh = 32 if ncls <= 32 else G.ceil_to(ncls, 64)
         v3 = any(r[0] == "head" and r[3] == "head3" for r in tape.recs)
         if v3:
@@ -780,13 +809,19 @@ class Engine:
                 _, xa, pa = rec
                 gp = self._grad(gmap, pa)
                 gx = self._grad(gmap, xa)
+                before = self._snap(gx) if self.bwd_trace is not None else None
                 L.call("zp_maxpool3s2_bwd", xa.ptr, xa.ld, xa.c0, gp.ptr, gp.ld, gp.c0, xa.B, xa.H, xa.W, xa.C, pa.H,
                        pa.W, self.dt, gx.ptr, gx.ld, gx.c0, 1, st)
+                if self.bwd_trace is not None:
+                    self.bwd_trace.append({"kind": "maxpool", "x": xa, "gp": gp, "gx": (before, self._snap(gx))})
             elif kind == "broadcast":
                 _, src, dst = rec
                 gd = self._grad(gmap, dst)
                 gs = self._grad(gmap, src)
+                before = self._snap(gs) if self.bwd_trace is not None else None
                 L.call("zp_sum_hw", gd.ptr, gd.B, gd.H, gd.W, gd.ld, gd.c0, gd.C, self.dt, gs.ptr, st)
+                if self.bwd_trace is not None:
+                    self.bwd_trace.append({"kind": "broadcast", "gd": gd, "gx": (before, self._snap(gs))})
             elif kind == "interp":
                 _, dst = rec
                 gd = self._grad(gmap, dst)
@@ -801,8 +836,11 @@ class Engine:
                 _, xa, pa = rec
                 gp = self._grad(gmap, pa)
                 gx = self._grad(gmap, xa)
+                before = self._snap(gx) if self.bwd_trace is not None else None
                 L.call("zp_add_broadcast_hw", gp.ptr, C.c_float(1.0 / (xa.H * xa.W)), xa.B, xa.C, self.dt, gx.ptr,
                        xa.H, xa.W, gx.ld, gx.c0, 1, st)
+                if self.bwd_trace is not None:
+                    self.bwd_trace.append({"kind": "avgpool", "gp": gp, "gx": (before, self._snap(gx))})
         self._side_join(dev)
         return grads
 
