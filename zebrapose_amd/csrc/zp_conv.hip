@@ -16,7 +16,8 @@
 
 // Diagnostic ablation builds only (tools/build_ablation.sh -> libzp_abl<N>.so; wrong results):
 // ZP_ABL 1 = k_conv / k_conv_strip / k_wgrad_lds issue no LDS-DMA, 2 = they run no MFMA, 3 = k_conv
-// / k_conv_strip stage only the weights (no activation DMA), 4 = k_conv_strip stages only the strips.
+// / k_conv_strip stage only the weights (no activation DMA), 4 = k_conv_strip stages only the strips,
+// 6 = the 16-bit NHWC epilogue stores nothing, 7 = it loads no BN scale / shift.
 // The product build is ZP_ABL 0.
 #ifndef ZP_ABL
 #define ZP_ABL 0
@@ -169,12 +170,12 @@ __device__ __forceinline__ void conv_epilogue(const zp_conv_args& A, const zp_co
           sc[r] = 1.f;
           sh[r] = 0.f;
         }
-        if (cok && S.scale) {
+        if (ZP_ABL != 7 && cok && S.scale) {
           const float4 s0 = *(const float4*)(S.scale + cs), s1 = *(const float4*)(S.scale + cs + 4);
           sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w;
           sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
         }
-        if (cok && S.shift) {
+        if (ZP_ABL != 7 && cok && S.shift) {
           const float4 s0 = *(const float4*)(S.shift + cs), s1 = *(const float4*)(S.shift + cs + 4);
           sh[0] = s0.x; sh[1] = s0.y; sh[2] = s0.z; sh[3] = s0.w;
           sh[4] = s1.x; sh[5] = s1.y; sh[6] = s1.z; sh[7] = s1.w;
@@ -209,7 +210,14 @@ __device__ __forceinline__ void conv_epilogue(const zp_conv_args& A, const zp_co
           uint32_t o[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) o[r] = H16<T>::to(v[2 * r]) | (H16<T>::to(v[2 * r + 1]) << 16);
-          *(uint4*)((unsigned short*)S.y + pix * S.ldy + S.cy0 + cs) = make_uint4(o[0], o[1], o[2], o[3]);
+          if (ZP_ABL == 6 && o[0] != 0x3f803f80u) continue;  // diagnostic: no stores (unless a value pair is exactly 1, 1)
+          if constexpr (ZP_ABL == 8) {  // diagnostic: non-temporal stores
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+            u32x4* yp = (u32x4*)((unsigned short*)S.y + pix * S.ldy + S.cy0 + cs);
+            __builtin_nontemporal_store((u32x4){o[0], o[1], o[2], o[3]}, yp);
+          } else {
+            *(uint4*)((unsigned short*)S.y + pix * S.ldy + S.cy0 + cs) = make_uint4(o[0], o[1], o[2], o[3]);
+          }
         }
       }
     }
@@ -938,8 +946,14 @@ __global__ void __launch_bounds__(512) k_conv_strip(const zp_conv_args A, const 
 //     row and piece) plus a scalar offset advanced by additions (no divisions);
 //   * one __shared__ array (weights ring, then strip ring).
 // ------------------------------------------------------------------------------------
-template <typename T, int WC, int SPW, bool SPREAD>
+template <typename T, int WC, int SPW, int DM>
 __global__ void __launch_bounds__(512) k_conv_strip2(const zp_conv_args A, const strip_geo SG, const int flags) {
+  // DM: where the next group's strip DMA is issued.  0: the read section of tap column 1; 1: spread
+  // over the read sections of the group's three steps; 2: between the MFMAs of tap column 0 (the
+  // read sections then carry only the weight pieces: the LDS-DMA issue cost, ~60 cycles per piece
+  // among bare MFMAs but 100-185 inside a read section already holding 16 ds_read_b128, leaves the
+  // critical path of the ping-pong schedule, and the strip is issued one phase earlier)
+  constexpr bool SPREAD = DM == 1, MSEC = DM == 2;
   constexpr int WP = 4, NWP = 4, NW = 8;
   constexpr int TC = 32 * WC, TP = 256;
   constexpr int WPW = TC / 8 / NW;  // weight DMA instrs per wave per step
@@ -968,6 +982,16 @@ __global__ void __launch_bounds__(512) k_conv_strip2(const zp_conv_args A, const
   const int CB = A.Cin / 64;
   const int lrow = lane >> 3;
   const int csrc = (lane & 7) ^ lrow;
+  if (flags & 512) {
+    // staggered start (first round of workgroups only): every tile takes the same time, so CUs that
+    // start together stay in lockstep and all write their output tiles in one burst at the end of
+    // each round; offsets of 0..7 x ~1k cycles spread those bursts over the next round's compute
+    const int bid = blockIdx.x + gridDim.x * blockIdx.y;
+    if (bid < (flags >> 10) * 256) {
+      const int k = ((bid >> 3) + bid) & 7;
+      for (int q = 0; q < k; ++q) __builtin_amdgcn_s_sleep(16);
+    }
+  }
 
 #if defined(__HIP_DEVICE_COMPILE__)
   const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)A.x, (short)0, (int)SG.x_bytes, 0x00020000);
@@ -1076,7 +1100,7 @@ __global__ void __launch_bounds__(512) k_conv_strip2(const zp_conv_args A, const
         issue_w(2, koff_cur + 2 * cin2);
       } else if constexpr (STEADY && PH == 1) {
         issue_w(0, koff_next);
-        issue_s(GP ^ 1, ncb, Z{}, KS{});
+        if constexpr (!MSEC) issue_s(GP ^ 1, ncb, Z{}, KS{});
       } else if constexpr (STEADY && PH == 2) {
         issue_w(1, koff_next + cin2);
       }
@@ -1103,7 +1127,11 @@ __global__ void __launch_bounds__(512) k_conv_strip2(const zp_conv_args A, const
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     auto wait_out = [&]() {
-      if constexpr (PH == 0) vm_wait<WPW + (SPREAD && STEADY ? N0 : 0)>();
+      // (MSEC without ping-pong: the wait follows the MFMA section, i.e. this step's strip issue)
+      if constexpr (MSEC && PH == 0 && STEADY) {
+        if (pingpong) vm_wait<WPW>();
+        else vm_wait<WPW + SPW>();
+      } else if constexpr (PH == 0) vm_wait<WPW + (SPREAD && STEADY ? N0 : 0)>();
       else if constexpr (STEADY && PH == 1) vm_wait<WPW + (SPREAD ? N0 + N1 : SPW)>();
       else if constexpr (STEADY && PH == 2) vm_wait<WPW>();
       else vm_wait<0>();
@@ -1115,12 +1143,19 @@ __global__ void __launch_bounds__(512) k_conv_strip2(const zp_conv_args A, const
     }
     __builtin_amdgcn_s_setprio(1);
     if constexpr (ZP_ABL != 2) {
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int i = 0; i < WC; ++i)
-#pragma unroll
-          for (int j = 0; j < WP; ++j) MfmaTraits<T>::mma(acc[i][j], af[s2][i], bfr[s2][j]);
+      // MSEC, tap column 0 of a steady group: strip piece k after MFMA SP (k + 1) - 1
+      constexpr int NM = 2 * WC * WP, SP = NM / (SPW + 1);
+      static_for<NM>([&](auto t_c) {
+        constexpr int t = decltype(t_c)::value;
+        constexpr int s2 = t / (WC * WP), i = (t / WP) % WC, j = t % WP;
+        MfmaTraits<T>::mma(acc[i][j], af[s2][i], bfr[s2][j]);
+        if constexpr (MSEC && PH == 0 && STEADY && ZP_ABL != 1 && (t + 1) % SP == 0 && (t + 1) / SP <= SPW) {
+          constexpr int k = (t + 1) / SP - 1;
+          __builtin_amdgcn_sched_barrier(0);  // pin the piece between MFMAs t and t + 1
+          issue_s(GP ^ 1, ncb, std::integral_constant<int, k>{}, std::integral_constant<int, k + 1>{});
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      });
     } else {
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
@@ -2243,12 +2278,13 @@ static int conv_stages_override() {
 // cluster, bit 3 ping-pong (staggered wave groups), bit 4 tap-row trimming (tap rows that read only
 // padding for a whole tile are skipped), bit 5 spread strip DMA (k_conv_strip only; slower), bit 6
 // k_conv_strip2 instead of k_conv_strip, bit 7 k_conv_quad for the four phases of stride-2 transposed
-// structures (ConvTranspose2d forward, stride-2 conv data gradient).  Default (measured, profiles/r01_conv_sweep.md,
+// structures (ConvTranspose2d forward, stride-2 conv data gradient), bit 8 k_conv_strip2 issues the
+// next strip's DMA between the MFMAs of a group's first step (DM 2).  Default (measured, profiles/r01_conv_sweep.md,
 // profiles/r02_conv_ab.md): XCD order + setprio + ping-pong + trimming + k_conv_strip2 (94).
 // ZP_CONV_FLAGS / zp_conv_tuning(1, .) override for sweeps.
 static int g_conv_flags = -1;  // zp_conv_tuning key 1 (runtime A/B in one process); -1 = env / default
 static int conv_flags() {
-  static const int v = getenv("ZP_CONV_FLAGS") ? env_int("ZP_CONV_FLAGS") : 94 + 128;
+  static const int v = getenv("ZP_CONV_FLAGS") ? env_int("ZP_CONV_FLAGS") : 94 + 128 + 256;
   return g_conv_flags >= 0 ? g_conv_flags : v;
 }
 
@@ -2440,9 +2476,10 @@ extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
                  zp_conv2d_stat_parts(&a));
     const int fl = conv_flags();
     if (fl & 64) {  // k_conv_strip2 (lean main loop); flags & 32: strip DMA spread over the group
-#define ZP_STRIP2(T, WC)                                                                              \
-  if (fl & 32) hipLaunchKernelGGL((k_conv_strip2<T, WC, 5, true>), grid, dim3(512), 0, st, a, sg, fl); \
-  else hipLaunchKernelGGL((k_conv_strip2<T, WC, 5, false>), grid, dim3(512), 0, st, a, sg, fl);
+#define ZP_STRIP2(T, WC)                                                                           \
+  if (fl & 256) hipLaunchKernelGGL((k_conv_strip2<T, WC, 5, 2>), grid, dim3(512), 0, st, a, sg, fl); \
+  else if (fl & 32) hipLaunchKernelGGL((k_conv_strip2<T, WC, 5, 1>), grid, dim3(512), 0, st, a, sg, fl); \
+  else hipLaunchKernelGGL((k_conv_strip2<T, WC, 5, 0>), grid, dim3(512), 0, st, a, sg, fl);
       if (a.dtype == ZP_F16) {
         if (tc == 64) { ZP_STRIP2(f16_t, 2) } else { ZP_STRIP2(f16_t, 4) }
       } else {
