@@ -982,16 +982,6 @@ __global__ void __launch_bounds__(512) k_conv_strip2(const zp_conv_args A, const
   const int CB = A.Cin / 64;
   const int lrow = lane >> 3;
   const int csrc = (lane & 7) ^ lrow;
-  if (flags & 512) {
-    // staggered start (first round of workgroups only): every tile takes the same time, so CUs that
-    // start together stay in lockstep and all write their output tiles in one burst at the end of
-    // each round; offsets of 0..7 x ~1k cycles spread those bursts over the next round's compute
-    const int bid = blockIdx.x + gridDim.x * blockIdx.y;
-    if (bid < (flags >> 10) * 256) {
-      const int k = ((bid >> 3) + bid) & 7;
-      for (int q = 0; q < k; ++q) __builtin_amdgcn_s_sleep(16);
-    }
-  }
 
 #if defined(__HIP_DEVICE_COMPILE__)
   const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)A.x, (short)0, (int)SG.x_bytes, 0x00020000);
