@@ -170,13 +170,15 @@ __device__ __forceinline__ void conv_epilogue(const zp_conv_args& A, const zp_co
           sc[r] = 1.f;
           sh[r] = 0.f;
         }
+        const float* psc = S.scale + cs;
+        const float* psh = S.shift + cs;
         if (ZP_ABL != 7 && cok && S.scale) {
-          const float4 s0 = *(const float4*)(S.scale + cs), s1 = *(const float4*)(S.scale + cs + 4);
+          const float4 s0 = *(const float4*)psc, s1 = *(const float4*)(psc + 4);
           sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w;
           sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
         }
         if (ZP_ABL != 7 && cok && S.shift) {
-          const float4 s0 = *(const float4*)(S.shift + cs), s1 = *(const float4*)(S.shift + cs + 4);
+          const float4 s0 = *(const float4*)psh, s1 = *(const float4*)(psh + 4);
           sh[0] = s0.x; sh[1] = s0.y; sh[2] = s0.z; sh[3] = s0.w;
           sh[4] = s1.x; sh[5] = s1.y; sh[6] = s1.z; sh[7] = s1.w;
         }
@@ -1258,8 +1260,10 @@ struct quad_geo {
 // slot -> phase (sub-problem) and input shift (host table: quad_plan)
 __host__ __device__ constexpr int quad_phase(int slot) { return slot == 0 ? 0 : slot == 1 || slot == 4 ? 1 : slot == 2 || slot == 6 ? 2 : 3; }
 
-template <typename T, int W>
+template <typename T, int W, bool MS>
 __global__ void __launch_bounds__(512) k_conv_quad(const zp_conv_args A, const quad_geo QG, const int flags) {
+  // MS (flags & 256, as k_conv_strip2's DM 2): the next chunk's strip DMA is issued between the MFMAs
+  // of step 0 instead of in its read section
   constexpr int WC = 2, WP = 4, NWP = 4;
   constexpr int TC = 64, TP = 256, TR = TP / W;
   constexpr int SROWS = (TR + 1) * W;    // strip rows: TR + 1 image rows of W pixels
@@ -1378,7 +1382,7 @@ __global__ void __launch_bounds__(512) k_conv_quad(const zp_conv_args A, const q
     if constexpr (ZP_ABL == 1) {  // diagnostic build: no DMA in the loop
     } else if constexpr (S == 0) {
       issue_w(8, cb);
-      if constexpr (STEADY) issue_s(gp ^ 1, cb + 1);
+      if constexpr (STEADY && !MS) issue_s(gp ^ 1, cb + 1);
     } else if constexpr (STEADY) {
       issue_w(2 * (S - 1), cb + 1);
       issue_w(2 * (S - 1) + 1, cb + 1);
@@ -1412,7 +1416,8 @@ __global__ void __launch_bounds__(512) k_conv_quad(const zp_conv_args A, const q
     // loads allowed in flight at the end of this step (issued after what the next step reads)
     auto wait_out = [&]() {
       if constexpr (STEADY) {
-        if constexpr (S <= 2) vm_wait<5 + SPW>();
+        if constexpr (S == 0 && MS) vm_wait<5>();  // the strip is issued after this wait
+        else if constexpr (S <= 2) vm_wait<5 + SPW>();
         else if constexpr (S == 3) vm_wait<6 + SPW>();
         else vm_wait<6>();
       } else {
@@ -1430,15 +1435,22 @@ __global__ void __launch_bounds__(512) k_conv_quad(const zp_conv_args A, const q
     __builtin_amdgcn_s_setprio(1);
     static_for<NT>([&](auto t) {
       constexpr int PH = quad_phase(2 * S + decltype(t)::value);
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int i = 0; i < WC; ++i)
-#pragma unroll
-          for (int j = 0; j < WP; ++j) {
-            if constexpr (ZP_ABL != 2) MfmaTraits<T>::mma(acc[PH][i][j], af[t][s2][i], bfr[s2][j]);
-            else acc[PH][i][j][0] += __uint_as_float(af[t][s2][i].x ^ bfr[s2][j].y);  // diagnostic: no MFMA
-          }
+      static_for<2 * WC * WP>([&](auto u_c) {
+        constexpr int u = decltype(u_c)::value, s2 = u / (WC * WP), i = (u / WP) % WC, j = u % WP;
+        if constexpr (ZP_ABL != 2) MfmaTraits<T>::mma(acc[PH][i][j], af[t][s2][i], bfr[s2][j]);
+        else acc[PH][i][j][0] += __uint_as_float(af[t][s2][i].x ^ bfr[s2][j].y);  // diagnostic: no MFMA
+        // MS: strip piece k after MFMA 5 (k + 1) - 1 of step 0 (32 MFMAs), pinned between MFMAs
+        constexpr int m = decltype(t)::value * 2 * WC * WP + u;
+        if constexpr (MS && S == 0 && STEADY && ZP_ABL != 1 && (m + 1) % 5 == 0 && (m + 1) / 5 <= SPW) {
+          constexpr int k = (m + 1) / 5 - 1;
+          __builtin_amdgcn_sched_barrier(0);
+#if defined(__HIP_DEVICE_COMPILE__)
+          auto* d = (__attribute__((address_space(3))) void*)&lds[(9 * TC + (gp ^ 1) * SRP + (wid + 8 * k) * 8) * 8];
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(xrsrc, d, 16, sv[k], (cb + 1) * 128, 0, 0);
+#endif
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      });
     });
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(0);
@@ -2497,8 +2509,10 @@ extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
                  zp_conv2d_stat_parts(&a));
     const int fl = conv_flags();
 #define ZP_QUAD(T)                                                                             \
-  if (a.GW == 32) hipLaunchKernelGGL((k_conv_quad<T, 32>), grid, dim3(512), 0, st, a, qg, fl); \
-  else hipLaunchKernelGGL((k_conv_quad<T, 64>), grid, dim3(512), 0, st, a, qg, fl);
+  if (a.GW == 32 && (fl & 256)) hipLaunchKernelGGL((k_conv_quad<T, 32, true>), grid, dim3(512), 0, st, a, qg, fl); \
+  else if (a.GW == 32) hipLaunchKernelGGL((k_conv_quad<T, 32, false>), grid, dim3(512), 0, st, a, qg, fl); \
+  else if (fl & 256) hipLaunchKernelGGL((k_conv_quad<T, 64, true>), grid, dim3(512), 0, st, a, qg, fl); \
+  else hipLaunchKernelGGL((k_conv_quad<T, 64, false>), grid, dim3(512), 0, st, a, qg, fl);
     if (a.dtype == ZP_F16) { ZP_QUAD(f16_t) } else { ZP_QUAD(bf16_t) }
 #undef ZP_QUAD
     ZP_LAUNCH_CHECK("zp_conv2d quad");
