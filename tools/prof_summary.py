@@ -32,7 +32,7 @@ def bench_label(name):
     m = re.search(r"k_conv_strip<(unsigned short|_Float16), (\d+), (\d+), (\d+)>", name)
     if m:
         return f"k_conv_strip<{tn[m.group(1)]},WC={m.group(2)},ST={m.group(3)}>"
-    m = re.search(r"k_conv_strip2<(unsigned short|_Float16), (\d+), (\d+), (true|false)>", name)
+    m = re.search(r"k_conv_strip2<(unsigned short|_Float16), (\d+), (\d+), (true|false|\d+)>", name)
     if m:
         return f"k_conv_strip2<{tn[m.group(1)]},WC={m.group(2)}>"
     m = re.search(r"k_conv<(unsigned short|_Float16|float), (\d+), (\d+), (\d+), (\d+), (true|false)>", name)
