@@ -63,6 +63,7 @@ def parse(argv=None):
     ap.add_argument("--mo-objects", type=int, default=30)
     ap.add_argument("--mo-crops", type=int, default=8, help="crops per object per step (configs[4] leg)")
     ap.add_argument("--no-fp32", action="store_true", help="skip the fp32-mode inference line")
+    ap.add_argument("--no-bs1", action="store_true", help="skip the bs=1 eager vs hipGraph latency leg")
     ap.add_argument("--dry-run", action="store_true", help="CPU stub workload over gloo (launcher test)")
     return ap.parse_args(argv)
 
@@ -240,6 +241,36 @@ def train_breakdown(ts, tnet, x, gt_code, gt_mask, world, rank, steps=3):
             + f" | enqueue ms into backward {out['bucket_enqueue_ms']} | exposed comm {out['exposed_comm_ms']} ms",
             file=sys.stderr, flush=True)
     return out
+
+
+def bs1_leg(net, dec, S, dev, iters=50):
+    """The reference's per-crop evaluation loop (test.py:190, 248: bs=1): forward + decode of one
+    crop, eager (about 50 launches whose arguments are packed in Python: host-bound) vs one
+    hipGraph replay of the same captured step (zebrapose_amd.graphs)."""
+    from zebrapose_amd.graphs import GraphedInference
+    x1 = synthetic_crops(1, S, dev, seed=7)
+    bb = np.array([[100, 80, 200, 200]])
+
+    def eager():
+        with torch.no_grad():
+            m, c = net(x1)
+            return dec(m, c, bb, bbox_size=S // 2)
+
+    def timed(fn):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / iters * 1e3
+
+    te = timed(eager)
+    g = GraphedInference(net, 1, S, decoder=dec, bbox_size=S // 2)
+    tg = timed(lambda: g(x1, bb))
+    return {"eager_ms_per_crop": round(te, 3), "graph_ms_per_crop": round(tg, 3),
+            "graph_crops_per_s": round(1e3 / tg, 1), "speedup": round(te / tg, 2), "iterations": iters}
 
 
 def multi_object_leg(args, dev):
@@ -482,6 +513,11 @@ def run(args):
                 "dtype": "f32", "whole_step_tflops": round(tfl, 2), "frac_of_f32_peak": round(tfl / PEAK["fp32"], 4)}
         net.set_precision(args.precision)
 
+    # ------------------------------------------------------------------ bs=1 latency: eager vs hipGraph
+    bs1 = None
+    if not args.no_bs1 and rank == 0:
+        bs1 = bs1_leg(net, dec, S, dev)
+
     # ------------------------------------------------------------------ on-device PnP (extra, §8f rank 1)
     # RANSAC-EPnP (150 iterations, 2 px) over the last step's decoded correspondences; the random
     # network gives random correspondences, i.e. the worst case (no early RANSAC termination)
@@ -615,7 +651,7 @@ def run(args):
                            "model": "BinaryCodeNet_Deeplab(34, 16, 2, concat=True)", "global_batch": world * B,
                            "per_gpu_batch": B, "input": f"{S}x{S}", "parallelism": f"replicas{world}",
                            "correspondences_last_step": n_corr},
-                "roofline": roofline, "fp32": fp32, "cpu_baseline": cpu, "train": train, "pnp": pnp_res, "crop": crop_res, "v3": v3,
+                "roofline": roofline, "fp32": fp32, "bs1": bs1, "cpu_baseline": cpu, "train": train, "pnp": pnp_res, "crop": crop_res, "v3": v3,
                 "multi_object": multi}
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -69,7 +69,10 @@ class Decoder:
         if Lfull < self.bits:
             raise ValueError("fewer code channels than LUT bits")
         dev = mask_logits.device
-        bb = torch.as_tensor(np.asarray(bboxes), dtype=torch.int32).reshape(B, 4).to(dev).contiguous()
+        if torch.is_tensor(bboxes) and bboxes.device == dev and bboxes.dtype == torch.int32:
+            bb = bboxes.reshape(B, 4).contiguous()  # already on the device (graph capture: no host copy)
+        else:
+            bb = torch.as_tensor(np.asarray(bboxes), dtype=torch.int32).reshape(B, 4).to(dev).contiguous()
         li = None
         if lut_index is not None:
             li = torch.as_tensor(np.asarray(lut_index), dtype=torch.int32).reshape(B).to(dev).contiguous()

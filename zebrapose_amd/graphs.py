@@ -1,0 +1,59 @@
+"""hipGraph capture of the inference step (forward + on-device decode).
+
+The reference's evaluation loop runs one crop at a time (test.py:190, 248).  At bs=1 the eager
+path is bound by host work, not the GPU: about 50 libzp launches, each with its ctypes argument
+struct built in Python (tools/host_overhead.py).  torch.cuda.CUDAGraph is hipGraph on ROCm.
+Every libzp launch goes to torch's current stream, so one capture records the whole forward and
+decode, and each later call is one graph launch.
+
+Inputs and outputs are static device tensors owned by the graph: a call copies the crops (and
+boxes) in, replays, and returns views that stay valid until the next call.  Weight packings and
+BN folds are cached by the eager warm-up run and referenced by address, so build a new
+GraphedInference after changing the weights (load_state_dict, an optimizer step).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+
+class GraphedInference:
+    def __init__(self, net, batch: int, size: int = 256, decoder=None, bbox_size: int = 128, warmup: int = 2,
+                 device=None):
+        if net.training:
+            raise ValueError("GraphedInference captures the eval forward: call net.eval() first")
+        dev = torch.device(device) if device is not None else next(net.parameters()).device
+        if dev.type != "cuda":
+            raise ValueError("GraphedInference needs the network on a HIP device")
+        self.net, self.decoder, self.bbox_size = net, decoder, int(bbox_size)
+        self.x = torch.zeros((batch, 3, size, size), dtype=torch.float32, device=dev)
+        self.bb = torch.zeros((batch, 4), dtype=torch.int32, device=dev)
+        self.bb[:, 2:] = size  # any valid box for the warm-up; callers pass their own
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.no_grad(), torch.cuda.stream(side):
+            for _ in range(max(1, warmup)):  # fills the weight-pack / BN-fold caches outside the capture
+                self._step()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.no_grad(), torch.cuda.graph(self.graph):
+            self.out = self._step()
+
+    def _step(self):
+        mask, code = self.net(self.x)
+        if self.decoder is None:
+            return mask, code
+        counts, xy, xyz = self.decoder(mask, code, self.bb, bbox_size=self.bbox_size)
+        return mask, code, counts, xy, xyz
+
+    def __call__(self, x, bboxes=None):
+        """x f32 [B, 3, size, size] (device or host); bboxes [B, 4] (x, y, w, h) when a decoder is
+        attached -> (mask, code) or (mask, code, counts, xy, xyz), the graph's static outputs."""
+        if tuple(x.shape) != tuple(self.x.shape):
+            raise ValueError(f"captured for input {tuple(self.x.shape)}, got {tuple(x.shape)}")
+        self.x.copy_(x, non_blocking=True)
+        if bboxes is not None:
+            self.bb.copy_(torch.as_tensor(np.asarray(bboxes), dtype=torch.int32).reshape(self.bb.shape),
+                          non_blocking=False)
+        self.graph.replay()
+        return self.out
