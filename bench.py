@@ -64,6 +64,7 @@ def parse(argv=None):
     ap.add_argument("--mo-crops", type=int, default=8, help="crops per object per step (configs[4] leg)")
     ap.add_argument("--no-fp32", action="store_true", help="skip the fp32-mode inference line")
     ap.add_argument("--no-bs1", action="store_true", help="skip the bs=1 eager vs hipGraph latency leg")
+    ap.add_argument("--eager", action="store_true", help="time the eager launches instead of the hipGraph replay")
     ap.add_argument("--dry-run", action="store_true", help="CPU stub workload over gloo (launcher test)")
     return ap.parse_args(argv)
 
@@ -407,10 +408,25 @@ def run(args):
     side = rng.integers(64, 401, B)
     bboxes = np.stack([rng.integers(0, 300, B), rng.integers(0, 200, B), side, side], 1)
 
-    def step():
+    def eager_step():
         with torch.no_grad():
             m, c = net(x)
             return dec(m, c, bboxes, bbox_size=S // 2)
+
+    # The timed step is one hipGraph replay of the same forward + decode (zebrapose_amd.graphs):
+    # the crops are copied into the graph's static input each step (a 25 MB device copy, timed);
+    # the boxes are uploaded once.  Every kernel of the eager step runs; only the ~50 per-launch
+    # host round trips are gone.  --eager times the launches one by one (also reported below).
+    graph = None
+    if not args.eager:
+        from zebrapose_amd.graphs import GraphedInference
+        graph = GraphedInference(net, B, S, decoder=dec, bbox_size=S // 2)
+        graph.bb.copy_(torch.as_tensor(bboxes, dtype=torch.int32))
+
+    def step():
+        if graph is None:
+            return eager_step()
+        return graph(x)[2:]
 
     # ------------------------------------------------------------------ inference (value)
     for _ in range(args.warmup):
@@ -494,14 +510,14 @@ def run(args):
     if not args.no_fp32 and args.precision != "fp32":
         net.set_precision("fp32")
         for _ in range(2):
-            step()
+            eager_step()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         K2 = max(3, args.steps // 2)
         t0 = time.perf_counter()
         for _ in range(K2):
-            step()
+            eager_step()
         torch.cuda.synchronize()
         el2 = time.perf_counter() - t0
         if world > 1:
@@ -517,6 +533,17 @@ def run(args):
     bs1 = None
     if not args.no_bs1 and rank == 0:
         bs1 = bs1_leg(net, dec, S, dev)
+        # the benched batch launched eagerly, one launch at a time (value is the graph replay)
+        for _ in range(2):
+            eager_step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            eager_step()
+        torch.cuda.synchronize()
+        ele = time.perf_counter() - t0
+        bs1["bs%d_eager_crops_per_s" % B] = round(B * args.steps / ele, 1)
+        bs1["bs%d_eager_ms_per_step" % B] = round(ele / args.steps * 1e3, 3)
 
     # ------------------------------------------------------------------ on-device PnP (extra, §8f rank 1)
     # RANSAC-EPnP (150 iterations, 2 px) over the last step's decoded correspondences; the random
@@ -650,6 +677,7 @@ def run(args):
                                        "256x256 crops, 16-bit code head, on-device decode",
                            "model": "BinaryCodeNet_Deeplab(34, 16, 2, concat=True)", "global_batch": world * B,
                            "per_gpu_batch": B, "input": f"{S}x{S}", "parallelism": f"replicas{world}",
+                           "launch": "eager" if graph is None else "hipgraph",
                            "correspondences_last_step": n_corr},
                 "roofline": roofline, "fp32": fp32, "bs1": bs1, "cpu_baseline": cpu, "train": train, "pnp": pnp_res, "crop": crop_res, "v3": v3,
                 "multi_object": multi}
