@@ -334,6 +334,11 @@ int zp_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, 
 int zp_adam_multi(int count, float* const* params, const float* const* grads, float* const* exp_avg,
                   float* const* exp_avg_sq, const long long* numel, double lr, double beta1, double beta2,
                   double eps, long long step, void* stream);
+/* the same with the step count read on the device (f32 scalar, already advanced to this step):
+ * capturable in a hipGraph, whose replays then use the current count (GraphedTrainStep) */
+int zp_adam_multi_dev(int count, float* const* params, const float* const* grads, float* const* exp_avg,
+                      float* const* exp_avg_sq, const long long* numel, double lr, double beta1, double beta2,
+                      double eps, const float* step_dev, void* stream);
 
 #ifdef __cplusplus
 }

@@ -113,6 +113,7 @@ _SIGS = {
     "zp_crop_image": (i32, [vp, i32, i32, i32, vp, vp, i32, i32, vp, vp]),
     "zp_crop_gt": (i32, [vp, vp, vp, i32, i32, i32, vp, vp, i32, i32, i32, vp, vp, vp, vp]),
     "zp_adam_multi": (i32, [i32, vp, vp, vp, vp, vp, f64, f64, f64, f64, i64, vp]),
+    "zp_adam_multi_dev": (i32, [i32, vp, vp, vp, vp, vp, f64, f64, f64, f64, vp, vp]),
 }
 
 

@@ -1009,7 +1009,15 @@ struct AdamTable {
 };
 
 __global__ void __launch_bounds__(256) k_adam_multi(const AdamTable T, float lr_bc1, float w1, float b2, float w2,
-                                                    float bc2_sqrt, float eps) {
+                                                    float bc2_sqrt, float eps, const float* __restrict__ step_dev,
+                                                    double lr, double beta1, double beta2) {
+  if (step_dev) {
+    // capturable form (zp_adam_multi_dev): the step count lives on the device, so a captured
+    // graph replays with the current count; the host's double-precision bias corrections, per block
+    const double st = (double)step_dev[0];
+    lr_bc1 = (float)(lr / (1.0 - pow(beta1, st)));
+    bc2_sqrt = (float)sqrt(1.0 - pow(beta2, st));
+  }
   const int b = blockIdx.x;
   int lo = 0, hi = T.count - 1;  // last t with blk0[t] <= b
   while (lo < hi) {
@@ -1405,13 +1413,14 @@ extern "C" int zp_adam(float* param, const float* grad, float* exp_avg, float* e
   return ZP_OK;
 }
 
-extern "C" int zp_adam_multi(int count, float* const* params, const float* const* grads, float* const* exp_avg,
-                             float* const* exp_avg_sq, const long long* numel, double lr, double beta1, double beta2,
-                             double eps, long long step, void* stream) {
-  ZP_CHECK_ARG(count >= 0 && (count == 0 || (params && grads && exp_avg && exp_avg_sq && numel)) && step >= 1,
+static int adam_multi(int count, float* const* params, const float* const* grads, float* const* exp_avg,
+                      float* const* exp_avg_sq, const long long* numel, double lr, double beta1, double beta2,
+                      double eps, long long step, const float* step_dev, void* stream) {
+  ZP_CHECK_ARG(count >= 0 && (count == 0 || (params && grads && exp_avg && exp_avg_sq && numel)) &&
+                   (step >= 1 || step_dev),
                "zp_adam_multi: bad args");
-  const double bc1 = 1.0 - pow(beta1, (double)step);
-  const double bc2 = 1.0 - pow(beta2, (double)step);
+  const double bc1 = step_dev ? 1.0 : 1.0 - pow(beta1, (double)step);
+  const double bc2 = step_dev ? 1.0 : 1.0 - pow(beta2, (double)step);
   // each launch takes up to ADAM_MT non-empty tensors; the next launch starts where this one's scan
   // stopped (empty tensors are skipped, never counted twice)
   for (int t0 = 0; t0 < count;) {
@@ -1438,10 +1447,24 @@ extern "C" int zp_adam_multi(int count, float* const* params, const float* const
     T.blk0[T.count] = nb;
     if (nb == 0) continue;
     hipLaunchKernelGGL(k_adam_multi, dim3(nb), dim3(256), 0, (hipStream_t)stream, T, (float)(lr / bc1),
-                       (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)sqrt(bc2), (float)eps);
+                       (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)sqrt(bc2), (float)eps,
+                       step_dev, lr, beta1, beta2);
     ZP_LAUNCH_CHECK("zp_adam_multi");
   }
   return ZP_OK;
+}
+
+extern "C" int zp_adam_multi(int count, float* const* params, const float* const* grads, float* const* exp_avg,
+                             float* const* exp_avg_sq, const long long* numel, double lr, double beta1, double beta2,
+                             double eps, long long step, void* stream) {
+  return adam_multi(count, params, grads, exp_avg, exp_avg_sq, numel, lr, beta1, beta2, eps, step, nullptr, stream);
+}
+
+extern "C" int zp_adam_multi_dev(int count, float* const* params, const float* const* grads, float* const* exp_avg,
+                                 float* const* exp_avg_sq, const long long* numel, double lr, double beta1,
+                                 double beta2, double eps, const float* step_dev, void* stream) {
+  ZP_CHECK_ARG(step_dev, "zp_adam_multi_dev: step_dev");
+  return adam_multi(count, params, grads, exp_avg, exp_avg_sq, numel, lr, beta1, beta2, eps, 0, step_dev, stream);
 }
 
 extern "C" int zp_mask_interp(const float* x, int B, int H, int W, int OH, int OW, int dtype, void* y, int ldy, int cy0,

@@ -57,3 +57,42 @@ class GraphedInference:
                           non_blocking=False)
         self.graph.replay()
         return self.out
+
+
+class GraphedTrainStep:
+    """One training step (TrainStep: forward, loss, backward, FusedAdam) captured in a hipGraph for
+    a fixed batch shape; each call copies the batch into the graph's static inputs and replays.
+
+    The training step is GPU-bound (tools/host_overhead.py), but its ~400 launches each leave a
+    gap on the queue; a replay issues them back to back.  Requirements: one process (no
+    data-parallel buckets: their collectives are not captured) and TrainStep(capturable=True),
+    whose FusedAdam keeps the step counts on the device.  The warm-up steps run eagerly and are
+    real optimizer steps.  Parameters, gradients and optimizer state keep their storage, so
+    state_dict / checkpointing work between calls.
+    """
+
+    def __init__(self, ts, x, gt_code, gt_mask, warmup: int = 2):
+        if ts.buckets is not None or ts.net is not ts.module:
+            raise ValueError("GraphedTrainStep runs single-process steps (no data-parallel wrapper)")
+        if not getattr(ts.optimizer, "capturable", False):
+            raise ValueError("GraphedTrainStep needs TrainStep(..., capturable=True)")
+        self.ts = ts
+        self.x, self.gc, self.gm = x.clone(), gt_code.clone(), gt_mask.clone()
+        dev = self.x.device
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(max(1, warmup)):
+                ts(self.x, self.gc, self.gm)
+        torch.cuda.current_stream(dev).wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.out = ts(self.x, self.gc, self.gm)
+
+    def __call__(self, x, gt_code, gt_mask):
+        """-> (loss, loss_b, loss_m), the graph's static output tensors (valid until the next call)."""
+        self.x.copy_(x, non_blocking=True)
+        self.gc.copy_(gt_code, non_blocking=True)
+        self.gm.copy_(gt_mask, non_blocking=True)
+        self.graph.replay()
+        return self.out

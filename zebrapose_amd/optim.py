@@ -13,10 +13,15 @@ from . import _lib as L
 
 
 class FusedAdam(torch.optim.Optimizer):
-    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
+    """capturable=True (torch.optim.Adam's flag of the same name): the per-parameter 'step' counts
+    live on the device and the kernels read the count there (zp_adam_multi_dev), so a step captured
+    in a hipGraph replays with the current count (zebrapose_amd.graphs.GraphedTrainStep)."""
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, capturable=False):
         if weight_decay != 0.0:
             raise NotImplementedError("weight decay is not used by the ZebraPose trainers")
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=0.0))
+        self.capturable = capturable
 
     def load_state_dict(self, state_dict):
         super().load_state_dict(state_dict)
@@ -41,12 +46,15 @@ class FusedAdam(torch.optim.Optimizer):
                     raise ValueError("FusedAdam expects contiguous float32 parameters and gradients")
                 state = self.state[p]
                 if len(state) == 0:
-                    state["step"] = torch.tensor(0.0)
+                    state["step"] = torch.zeros((), dtype=torch.float32, device=p.device) if self.capturable else \
+                        torch.tensor(0.0)
                     state["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     state["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     steps[p] = 0
                 elif p not in steps:
                     steps[p] = int(state["step"].item())
+                    if self.capturable and state["step"].device != p.device:
+                        state["step"] = state["step"].to(p.device)
                 steps[p] += 1
                 live.append(p)
                 step_t.append(state["step"])
@@ -59,11 +67,15 @@ class FusedAdam(torch.optim.Optimizer):
             for step, ps in by_step.items():
                 n = len(ps)
                 arr = C.c_void_p * n
-                L.call("zp_adam_multi", n, arr(*[p.data_ptr() for p in ps]), arr(*[p.grad.data_ptr() for p in ps]),
-                       arr(*[self.state[p]["exp_avg"].data_ptr() for p in ps]),
-                       arr(*[self.state[p]["exp_avg_sq"].data_ptr() for p in ps]),
-                       (C.c_longlong * n)(*[p.numel() for p in ps]), float(group["lr"]), float(b1), float(b2),
-                       float(group["eps"]), step, st)
+                args = (n, arr(*[p.data_ptr() for p in ps]), arr(*[p.grad.data_ptr() for p in ps]),
+                        arr(*[self.state[p]["exp_avg"].data_ptr() for p in ps]),
+                        arr(*[self.state[p]["exp_avg_sq"].data_ptr() for p in ps]),
+                        (C.c_longlong * n)(*[p.numel() for p in ps]), float(group["lr"]), float(b1), float(b2),
+                        float(group["eps"]))
+                if self.capturable:  # every tensor of this launch group is at the same (device) count
+                    L.call("zp_adam_multi_dev", *args, self.state[ps[0]]["step"].data_ptr(), st)
+                else:
+                    L.call("zp_adam_multi", *args, step, st)
                 # the kernel wrote p in place behind autograd's back: bump its version counter so
                 # version-keyed caches (packed eval weights in the engine) see the update
                 for p in ps:

@@ -29,7 +29,8 @@ def scale_for_world(learning_rate, total_iteration, world_size):
 
 
 class TrainStep:
-    def __init__(self, net, learning_rate=2e-4, binary_loss_weight=3.0, ddp=None, device=None, bucket_mb=25.0):
+    def __init__(self, net, learning_rate=2e-4, binary_loss_weight=3.0, ddp=None, device=None, bucket_mb=25.0,
+                 capturable=False):
         self.module = net
         self.net = net
         if ddp is None:
@@ -45,7 +46,8 @@ class TrainStep:
         self.binary_loss_weight = binary_loss_weight
         self.code_loss = BinaryCodeLoss("BCE", True, 2, use_histgramm_weighted_binary_loss=True)
         self.mask_loss = MaskLoss()
-        self.optimizer = FusedAdam(self.net.parameters(), lr=learning_rate)
+        # capturable: device-side Adam step counts, for zebrapose_amd.graphs.GraphedTrainStep
+        self.optimizer = FusedAdam(self.net.parameters(), lr=learning_rate, capturable=capturable)
         self.events = None  # optional list: (label, event) at step start / before backward / after backward / end
 
     def _mark(self, label):
