@@ -36,7 +36,8 @@ class GraphedInference:
                 self._step()
         torch.cuda.current_stream(dev).wait_stream(side)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.no_grad(), torch.cuda.graph(self.graph):
+        # thread_local: under torch.distributed the RCCL watchdog thread may query events meanwhile
+        with torch.no_grad(), torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
             self.out = self._step()
 
     def _step(self):
@@ -86,7 +87,7 @@ class GraphedTrainStep:
                 ts(self.x, self.gc, self.gm)
         torch.cuda.current_stream(dev).wait_stream(side)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
             self.out = ts(self.x, self.gc, self.gm)
 
     def __call__(self, x, gt_code, gt_mask):
