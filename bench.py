@@ -420,8 +420,13 @@ def run(args):
     graph = None
     if not args.eager:
         from zebrapose_amd.graphs import GraphedInference
-        graph = GraphedInference(net, B, S, decoder=dec, bbox_size=S // 2)
-        graph.bb.copy_(torch.as_tensor(bboxes, dtype=torch.int32))
+        try:
+            graph = GraphedInference(net, B, S, decoder=dec, bbox_size=S // 2)
+            graph.bb.copy_(torch.as_tensor(bboxes, dtype=torch.int32))
+        except RuntimeError as e:  # the same kernels, launched one by one (config.launch says which)
+            print(f"[bench] rank {rank}: hipGraph capture failed ({e}); timing the eager launches",
+                  file=sys.stderr, flush=True)
+            graph = None
 
     def step():
         if graph is None:
