@@ -1496,6 +1496,71 @@ __global__ void __launch_bounds__(512) k_conv_quad(const zp_conv_args A, const q
 }
 
 // ------------------------------------------------------------------------------------
+// Tiny-M 1x1 convs without statistics or residual (the ASPP image-pool conv, aspp.py:94-96: B
+// pixels of a 1x1 image, 512 -> 256 channels).  k_conv spends ~17 us on it: one 256-pixel tile,
+// 8 K steps of full-tile DMA for 32 live pixels.  Here one wave computes 16 output channels of
+// one pixel: lanes split K into 16-byte chunks (coalesced 1 KB weight-row reads), f32 products,
+// a butterfly sum over the 64 lanes, and k_conv's epilogue arithmetic (scale / shift, ReLU).
+// ------------------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ void ld16x8(const T* p, float* v) {  // 8 16-bit values, one 16-byte load
+  const uint4 u = *(const uint4*)p;
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = H16<T>::from(w[i] & 0xffffu);
+    v[2 * i + 1] = H16<T>::from(w[i] >> 16);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_conv_smallm(const zp_conv_args A) {
+  const zp_conv_sub& S = A.sub[0];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int m = blockIdx.y;  // grid point
+  const int GHW = A.GH * A.GW;
+  const int n = m / GHW, r = m - n * GHW, gy = r / A.GW, gx = r - gy * A.GW;
+  const int iy = gy * A.sy + S.ty[0], ix = gx * A.sx + S.tx[0];
+  const bool inb = (unsigned)iy < (unsigned)A.IH && (unsigned)ix < (unsigned)A.IW;
+  const T* xr = (const T*)A.x + (((size_t)n * A.IH + (inb ? iy : 0)) * A.IW + (inb ? ix : 0)) * A.ldx + A.cx0;
+  const int oy = gy * S.oys + S.oyo, ox = gx * S.oxs + S.oxo;
+  const size_t pix = ((size_t)n * S.OH + oy) * S.OW + ox;
+  const int co0 = blockIdx.x * 64 + w * 16;
+  float acc[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+  for (int k0 = lane * 8; k0 < A.Cin; k0 += 512) {
+    float xv[8];
+    ld16x8<T>(xr + k0, xv);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) xv[i] = inb ? xv[i] : 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      float wv[8];
+      ld16x8<T>((const T*)S.w + (size_t)(co0 + q) * A.k_pad + k0, wv);  // rows < w_rows (host check)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[q] = fmaf(xv[i], wv[i], acc[q]);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 16; ++q)
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) acc[q] += __shfl_xor(acc[q], off);
+  if (lane < 16) {
+    float v = acc[0];
+#pragma unroll
+    for (int q = 1; q < 16; ++q) v = lane == q ? acc[q] : v;
+    const int co = co0 + lane;
+    if (co < A.Cout) {
+      const float sc = S.scale ? S.scale[co] : 1.f, sh = S.shift ? S.shift[co] : 0.f;
+      v = v * sc + sh;
+      if (A.relu) v = fmaxf(v, 0.f);
+      ((T*)S.y)[pix * S.ldy + S.cy0 + co] = Elem<T>::cvt(v);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // weight gradient:  ws[split][sub][co][col] = sum over the split's grid points of
 //   dy[out pixel][co] * x[in pixel (tap of col)][ci of col],   col = t*Cin + ci
 // K (pixels) is the MFMA reduction axis, so both LDS tiles [pixel][channel] are read
@@ -2460,6 +2525,19 @@ extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
       for (int t = 0; grid && t < S.ntaps; ++t)
         grid = S.ty[t] == tg.ty0[s] + (t / nx) * tg.dty[s] && S.tx[t] == tg.tx0[s] + (t % nx) * tg.dtx[s];
       ZP_CHECK_ARG(grid, "zp_conv2d: sub %d taps must form a (row x column) grid of at most 32 x 32, rows outer", s);
+    }
+  }
+  // tiny-M 1x1 convs (the ASPP image-pool conv): one wave per (grid point, 16 output channels)
+  {
+    const long mpix = (long)a.N * a.GH * a.GW;
+    const zp_conv_sub& S = a.sub[0];
+    if (E == 8 && !smallc && mpix <= 64 && a.nsub == 1 && S.ntaps == 1 && !a.stats && !a.res &&
+        a.out_mode == ZP_OUT_NHWC && a.w_rows >= ((a.Cout + 63) / 64) * 64 && (conv_flags() & 1024) != 0) {
+      const dim3 grid((a.Cout + 63) / 64, (unsigned)mpix);
+      if (a.dtype == ZP_F16) hipLaunchKernelGGL(k_conv_smallm<f16_t>, grid, dim3(256), 0, (hipStream_t)stream, a);
+      else hipLaunchKernelGGL(k_conv_smallm<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, a);
+      ZP_LAUNCH_CHECK("zp_conv2d small-M");
+      return ZP_OK;
     }
   }
   const int tc = conv_tc(a);
