@@ -1497,10 +1497,11 @@ __global__ void __launch_bounds__(512) k_conv_quad(const zp_conv_args A, const q
 
 // ------------------------------------------------------------------------------------
 // Tiny-M 1x1 convs without statistics or residual (the ASPP image-pool conv, aspp.py:94-96: B
-// pixels of a 1x1 image, 512 -> 256 channels).  k_conv spends ~17 us on it: one 256-pixel tile,
-// 8 K steps of full-tile DMA for 32 live pixels.  Here one wave computes 16 output channels of
-// one pixel: lanes split K into 16-byte chunks (coalesced 1 KB weight-row reads), f32 products,
-// a butterfly sum over the 64 lanes, and k_conv's epilogue arithmetic (scale / shift, ReLU).
+// pixels of a 1x1 image, 512 -> 256 channels).  One wave computes 16 output channels of one pixel:
+// lanes split K into 16-byte chunks (coalesced 1 KB weight-row reads), f32 products, a butterfly
+// sum over the 64 lanes, and k_conv's epilogue arithmetic (scale / shift, ReLU).  Opt-in (conv flag
+// 1024): measured 16.8 vs 17.7 us per eager launch, i.e. both are launch latency, which the
+// hipGraph-replayed inference step does not pay; the network tests pass with it enabled.
 // ------------------------------------------------------------------------------------
 template <typename T>
 __device__ __forceinline__ void ld16x8(const T* p, float* v) {  // 8 16-bit values, one 16-byte load
