@@ -117,3 +117,49 @@ def test_v3_train_step_fp32_matches_reference(golden):
             budget = 0.01 if name.endswith("conv_1x1_4.weight") or name.endswith("conv_1x1_4.bias") else 0.10
             print(f"v3 grad {name}: rel-L2 {rel:.3g}")
             assert rel <= budget, (name, rel)
+
+
+def test_v3_bf16_teacher_forced(v3, golden):
+    """bf16 v3 forward replayed op by op (as tests/test_gpu_bench_geometry.py does for the main
+    network): every conv of the shared encoder / decoder and of the entire-mask head ASPP_v3
+    (its concat inputs padded with zero channels) from the device's own stored 16-bit inputs,
+    within 1 bf16 ulp (+ 2^-12 of the layer rms), and both f32 heads to accumulation order."""
+    from oracle import ref_cpu
+    from tests.test_gpu_bench_geometry import replay, _label, _nchw, _ulp_bf16
+    f = golden("r34v3_fwd256.npz")
+    v3.set_precision("bf16")
+    eng = v3.net._engine
+    eng.trace = []
+    try:
+        with torch.no_grad():
+            m, e, c = v3(torch.from_numpy(f["x"]).cuda())
+        torch.cuda.synchronize()
+        trace = eng.trace
+    finally:
+        eng.trace = None
+        v3.set_precision("fp32")
+    n_conv = 0
+    for i, rec in enumerate(trace):
+        if rec[0] == "head" and rec[4] is None and rec[3][1] is None:  # the entire-mask head: f32, one channel
+            unit, x, (ent, _) = rec[1], rec[2], rec[3]
+            for b in range(ent.shape[0]):
+                xin = _nchw(x, b)[:, :unit.cin_w]
+                exp = ref_cpu.lp_conv(xin, unit.conv.weight.detach().float().cpu(), None,
+                                      unit.conv.bias.detach().float().cpu(), None, False, dt=torch.bfloat16,
+                                      out_f32=True)
+                got = ent[b:b + 1].cpu()
+                assert float((got - exp).abs().max()) <= 2e-5 * max(float(exp.abs().max()), 1.0), _label(rec, i)
+            continue
+        for b in range(m.shape[0]):
+            exp, got = replay(rec, b, torch.bfloat16)
+            assert exp.shape == got.shape, (_label(rec, i), exp.shape, got.shape)
+            d = (got - exp).abs()
+            if rec[0] == "head":
+                assert float(d.max()) <= 2e-5 * max(float(exp.abs().max()), 1.0), _label(rec, i)
+                continue
+            rms = float(exp.pow(2).mean().sqrt())
+            bad = d > _ulp_bf16(torch.maximum(exp.abs(), got.abs())) + 2.0 ** -12 * rms
+            assert not bool(bad.any()), (_label(rec, i), int(bad.sum()))
+            assert float((d > 0).float().mean()) <= 0.005, _label(rec, i)
+        n_conv += rec[0] == "conv"
+    assert n_conv >= 48 + 9, n_conv  # the main network's 48 + ASPP_v3's convs
