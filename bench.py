@@ -2,8 +2,9 @@
 """ZebraPose hot-path benchmark on MI355X (BASELINE.json metric: 256x256 crops/s/GPU).
 
 One *step* = one pass of the hot path over one batch of synthetic crops resident in HBM:
-BinaryCodeNet_Deeplab(34, 16, 2, concat=True) forward at bs=32 (bf16 MFMA, f32 accumulate)
-+ the on-device code->vertex decode (configs[1] of BASELINE.json).  `value` is the whole-job
+BinaryCodeNet_Deeplab(34, 16, 2, concat=True) forward at bs=32 in fp32 (the reference's own
+arithmetic, BinaryCodeNet.py:161-174: no AMP) + the on-device code->vertex decode (configs[1] of
+BASELINE.json); the same step in bf16 (bf16 MFMA, f32 accumulate) is a labelled leg.  `value` is the whole-job
 throughput (crops/s summed over ranks; each rank runs its own independent batch: the inference
 path shards by crop with no collective -> weak scaling).
 
@@ -53,7 +54,8 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--size", type=int, default=256)
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--precision", default="fp32", choices=["bf16", "fp32"],
+                    help="headline precision; fp32 = the reference's own arithmetic (bf16 runs as a labelled leg)")
     ap.add_argument("--no-train", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--train-steps", type=int, default=None)
@@ -62,7 +64,8 @@ def parse(argv=None):
     ap.add_argument("--no-multi", action="store_true", help="skip the configs[4] multi-object leg")
     ap.add_argument("--mo-objects", type=int, default=30)
     ap.add_argument("--mo-crops", type=int, default=8, help="crops per object per step (configs[4] leg)")
-    ap.add_argument("--no-fp32", action="store_true", help="skip the fp32-mode inference line")
+    ap.add_argument("--no-bf16", action="store_true", help="skip the bf16 inference leg")
+    ap.add_argument("--no-rccl", action="store_true", help="N = 1: no world-size-1 RCCL group for the train leg")
     ap.add_argument("--no-bs1", action="store_true", help="skip the bs=1 eager vs hipGraph latency leg")
     ap.add_argument("--eager", action="store_true", help="time the eager launches instead of the hipGraph replay")
     ap.add_argument("--dry-run", action="store_true", help="CPU stub workload over gloo (launcher test)")
@@ -235,8 +238,10 @@ def train_breakdown(ts, tnet, x, gt_code, gt_mask, world, rank, steps=3):
             times.append(time.perf_counter() - t0)
         ar = float(np.median(times))
         out.update(buckets=len(flats), bucket_mb=[b[1] for b in layout], grad_mb=round(nbytes / 2 ** 20, 2),
-                   allreduce_ms_standalone=round(ar * 1e3, 3),
-                   allreduce_busbw_GBps=round(2 * (world - 1) / world * nbytes / ar / 1e9, 1))
+                   allreduce_ms_standalone=round(ar * 1e3, 3), allreduce_algbw_GBps=round(nbytes / ar / 1e9, 1),
+                   backend=dist.get_backend(), world=world)
+        if world > 1:  # ring bus bandwidth 2 (N - 1) / N x bytes / time (0 at N = 1: nothing crosses a link)
+            out["allreduce_busbw_GBps"] = round(2 * (world - 1) / world * nbytes / ar / 1e9, 1)
         print(f"[rank {rank}] grad buckets (launch order): " + "; ".join(
             f"#{b} {mb} MB {n} params {first}..{last}" for b, mb, n, first, last in layout)
             + f" | enqueue ms into backward {out['bucket_enqueue_ms']} | exposed comm {out['exposed_comm_ms']} ms",
@@ -377,6 +382,135 @@ def main():
     run(args)
 
 
+def lib_sha16():
+    """Identity of the libzp.so build being benched (PMC traffic files carry the one they measured)."""
+    import hashlib
+    from zebrapose_amd import _lib
+    with open(_lib.LIB_PATH, "rb") as fh:
+        return hashlib.sha256(fh.read()).hexdigest()[:16]
+
+
+def pmc_traffic(kname):
+    """HBM bytes per launch of kernel instance ``kname`` from the newest committed PMC pass
+    (tools/prof_round.sh + tools/prof_summary.py -> profiles/<tag>_pmc_traffic.json) that was
+    measured on THIS libzp.so build (its lib_sha16); a pass of another build is refused, so the
+    number cannot go stale silently.  rocprofv3 cannot run inside this process."""
+    sha = lib_sha16()
+    for pf in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")), reverse=True):
+        if "_train_" in os.path.basename(pf):  # the eval (folded-BN) launches are the ones timed here
+            continue
+        with open(pf) as fh:
+            d = json.load(fh)
+        if d.get("lib_sha16") != sha:
+            continue
+        t = d.get("by_label", {}).get(kname)
+        if t is not None:
+            return t, os.path.relpath(pf, ROOT)
+    return None, f"no committed PMC pass of this libzp.so build (lib_sha16 {sha})"
+
+
+def time_infer(net, x, dec, bboxes, steps, warmup, world, dev, rank, use_graph=True):
+    """configs[1] step = forward + on-device decode of one bs=B batch resident in HBM.  The timed
+    step is one hipGraph replay of that step (zebrapose_amd.graphs; the crops are copied into the
+    graph's static input each step -- a device copy, timed); every kernel of the eager step runs,
+    only the ~50 per-launch host round trips are gone.  Barrier + synchronize on both sides of
+    the K timed steps; the max over ranks is the job time."""
+    B, S = x.shape[0], x.shape[-1]
+
+    def eager_step():
+        with torch.no_grad():
+            m, c = net(x)
+            return dec(m, c, bboxes, bbox_size=S // 2)
+
+    graph = None
+    if use_graph:
+        from zebrapose_amd.graphs import GraphedInference
+        try:
+            graph = GraphedInference(net, B, S, decoder=dec, bbox_size=S // 2)
+            graph.bb.copy_(torch.as_tensor(bboxes, dtype=torch.int32))
+        except RuntimeError as e:  # the same kernels, launched one by one (launch says which)
+            print(f"[bench] rank {rank}: hipGraph capture failed ({e}); timing the eager launches",
+                  file=sys.stderr, flush=True)
+            graph = None
+
+    def step():
+        if graph is None:
+            return eager_step()
+        return graph(x)[2:]
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = t.item()
+    n_corr = int(out[0].sum().item())
+    res = {"el": el, "ms_per_step": el / steps * 1e3, "value": world * B * steps / el, "n_corr": n_corr,
+           "launch": "eager" if graph is None else "hipgraph", "out": tuple(t.clone() for t in out)}
+    del graph
+    return res
+
+
+def conv_roofline(net, x, steps, precision, ms_per_step, layer_report=None, rank=0):
+    """Roofline of the dominant conv kernel instance (largest total time over the step's launches):
+    every conv launch of `steps` eager forwards bracketed by HIP events on the stream it runs on
+    (torch's current stream, where libzp enqueues); achieved = sum of algorithmic FLOPs
+    (2 * M * taps * Cin * Cout per launch) / sum of launch durations."""
+    eng = net.net._engine
+    eng.timing = []
+    with torch.no_grad():
+        for _ in range(steps):
+            net(x)
+    torch.cuda.synchronize()
+    per = {}
+    eng_t = eng.timing
+    eng.timing = None
+    for label, e0, e1, flops, kname, nbytes in eng_t:
+        d = per.setdefault(kname, [0.0, 0.0, 0, 0.0])
+        d[0] += flops
+        d[1] += e0.elapsed_time(e1) * 1e-3
+        d[2] += 1
+        d[3] += nbytes
+    if layer_report and rank == 0:
+        lay = {}
+        for label, e0, e1, flops, kname, _ in eng_t:
+            d = lay.setdefault(label, [kname, 0.0, 0.0, 0])
+            d[1] += e0.elapsed_time(e1) * 1e3
+            d[2] += flops
+            d[3] += 1
+        rows = [{"label": k, "kernel": v[0], "us": round(v[1] / v[3], 2), "tflops": round(v[2] / v[1] * 1e-6, 1)}
+                for k, v in lay.items()]
+        with open(layer_report, "w") as f:
+            json.dump(rows, f, indent=0)
+    kname, (fl, tsec, nl, algo_bytes) = max(per.items(), key=lambda kv: kv[1][1])
+    achieved = fl / tsec / 1e12
+    traffic, traffic_src = pmc_traffic(kname)
+    algo_per_launch = algo_bytes / nl
+    B = x.shape[0]
+    all_fl = sum(v[0] for v in per.values())
+    all_t = sum(v[1] for v in per.values())
+    return {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 2), "peak": PEAK[precision],
+            "unit": "TFLOP/s", "frac": round(achieved / PEAK[precision], 4), "traffic": traffic,
+            "traffic_source": traffic_src, "algorithmic_bytes_per_launch": round(algo_per_launch),
+            "traffic_over_algorithmic": None if traffic is None else round(traffic / algo_per_launch, 3),
+            "launches_per_step": nl // steps, "avg_launch_us": round(tsec / nl * 1e6, 2),
+            "algorithmic_flop_per_launch": round(fl / nl),
+            "all_conv_tflops": round(all_fl / all_t / 1e12, 2),
+            "conv_ms_per_step": round(all_t / steps * 1e3, 3),
+            "whole_step_tflops": round(FWD_GFLOP_PER_CROP * 1e9 * B / (ms_per_step * 1e-3) / 1e12, 2),
+            "lib_sha16": lib_sha16()}
+
+
 def run(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -391,9 +525,16 @@ def run(args):
         return
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    rccl1 = False
     if world > 1:
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
         world = dist.get_world_size()  # the ranks that actually joined the RCCL group
+    elif not args.no_rccl and not args.no_train:
+        # N = 1: a world-size-1 RCCL group, so the train leg's data-parallel gradient exchange
+        # (configs[3]'s code path: GradBuckets' async all_reduce on the RCCL stream) runs for real
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                                device_id=dev)
+        rccl1 = True
 
     from zebrapose_amd.model.BinaryCodeNet import BinaryCodeNet_Deeplab
     from zebrapose_amd.decode import Decoder
@@ -413,131 +554,29 @@ def run(args):
             m, c = net(x)
             return dec(m, c, bboxes, bbox_size=S // 2)
 
-    # The timed step is one hipGraph replay of the same forward + decode (zebrapose_amd.graphs):
-    # the crops are copied into the graph's static input each step (a 25 MB device copy, timed);
-    # the boxes are uploaded once.  Every kernel of the eager step runs; only the ~50 per-launch
-    # host round trips are gone.  --eager times the launches one by one (also reported below).
-    graph = None
-    if not args.eager:
-        from zebrapose_amd.graphs import GraphedInference
-        try:
-            graph = GraphedInference(net, B, S, decoder=dec, bbox_size=S // 2)
-            graph.bb.copy_(torch.as_tensor(bboxes, dtype=torch.int32))
-        except RuntimeError as e:  # the same kernels, launched one by one (config.launch says which)
-            print(f"[bench] rank {rank}: hipGraph capture failed ({e}); timing the eager launches",
-                  file=sys.stderr, flush=True)
-            graph = None
-
-    def step():
-        if graph is None:
-            return eager_step()
-        return graph(x)[2:]
-
     # ------------------------------------------------------------------ inference (value)
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        out = step()
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    if world > 1:
-        dist.barrier()
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = t.item()
-    ms_per_step = el / args.steps * 1e3
-    value = world * B * args.steps / el
-    n_corr = int(out[0].sum().item())
+    main = time_infer(net, x, dec, bboxes, args.steps, args.warmup, world, dev, rank, use_graph=not args.eager)
+    value, ms_per_step, n_corr, out = main["value"], main["ms_per_step"], main["n_corr"], main["out"]
+    roofline = conv_roofline(net, x, args.steps, args.precision, ms_per_step, args.layer_report, rank)
 
-    # ------------------------------------------------------------------ roofline of the dominant kernel
-    eng = net.net._engine
-    eng.timing = []
-    with torch.no_grad():
-        for _ in range(args.steps):
-            net(x)
-    torch.cuda.synchronize()
-    per = {}
-    eng_t = eng.timing
-    eng.timing = None
-    # group launches by kernel instantiation (the names rocprofv3 reports)
-    for rec in eng_t:
-        label, e0, e1, flops, kname, nbytes = rec
-        d = per.setdefault(kname, [0.0, 0.0, 0, 0.0])
-        d[0] += flops
-        d[1] += e0.elapsed_time(e1) * 1e-3
-        d[2] += 1
-        d[3] += nbytes
-    if args.layer_report and rank == 0:
-        lay = {}
-        for label, e0, e1, flops, kname, _ in eng_t:
-            d = lay.setdefault(label, [kname, 0.0, 0.0, 0])
-            d[1] += e0.elapsed_time(e1) * 1e3
-            d[2] += flops
-            d[3] += 1
-        rows = [{"label": k, "kernel": v[0], "us": round(v[1] / v[3], 2), "tflops": round(v[2] / v[1] * 1e-6, 1)}
-                for k, v in lay.items()]
-        with open(args.layer_report, "w") as f:
-            json.dump(rows, f, indent=0)
-    dom = max(per.items(), key=lambda kv: kv[1][1])
-    kname, (fl, tsec, nl, algo_bytes) = dom
-    achieved = fl / tsec / 1e12
-    traffic = None
-    # HBM bytes per launch of this kernel instance from the committed PMC passes (rocprofv3 cannot
-    # run inside this process): tools/prof_round.sh + tools/prof_summary.py -> profiles/<tag>_pmc_traffic.json
-    traffic_src = None
-    for pf in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")), reverse=True):
-        if "_train_" in os.path.basename(pf):  # the eval (folded-BN) launches are the ones timed here
-            continue
-        with open(pf) as fh:
-            traffic = json.load(fh).get("by_label", {}).get(kname)
-        if traffic is not None:
-            traffic_src = os.path.relpath(pf, ROOT)
-            break
-    all_conv_flops = sum(v[0] for v in per.values())  # noqa
-    all_conv_time = sum(v[1] for v in per.values())
-    algo_per_launch = algo_bytes / nl
-    roofline = {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 2), "peak": PEAK[args.precision],
-                "unit": "TFLOP/s", "frac": round(achieved / PEAK[args.precision], 4), "traffic": traffic,
-                "traffic_source": traffic_src, "algorithmic_bytes_per_launch": round(algo_per_launch),
-                "traffic_over_algorithmic": None if traffic is None else round(traffic / algo_per_launch, 3),
-                "launches_per_step": nl // args.steps, "avg_launch_us": round(tsec / nl * 1e6, 2),
-                "all_conv_tflops": round(all_conv_flops / all_conv_time / 1e12, 2),
-                "whole_step_tflops": round(FWD_GFLOP_PER_CROP * 1e9 * B / (ms_per_step * 1e-3) / 1e12, 2)}
-
-    # ------------------------------------------------------------------ fp32 mode at the same config
-    # (the reference's own precision; f32 MFMA v_mfma_f32_16x16x4_f32, 157.3 TFLOP/s dense peak)
-    fp32 = None
-    if not args.no_fp32 and args.precision != "fp32":
-        net.set_precision("fp32")
-        for _ in range(2):
-            eager_step()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        K2 = max(3, args.steps // 2)
-        t0 = time.perf_counter()
-        for _ in range(K2):
-            eager_step()
-        torch.cuda.synchronize()
-        el2 = time.perf_counter() - t0
-        if world > 1:
-            t = torch.tensor([el2], device=dev, dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el2 = t.item()
-        tfl = FWD_GFLOP_PER_CROP * 1e9 * B * K2 / el2 / 1e12
-        fp32 = {"crops_per_s": round(world * B * K2 / el2, 2), "ms_per_step": round(el2 / K2 * 1e3, 3), "steps": K2,
-                "dtype": "f32", "whole_step_tflops": round(tfl, 2), "frac_of_f32_peak": round(tfl / PEAK["fp32"], 4)}
+    # ------------------------------------------------------------------ bf16 leg (throughput mode)
+    # the same step with bf16 storage / bf16 MFMA (f32 accumulate): narrower than the reference's
+    # fp32, so a labelled extra with its own roofline, not the headline
+    bf16 = None
+    if args.precision != "bf16" and not args.no_bf16:
+        net.set_precision("bf16")
+        r = time_infer(net, x, dec, bboxes, args.steps, args.warmup, world, dev, rank, use_graph=not args.eager)
+        bf16 = {"crops_per_s": round(r["value"], 2), "ms_per_step": round(r["ms_per_step"], 3), "dtype": "bf16",
+                "launch": r["launch"], "steps": args.steps,
+                "roofline": conv_roofline(net, x, args.steps, "bf16", r["ms_per_step"])}
         net.set_precision(args.precision)
+        torch.cuda.empty_cache()
 
     # ------------------------------------------------------------------ bs=1 latency: eager vs hipGraph
     bs1 = None
     if not args.no_bs1 and rank == 0:
         bs1 = bs1_leg(net, dec, S, dev)
+        bs1["dtype"] = args.precision
         # the benched batch launched eagerly, one launch at a time (value is the graph replay)
         for _ in range(2):
             eager_step()
@@ -594,45 +633,65 @@ def run(args):
     del imgs, gts, msk
 
     # ------------------------------------------------------------------ training step (extra)
+    # configs[2]: bs=32 per GPU, bf16 (BASELINE.json), hist-weighted BCE + mask loss, backward, Adam;
+    # configs[3] at N > 1 (DDP over RCCL).  At N = 1 the same step also runs through a world-size-1
+    # RCCL group (rccl_world1): every bucket's all_reduce is a real RCCL collective on its stream.
     train = None
+    tprec = "bf16"
     if not args.no_train:
         from zebrapose_amd.train import TrainStep
-        tnet = BinaryCodeNet_Deeplab(34, 16, 2, concat=True, output_kernel_size=1, precision=args.precision).to(dev)
+        tnet = BinaryCodeNet_Deeplab(34, 16, 2, concat=True, output_kernel_size=1, precision=tprec).to(dev)
         calibrate_bn(tnet, x)
         tnet.train()
         lr = 2e-4 * world  # train_v6.py:89-91
-        ts = TrainStep(tnet, learning_rate=lr)
         g = torch.Generator(device="cpu").manual_seed(7 + rank)
         gt_code = (torch.rand((B, 16, S // 2, S // 2), generator=g) < 0.5).to(torch.uint8).to(dev)
         gt_mask = (torch.rand((B, S // 2, S // 2), generator=g) < 0.7).float().to(dev)
         K = args.train_steps or max(3, args.steps // 2)
-        for _ in range(max(2, args.warmup // 2)):
-            ts(x, gt_code, gt_mask)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        t0 = time.perf_counter()
-        for _ in range(K):
-            loss = ts(x, gt_code, gt_mask)
-        torch.cuda.synchronize()
-        tel = time.perf_counter() - t0
-        if world > 1:
-            t = torch.tensor([tel], device=dev, dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            tel = t.item()
+
+        def timed_train(ts):
+            for _ in range(max(2, args.warmup // 2)):
+                ts(x, gt_code, gt_mask)
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(K):
+                loss = ts(x, gt_code, gt_mask)
+            torch.cuda.synchronize()
+            tel = time.perf_counter() - t0
+            if world > 1:
+                t = torch.tensor([tel], device=dev, dtype=torch.float64)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                tel = t.item()
+            return tel, loss
+
+        ts = TrainStep(tnet, learning_rate=lr)
+        tel, loss = timed_train(ts)
         train = {"crops_per_s": round(world * B * K / tel, 2), "ms_per_step": round(tel / K * 1e3, 3),
-                 "steps": K, "global_batch": world * B, "loss": round(float(loss[0].item()), 5),
+                 "steps": K, "global_batch": world * B, "dtype": tprec, "loss": round(float(loss[0].item()), 5),
                  "achieved_tflops": round(3 * FWD_GFLOP_PER_CROP * 1e9 * world * B * K / tel / 1e12 / world, 2),
                  "parallelism": f"ddp{world}" if world > 1 else "single"}
         train["breakdown"] = train_breakdown(ts, tnet, x, gt_code, gt_mask, world, rank)
-        del ts, tnet
+        del ts
+        if rccl1:
+            ts = TrainStep(tnet, learning_rate=lr, ddp=True, device=local)
+            tel, _ = timed_train(ts)
+            train["rccl_world1"] = {
+                "what": "the same step through a world-size-1 RCCL process group (backend nccl): GradBuckets' "
+                        "bucketed async all_reduce on the RCCL stream, overlapped with the backward, plus the "
+                        "per-forward BN buffer broadcast -- configs[3]'s exchange code, on one GPU",
+                "ms_per_step": round(tel / K * 1e3, 3), "crops_per_s": round(B * K / tel, 2),
+                "breakdown": train_breakdown(ts, tnet, x, gt_code, gt_mask, 1, rank)}
+            del ts
+        del tnet
 
     # ------------------------------------------------------------------ 3-head v3 network (extra, §8f rank 3)
     v3 = None
     if not args.no_train:
         from zebrapose_amd.model.BinaryCodeNet_v3 import BinaryCodeNet_Deeplab_v3
         from zebrapose_amd.train import TrainStep
-        n3 = BinaryCodeNet_Deeplab_v3(34, 16, 2, concat=True, output_kernel_size=1, precision=args.precision).to(dev)
+        n3 = BinaryCodeNet_Deeplab_v3(34, 16, 2, concat=True, output_kernel_size=1, precision=tprec).to(dev)
         calibrate_bn(n3, x)
         with torch.no_grad():
             n3(x)
@@ -658,7 +717,7 @@ def run(args):
             ts3(x, gt_code, gt_mask, gt_ent)
         torch.cuda.synchronize()
         tr_ms = (time.perf_counter() - t0) / K3 * 1e3
-        v3 = {"model": "BinaryCodeNet_Deeplab_v3(34, 16, 2, concat=True) (train_v5.py)", "batch": B,
+        v3 = {"model": "BinaryCodeNet_Deeplab_v3(34, 16, 2, concat=True) (train_v5.py)", "batch": B, "dtype": tprec,
               "infer_crops_per_s": round(B / (inf_ms * 1e-3), 1), "infer_ms_per_step": round(inf_ms, 3),
               "train_crops_per_s": round(B / (tr_ms * 1e-3), 1), "train_ms_per_step": round(tr_ms, 3)}
         del ts3, n3
@@ -674,20 +733,21 @@ def run(args):
         cpu = cpu_baseline(args, net, x, bboxes)
 
     if rank == 0:
+        dname = {"fp32": "f32", "bf16": "bf16"}[args.precision]
         line = {"metric": "256x256 crops/sec (R34 DeepLabv3 inference bs=32, forward + code->vertex decode)",
                 "value": round(value, 2), "unit": "crops/s", "n_gpus": world, "steps": args.steps,
                 "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
-                "scaling": "weak", "vs_baseline": None, "dtype": args.precision, "data": "synthetic",
+                "scaling": "weak", "vs_baseline": None, "dtype": dname, "data": "synthetic",
                 "config": {"workload": "configs[1]: ResNet34+DeepLabv3 inference bs=32 on 1xMI355X, synthetic "
                                        "256x256 crops, 16-bit code head, on-device decode",
                            "model": "BinaryCodeNet_Deeplab(34, 16, 2, concat=True)", "global_batch": world * B,
                            "per_gpu_batch": B, "input": f"{S}x{S}", "parallelism": f"replicas{world}",
-                           "launch": "eager" if graph is None else "hipgraph",
+                           "precision": args.precision, "launch": main["launch"],
                            "correspondences_last_step": n_corr},
-                "roofline": roofline, "fp32": fp32, "bs1": bs1, "cpu_baseline": cpu, "train": train, "pnp": pnp_res, "crop": crop_res, "v3": v3,
-                "multi_object": multi}
+                "roofline": roofline, "bf16": bf16, "bs1": bs1, "cpu_baseline": cpu, "train": train, "pnp": pnp_res,
+                "crop": crop_res, "v3": v3, "multi_object": multi}
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -1,0 +1,119 @@
+"""configs[3]'s gradient exchange over RCCL (backend "nccl"), as far as one GPU allows: a
+world-size-1 RCCL process group on cuda:0 drives exactly the data-parallel code of the 8-GPU run
+(reference train_v6.py:50-51 init_process_group, :259 DistributedDataParallel, :337 backward
+all-reduce): GradBuckets' async all_reduce on the process group's stream, the current-stream ->
+RCCL-stream hand-off, finish()'s wait(), the per-forward BN buffer broadcast; and torch's own
+DistributedDataParallel(net) over the libzp network (ZP_TORCH_DDP=1).
+
+At world size 1 the mean over ranks is the local gradient, so the averaged gradients must equal
+the plain local ones BIT FOR BIT (the backward is deterministic: fixed-order split reductions)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(port, mode, q):
+    os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      ZP_QUIET="1")
+    if mode == "torch_ddp":
+        os.environ["ZP_TORCH_DDP"] = "1"
+    try:
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+        from zebrapose_amd import parallel as P
+        from zebrapose_amd.model.BinaryCodeNet import BinaryCodeNet_Deeplab
+        from zebrapose_amd.train import TrainStep
+        torch.manual_seed(0)
+        net = BinaryCodeNet_Deeplab(34, 16, 2, concat=True, output_kernel_size=1, precision="bf16").to(dev)
+        net.train()
+        g = torch.Generator().manual_seed(5)
+        x = torch.randn(2, 3, 64, 64, generator=g).to(dev)
+        gt = (torch.rand(2, 16, 32, 32, generator=g) < 0.5).to(torch.uint8).to(dev)
+        gm = (torch.rand(2, 32, 32, generator=g) < 0.7).float().to(dev)
+        ts0 = TrainStep(net, ddp=False, learning_rate=0.0)
+        ts0.optimizer.step = lambda: None
+        ts0(x, gt, gm)
+        local = {n: p.grad.detach().clone() for n, p in net.named_parameters()}
+        # count the BN-buffer broadcasts (DDP broadcast_buffers=True: one per forward)
+        calls = {"bcast": 0}
+        orig = dist._broadcast_coalesced
+
+        def counting(*a, **k):
+            calls["bcast"] += 1
+            return orig(*a, **k)
+        dist._broadcast_coalesced = counting
+        ts = TrainStep(net, ddp=True, learning_rate=0.0, device=0)
+        ts.optimizer.step = lambda: None
+        works = []
+        if mode == "buckets":
+            assert ts.buckets is not None and ts.net is net
+            assert dist.get_backend() == "nccl"
+            launch = ts.buckets._launch
+
+            def recording(b):
+                launch(b)
+                works.append(ts.buckets.buckets[b][3])
+            ts.buckets._launch = recording
+            ts.buckets.timing = []
+        else:
+            assert ts.buckets is None and isinstance(ts.net, torch.nn.parallel.DistributedDataParallel)
+        bc0 = calls["bcast"]
+        ts(x, gt, gm)
+        torch.cuda.synchronize()
+        diffs = {n: int((p.grad != local[n]).sum().item()) for n, p in net.named_parameters()}
+        res = {"mode": mode, "diffs": diffs, "bcast": calls["bcast"] - bc0, "nparams": len(local)}
+        if mode == "buckets":
+            res["nbuckets"] = len(ts.buckets.buckets)
+            res["launched"] = len(works)
+            res["completed"] = sum(1 for w in works if w.is_completed())
+            tl = ts.buckets.timing
+            res["done_event"] = sum(1 for b, _ in tl if b == "done")
+            # the exchange itself, standalone: every bucket all-reduced on the RCCL stream
+            flats = [bk[0] for bk in ts.buckets.buckets]
+            ref = [f.clone() for f in flats]
+            for f in flats:
+                dist.all_reduce(f, op=dist.ReduceOp.SUM)
+            torch.cuda.synchronize()
+            res["allreduce_identity"] = all(torch.equal(a, b) for a, b in zip(flats, ref))
+        q.put(res)
+    except Exception as e:  # reported to the parent as a failure message
+        q.put({"error": repr(e)})
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["buckets", "torch_ddp"])
+def test_rccl_world1_grad_exchange(gpu, mode):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker, args=(_free_port(), mode, q))
+    p.start()
+    try:
+        res = q.get(timeout=110)
+    finally:
+        p.join(timeout=60)
+    assert "error" not in res, res.get("error")
+    assert p.exitcode == 0
+    bad = {n: d for n, d in res["diffs"].items() if d}
+    assert not bad, f"averaged gradients differ from the local ones: {bad}"
+    assert res["nparams"] == 152
+    if mode == "buckets":
+        assert res["nbuckets"] >= 4  # 116 MB of f32 gradients in ~25 MB buckets
+        assert res["launched"] == res["nbuckets"] == res["completed"]
+        assert res["done_event"] == 1
+        assert res["bcast"] == 1  # rank 0's BN buffers broadcast before the forward
+        assert res["allreduce_identity"]

@@ -9,7 +9,7 @@ O=gpurun_out/prof_$TAG
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/infer -o run -- \
-    python3 bench.py --no-train --no-cpu --no-multi --no-fp32 --no-bs1 --steps 10 --warmup 3 > $O/infer.log 2>&1
+    python3 bench.py --no-train --no-cpu --no-multi --no-bf16 --no-bs1 --steps 10 --warmup 3 > $O/infer.log 2>&1
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/train -o run -- \
     python3 tools/prof_driver.py --mode train --steps 5 --warmup 2 > $O/train.log 2>&1
 timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/pmc_fetch -o run -- \

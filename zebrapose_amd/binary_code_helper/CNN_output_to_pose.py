@@ -57,7 +57,11 @@ def _fingerprint(d):
 
 def _decoder_for(dict_class_id_3D_points, device):
     """The cache entry keeps a strong reference to the dict, so its id() cannot be recycled by
-    another object while cached; a changed size / sampled entry rebuilds the LUT."""
+    another object while cached; a changed size / sampled entry rebuilds the LUT.
+
+    The dict is treated as immutable once loaded (as the reference's test.py uses it): an in-place
+    edit of entries outside the sampled ids (_FP_IDS) that keeps the size is NOT detected.  After
+    editing a loaded dict in place, call ``clear_decoder_cache()``."""
     key = (id(dict_class_id_3D_points), str(device))
     fp = _fingerprint(dict_class_id_3D_points)
     hit = _DEC_CACHE.get(key)
@@ -70,6 +74,11 @@ def _decoder_for(dict_class_id_3D_points, device):
     while len(_DEC_CACHE) > _DEC_CACHE_MAX:
         _DEC_CACHE.popitem(last=False)
     return dec
+
+
+def clear_decoder_cache():
+    """Drop every cached device LUT (after editing a loaded class-id dict in place)."""
+    _DEC_CACHE.clear()
 
 
 def _bits_to_logits(bits):

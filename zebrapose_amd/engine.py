@@ -104,11 +104,18 @@ class Engine:
         self._job_table = None
         self._folds = {}
         self._fold_epoch = 0
+        self._cache_gen = 0  # bumped when a packing / fold buffer is allocated or dropped (graphs.py)
         self.timing = None  # optional list of (label, start_event, end_event) for conv launches
         # optional list: every eval-mode op appends (kind, unit, x, out, res) with the buffers it
         # read and wrote (kept alive by the list) -- the teacher-forced layer parity tests replay
         # each op on the host from the device's own stored inputs (tests/test_gpu_bench_geometry.py)
         self.trace = None
+        # optional list: every conv launch appends (stage, kernel label, flops, algorithmic bytes) in
+        # launch order; self.stage names the network stage being enqueued (stem, layer1, layer2,
+        # layer4, layer5, aspp, up1, up2, head) -- tools/prof_stages.py attributes rocprofv3's
+        # per-dispatch counters to stages with it
+        self.stage_log = None
+        self.stage = None
         # optional list: every training-backward op appends a dict with the buffers it read and the
         # gradients it wrote (accumulated gradient slices as (before, after) copies) -- the
         # teacher-forced train-step parity test replays each one on the host (tests/test_gpu_train_tf.py)
@@ -124,6 +131,7 @@ class Engine:
 
     # ------------------------------------------------------------------ weight / BN caches
     def invalidate(self):
+        self._cache_gen += 1
         self._packed.clear()
         self._jobs = []
         self._job_table = None
@@ -139,8 +147,11 @@ class Engine:
         if hit is not None and hit[0] == ver:
             return hit[1]
         d0, d1 = w.shape[0], w.shape[1]
-        out = hit[1] if hit is not None and hit[1].shape == (rows, k_pad) else \
-            torch.empty((rows, k_pad), dtype=self.dtype, device=w.device)
+        if hit is not None and hit[1].shape == (rows, k_pad):
+            out = hit[1]
+        else:
+            out = torch.empty((rows, k_pad), dtype=self.dtype, device=w.device)
+            self._cache_gen += 1
         ky = [t[0] for t in sub.taps]
         kx = [t[1] for t in sub.taps]
         L.call("zp_pack_weight", w.data_ptr(), d0, d1, w.shape[2], w.shape[3], transposed, len(sub.taps),
@@ -194,8 +205,12 @@ class Engine:
         if hit is not None and hit[0] == vers:
             return hit[1], hit[2]
         dev = bn.weight.device
-        scale = torch.empty(unit.cout, dtype=torch.float32, device=dev)
-        shift = torch.empty_like(scale)
+        if hit is not None:  # refold in place: a captured graph keeps reading these addresses
+            scale, shift = hit[1], hit[2]
+        else:
+            scale = torch.empty(unit.cout, dtype=torch.float32, device=dev)
+            shift = torch.empty_like(scale)
+            self._cache_gen += 1
         L.call("zp_bn_fold", bn.weight.data_ptr(), bn.bias.data_ptr(), bn.running_mean.data_ptr(),
                bn.running_var.data_ptr(), L.ptr(bias), C.c_float(bn.eps), unit.cout, scale.data_ptr(),
                shift.data_ptr(), L.stream_ptr())
@@ -236,25 +251,16 @@ class Engine:
         if stats is not None:
             a.stats = stats.data_ptr()
         st = L.stream_ptr()
-        if self.timing is not None:
-            e0 = torch.cuda.Event(enable_timing=True)
-            e1 = torch.cuda.Event(enable_timing=True)
-            e0.record()
+        if self.timing is not None or self.stage_log is not None:
+            if self.timing is not None:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record()
             L.check(L.lib.zp_conv2d(C.byref(a), st), "zp_conv2d")
-            e1.record()
+            if self.timing is not None:
+                e1.record()
             flops = 2.0 * x.B * plan.GH * plan.GW * sum(len(sb.taps) for sb in plan.subs) * x.C * cout
-            tc, tp, stages, var = C.c_int(), C.c_int(), C.c_int(), C.c_int()
-            L.call("zp_conv2d_config", C.byref(a), C.byref(tc), C.byref(tp), C.byref(stages), C.byref(var))
-            tn = {L.ZP_F32: "f32", L.ZP_BF16: "bf16", L.ZP_F16: "f16"}[self.dt]
-            if var.value == 1:  # rocprofv3 name: k_conv_strip<T, WC, STAGES, SPW = 5>
-                kname = f"k_conv_strip<{tn},WC={tc.value // 32},ST=3>"
-            elif var.value == 3:  # rocprofv3 name: k_conv_quad<T, W>
-                kname = f"k_conv_quad<{tn},W={plan.GW}>"
-            elif var.value == 2:  # rocprofv3 name: k_conv_strip2<T, WC, SPW = 5>
-                kname = f"k_conv_strip2<{tn},WC={tc.value // 32}>"
-            else:  # rocprofv3 name: k_conv<T, WC = tc / 32, WP = 4, NWP = tp / 64, STAGES, smallC>
-                kname = (f"k_conv<{tn},WC={tc.value // 32},WP=4,"
-                         f"NWP={tp.value // 64},ST={stages.value},smallC={int(x.C < _KE[self.dt])}>")
+            kname = self._kname(a, plan, x)
             geo = (f"{label}:{x.C}->{cout} taps{max(len(sb.taps) for sb in plan.subs)} "
                    f"{x.H}x{x.W}->{plan.GH}x{plan.GW}x{a.nsub}")
             # algorithmic HBM bytes: the input slice and every output read / written once, the
@@ -264,10 +270,29 @@ class Engine:
             mgrid = x.B * plan.GH * plan.GW
             nbytes = (x.P * x.C * es + len(plan.subs) * mgrid * cout * osz
                       + sum(w.numel() * w.element_size() for w in weights) + (0 if res is None else mgrid * cout * es))
-            self.timing.append((geo, e0, e1, flops, kname, nbytes))
+            if self.timing is not None:
+                self.timing.append((geo, e0, e1, flops, kname, nbytes))
+            if self.stage_log is not None:
+                self.stage_log.append((self.stage, kname, flops, nbytes, geo))
         else:
             L.check(L.lib.zp_conv2d(C.byref(a), st), "zp_conv2d")
         return stats, parts
+
+    def _kname(self, a, plan, x):
+        """rocprofv3's kernel instantiation of this launch, in the label form tools/prof_summary.py
+        maps the demangled names to."""
+        tc, tp, stages, var = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+        L.call("zp_conv2d_config", C.byref(a), C.byref(tc), C.byref(tp), C.byref(stages), C.byref(var))
+        tn = {L.ZP_F32: "f32", L.ZP_BF16: "bf16", L.ZP_F16: "f16"}[self.dt]
+        if var.value == 1:  # rocprofv3 name: k_conv_strip<T, WC, STAGES, SPW = 5>
+            return f"k_conv_strip<{tn},WC={tc.value // 32},ST=3>"
+        if var.value == 3:  # rocprofv3 name: k_conv_quad<T, W>
+            return f"k_conv_quad<{tn},W={plan.GW}>"
+        if var.value == 2:  # rocprofv3 name: k_conv_strip2<T, WC, SPW = 5>
+            return f"k_conv_strip2<{tn},WC={tc.value // 32}>"
+        # rocprofv3 name: k_conv<T, WC = tc / 32, WP = 4, NWP = tp / 64, STAGES, smallC>
+        return (f"k_conv<{tn},WC={tc.value // 32},WP=4,"
+                f"NWP={tp.value // 64},ST={stages.value},smallC={int(x.C < _KE[self.dt])}>")
 
     def _kpad(self, ntaps, cin):
         return G.ceil_to(ntaps * cin, _KE[self.dt])
@@ -532,8 +557,12 @@ class Engine:
             # bias); the gradients are handed over (grads / GradBuckets.ready copies) from the side
             # stream too, so a bucket's all-reduce is ordered after its weight gradients
             side.wait_stream(torch.cuda.current_stream(dev))
+            # dw is allocated on the main stream, which consumes and frees it (Adam, zero_grad):
+            # the block belongs to that stream's pool, and record_stream keeps it from being
+            # reused there before the side stream's wgrad has written it
+            dw = torch.empty_like(conv.weight)
+            dw.record_stream(side)
             with torch.cuda.stream(side):
-                dw = torch.empty_like(conv.weight)
                 self._wgrad(unit, x, plan, wdy, dw)
                 for k, v in pending.items():
                     grads[k] = v
@@ -587,6 +616,7 @@ class Engine:
 
         self._prepack(dev)
         st = L.stream_ptr()
+        self.stage = "stem"
         xin = new(H, W, 8)
         L.call("zp_nchw_to_nhwc", x.data_ptr(), B, 3, H, W, 8, self.dt, xin.ptr, st)
         if self.trace is not None and tape is None:
@@ -598,6 +628,7 @@ class Engine:
         head_in = torch.empty((B, H2, W2, 320), dtype=dt, device=dev)
         x128 = Act(head_in, 256, 64)
         self.unit_fwd(self._u(r[0], r[1], True, cin_act=8), xin, x128, tape, label="stem")
+        self.stage = "layer1"
         pooled = new(H4, W4, 64)
         L.call("zp_maxpool3s2", x128.ptr, B, H2, W2, x128.ld, x128.c0, 64, self.dt, pooled.ptr, H4, W4, 64, 0, st)
         if tape is not None:
@@ -607,10 +638,14 @@ class Engine:
         up2_in = torch.empty((B, H4, W4, 256 + c64), dtype=dt, device=dev)
         x64 = Act(up2_in, 256, c64)
         h = self._layer(r[4], pooled, x64, tape)
+        self.stage = "layer2"
         h = self._layer(r[5], h, None, tape)
+        self.stage = "layer4"
         h = self._layer(rn.layer4, h, None, tape)
+        self.stage = "layer5"
         xh = self._layer(rn.layer5, h, None, tape)
         # ---- ASPP (aspp.py:83-99)
+        self.stage = "aspp"
         A = torch.empty((B, H8, W8, 1280), dtype=dt, device=dev)
         br = [self._u(aspp.conv_1x1_1, aspp.bn_conv_1x1_1), self._u(aspp.conv_3x3_1, aspp.bn_conv_3x3_1),
               self._u(aspp.conv_3x3_2, aspp.bn_conv_3x3_2), self._u(aspp.conv_3x3_3, aspp.bn_conv_3x3_3)]
@@ -631,8 +666,11 @@ class Engine:
         o = new(H8, W8, 256)
         self.unit_fwd(self._u(aspp.conv_1x1_3, aspp.bn_conv_1x1_3), Act(A), o, tape, label="aspp_proj")
         # ---- decoder (aspp.py:101-112)
+        self.stage = "up1"
         self._upsample(aspp.upsample_1, o, Act(up2_in, 0, 256), tape)
+        self.stage = "up2"
         self._upsample(aspp.upsample_2, Act(up2_in), Act(head_in, 0, 256), tape)
+        self.stage = "head"
         ncls = aspp.conv_1x1_4.out_channels
         mask = torch.empty((B, 1, H2, W2), dtype=torch.float32, device=dev)
         code = torch.empty((B, ncls - 1, H2, W2), dtype=torch.float32, device=dev)

@@ -9,12 +9,29 @@ decode, and each later call is one graph launch.
 Inputs and outputs are static device tensors owned by the graph: a call copies the crops (and
 boxes) in, replays, and returns views that stay valid until the next call.  Weight packings and
 BN folds are cached by the eager warm-up run and referenced by address, so build a new
-GraphedInference after changing the weights (load_state_dict, an optimizer step).
+GraphedInference after changing the weights (load_state_dict, an optimizer step): a call after
+such a change raises instead of replaying kernels that read stale (or freed) packings.
 """
 from __future__ import annotations
 
 import numpy as np
 import torch
+
+
+def _engines(net):
+    return [m._engine for m in net.modules() if hasattr(m, "_engine")]
+
+
+def _state_tensors(net):
+    return list(net.parameters()) + list(net.buffers())
+
+
+def _state_stamp(ts, engines):
+    """The version counter of every parameter and buffer (what the engine's packing / fold caches
+    are keyed on), plus each engine's BN-fold epoch and cache generation (bumped whenever a packing
+    or fold buffer is allocated, replaced or dropped -- this catches re-addressed tensors too).
+    ~35 us for the R34 net's 296 tensors; (version, data_ptr) pairs cost 3x that per call."""
+    return [t._version for t in ts], [(e._fold_epoch, e._cache_gen) for e in engines]
 
 
 class GraphedInference:
@@ -39,6 +56,8 @@ class GraphedInference:
         # thread_local: under torch.distributed the RCCL watchdog thread may query events meanwhile
         with torch.no_grad(), torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
             self.out = self._step()
+        self._tensors, self._engs = _state_tensors(net), _engines(net)
+        self._stamp = _state_stamp(self._tensors, self._engs)
 
     def _step(self):
         mask, code = self.net(self.x)
@@ -52,6 +71,9 @@ class GraphedInference:
         attached -> (mask, code) or (mask, code, counts, xy, xyz), the graph's static outputs."""
         if tuple(x.shape) != tuple(self.x.shape):
             raise ValueError(f"captured for input {tuple(self.x.shape)}, got {tuple(x.shape)}")
+        if _state_stamp(self._tensors, self._engs) != self._stamp:
+            raise RuntimeError("GraphedInference: the network's weights or BN buffers changed since capture "
+                               "(the graph reads the packings made then); build a new GraphedInference")
         self.x.copy_(x, non_blocking=True)
         if bboxes is not None:
             self.bb.copy_(torch.as_tensor(np.asarray(bboxes), dtype=torch.int32).reshape(self.bb.shape),
@@ -89,11 +111,28 @@ class GraphedTrainStep:
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
             self.out = ts(self.x, self.gc, self.gm)
+        # the replayed FusedAdam launches carry lr / betas / eps as captured
+        self._hyper = self._hyperparams()
+
+    def _hyperparams(self):
+        return [(g["lr"], tuple(g["betas"]), g["eps"]) for g in self.ts.optimizer.param_groups]
 
     def __call__(self, x, gt_code, gt_mask):
         """-> (loss, loss_b, loss_m), the graph's static output tensors (valid until the next call)."""
+        if self._hyperparams() != self._hyper:
+            raise RuntimeError("GraphedTrainStep: optimizer lr / betas / eps changed since capture (the graph "
+                               "replays the captured values); capture a new GraphedTrainStep after a schedule step")
         self.x.copy_(x, non_blocking=True)
         self.gc.copy_(gt_code, non_blocking=True)
         self.gm.copy_(gt_mask, non_blocking=True)
         self.graph.replay()
+        # the replay changed parameters, Adam state and BN running statistics on the device behind
+        # the host's version counters: bump them (and the engines' fold epochs) so the engine's
+        # eval packings / BN folds are rebuilt by the next eager or eval forward
+        net = self.ts.module
+        with torch.no_grad():
+            for t in list(net.parameters()) + list(net.buffers()):
+                torch.autograd.graph.increment_version(t)
+        for e in _engines(net):
+            e._fold_epoch += 1
         return self.out
