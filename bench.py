@@ -43,6 +43,19 @@ sys.path.insert(0, ROOT)
 os.environ.setdefault("ZP_QUIET", "1")
 
 PEAK = {"bf16": 2516.6, "fp32": 157.3}  # TFLOP/s dense MFMA (256 CU x 4 SIMD x 2.4 GHz; MI355X_MICROARCH.md)
+# The split-fp32 kernel (k_conv3, include/zp.h ZP_F32X3) forms each f32 product from 6 bf16 MFMA
+# products: its MFMA ceiling in f32 FLOP/s is the dense bf16 peak / 6.
+PEAK_X3 = PEAK["bf16"] / 6.0
+
+
+def peak_of(kname, precision):
+    """(peak TFLOP/s, basis) for the dominant kernel instance."""
+    if kname.startswith("k_conv3"):
+        return PEAK_X3, ("split-fp32 kernel: dense bf16 MFMA peak 2516.6 / 6 bf16 products per f32 MAC "
+                         "(f32 MFMA peak 157.3)")
+    if "<f32" in kname:
+        return PEAK["fp32"], "dense f32 MFMA peak (v_mfma_f32_16x16x4_f32)"
+    return PEAK["bf16"], "dense bf16 MFMA peak"
 FWD_GFLOP_PER_CROP = 109.136  # SURVEY.md §8(d): 2 x 54,568,026,112 MAC per 256x256 crop (R34)
 R50_GFLOP_PER_CROP = 747.68  # SURVEY.md §8(d): ResNet50_OS8 + ASPP_50 forward per crop
 
@@ -466,7 +479,7 @@ def conv_roofline(net, x, steps, precision, ms_per_step, layer_report=None, rank
     every conv launch of `steps` eager forwards bracketed by HIP events on the stream it runs on
     (torch's current stream, where libzp enqueues); achieved = sum of algorithmic FLOPs
     (2 * M * taps * Cin * Cout per launch) / sum of launch durations."""
-    eng = net.net._engine
+    eng = net.net.eval_engine()
     eng.timing = []
     with torch.no_grad():
         for _ in range(steps):
@@ -499,8 +512,11 @@ def conv_roofline(net, x, steps, precision, ms_per_step, layer_report=None, rank
     B = x.shape[0]
     all_fl = sum(v[0] for v in per.values())
     all_t = sum(v[1] for v in per.values())
-    return {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 2), "peak": PEAK[precision],
-            "unit": "TFLOP/s", "frac": round(achieved / PEAK[precision], 4), "traffic": traffic,
+    peak, basis = peak_of(kname, precision)
+    return {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 2), "peak": round(peak, 2),
+            "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "peak_basis": basis,
+            "frac_of_f32_mfma_peak": round(achieved / PEAK["fp32"], 4) if precision == "fp32" else None,
+            "traffic": traffic,
             "traffic_source": traffic_src, "algorithmic_bytes_per_launch": round(algo_per_launch),
             "traffic_over_algorithmic": None if traffic is None else round(traffic / algo_per_launch, 3),
             "launches_per_step": nl // steps, "avg_launch_us": round(tsec / nl * 1e6, 2),

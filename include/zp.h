@@ -50,11 +50,21 @@ extern "C" {
 #define ZP_F32 0
 #define ZP_BF16 1
 #define ZP_F16 2 /* IEEE fp16 storage + v_mfma_f32_16x16x32_f16; inference (forward) kernels only */
+/* fp32 in split form (eval-mode inference): a tensor is THREE contiguous bf16 planes [3][...], the
+ * pointer names plane 0, plane p starts p plane-sizes later (plane size = the tensor's element
+ * count: N*H*W*ld for an activation, rows_pad*k_pad for packed weights, N*C for a pooled vector).
+ * v = hi + mid + lo exactly (hi = bf16(v), mid = bf16(v - hi), lo = bf16(v - hi - mid)).  zp_conv2d
+ * forms every product a*b from the six terms of magnitude >= 2^-16 |a b| (hi*hi, hi*mid, mid*hi,
+ * hi*lo, mid*mid, lo*hi) on bf16 MFMAs with f32 accumulation: the dropped terms are below
+ * 2^-23 |a b| (f32's own product rounding is 2^-24), i.e. f32-accurate convolutions at 6/16 of the
+ * f32-MFMA cost.  Forward (eval) kernels only. */
+#define ZP_F32X3 3
 
 /* zp_conv_args.out_mode */
 #define ZP_OUT_NHWC 0       /* y[n, oy, ox, cy0 + c] (ldy elements per pixel), dtype of the call */
 #define ZP_OUT_HEAD_NCHW 1  /* c == 0 -> y (f32 [N,1,OH,OW]); c >= 1 -> y2 (f32 [N,Cout-1,OH,OW]) */
 #define ZP_OUT_NHWC_F32 2   /* y f32 NHWC regardless of dtype (raw conv output for train-mode BN) */
+#define ZP_OUT_NHWC_X3 3    /* y = plane 0 of a ZP_F32X3 NHWC tensor (an f32 call writing split output) */
 
 #define ZP_MAX_TAPS 64
 #define ZP_MAX_SUB 4
@@ -79,7 +89,8 @@ typedef struct zp_conv_sub {
 } zp_conv_sub;
 
 typedef struct zp_conv_args {
-  int dtype;            /* ZP_F32 (exact-f32 MFMA path), ZP_BF16 or ZP_F16 (16-bit MFMA, fp32 accumulate) */
+  int dtype;            /* ZP_F32 (exact-f32 MFMA path), ZP_BF16 or ZP_F16 (16-bit MFMA, fp32 accumulate),
+                           ZP_F32X3 (split fp32: x / w / res in 3 planes, Cin a multiple of 32) */
   const void* x;        /* input NHWC */
   int ldx, cx0, IH, IW, Cin;   /* Cin: multiple of 64 (bf16) / 32 (f32), or 8 (small-Cin path) */
   int N, GH, GW, sy, sx;       /* GEMM grid (pixels) and input stride */
@@ -110,7 +121,7 @@ int zp_conv2d_stat_parts(const zp_conv_args* a);
 /* launch configuration zp_conv2d picks: cout tile, pixel tile, LDS ring depth, kernel variant
  * (0 = k_conv, 1 = k_conv_strip: 3x3 stride-1 convs with activation-strip reuse, 2 = k_conv_strip2:
  * the same with the lean main loop, 3 = k_conv_quad: the four phases of a stride-2 transposed
- * structure in one tile) */
+ * structure in one tile, 4 = k_conv3: the split-fp32 (ZP_F32X3) kernel) */
 int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* stages, int* variant);
 /* runtime tuning knobs (tests / sweeps): key 0 = minimum workgroup count for the 256-channel
  * tile (default 1024); key 1 = conv schedule flags (-1 = ZP_CONV_FLAGS or the default); key 2 =

@@ -59,8 +59,10 @@ def setup(golden):
 
 
 def _nchw(act, b):
-    """crop b of an NHWC channel slice -> f32 NCHW [1, C, H, W] on the host."""
-    return act.buf[b:b + 1, :, :, act.c0:act.c0 + act.C].permute(0, 3, 1, 2).float().cpu()
+    """crop b of an NHWC channel slice -> f32 NCHW [1, C, H, W] on the host (the split-fp32 engine's
+    three planes joined exactly)."""
+    from zebrapose_amd.engine import joined
+    return joined(act.buf)[b:b + 1, :, :, act.c0:act.c0 + act.C].permute(0, 3, 1, 2).cpu()
 
 
 def _ulp_bf16(v):
@@ -134,7 +136,7 @@ def _label(rec, i):
 
 
 def run_traced(net, x):
-    eng = net.net._engine
+    eng = net.net.eval_engine()
     eng.trace = []
     try:
         with torch.no_grad():
@@ -222,12 +224,16 @@ def test_bf16_bench_geometry_end_to_end(setup):
         np.testing.assert_array_equal(res[b][1], p3d)
 
 
-def test_fp32_bench_geometry(setup):
-    """fp32 mode at bs=32: logits of crops 0, 13, 31 within the north-star 1e-3 of the fp32 oracle,
-    mask / code bits identical outside the band; every op replayed teacher-forced to 1e-5 rel."""
+@pytest.mark.parametrize("split", [True, False], ids=["split_f32", "f32_mfma"])
+def test_fp32_bench_geometry(setup, split):
+    """fp32 mode at bs=32 -- the benched headline: the split-fp32 eval engine (ZP_F32X3, the
+    default), and the exact-f32-MFMA engine: logits of crops 0, 13, 31 within the north-star 1e-3 of
+    the fp32 oracle, mask / code bits identical outside the band; every op replayed teacher-forced
+    to 1e-5 rel from the device's own stored (joined) inputs."""
     from oracle import ref_cpu
     net, sd, x = setup
     net.set_precision("fp32")
+    net.net.f32_split = split
     net.cuda().eval()
     m, c, trace = run_traced(net, x.cuda())
     xs = x[list(SAMPLE)]
@@ -246,16 +252,19 @@ def test_fp32_bench_geometry(setup):
         exp, got = replay(rec, b, torch.float32)
         scale = max(float(exp.abs().max()), 1e-6)
         assert float((got - exp).abs().max()) <= 1e-5 * scale, (_label(rec, i), float((got - exp).abs().max()), scale)
+    net.net.f32_split = True
     net.set_precision("bf16")
 
 
-def test_fp32_matches_reference_fixture_256(golden):
+@pytest.mark.parametrize("split", [True, False], ids=["split_f32", "f32_mfma"])
+def test_fp32_matches_reference_fixture_256(golden, split):
     """The reference's own 256x256 forward (B=2, BN calibrated at 256x256 -- r34_fwd256.npz) through
-    the fp32 HIP path within the north-star 1e-3."""
+    the fp32 HIP path (split-fp32 eval engine and exact-f32 MFMA) within the north-star 1e-3."""
     from oracle import ref_cpu
     from zebrapose_amd.model.BinaryCodeNet import BinaryCodeNet_Deeplab
     f = golden("r34_fwd256.npz")
     net = BinaryCodeNet_Deeplab(34, 16, 2, concat=True, output_kernel_size=1, precision="fp32")
+    net.net.f32_split = split
     net.load_state_dict(ref_cpu.synthetic_state(34, 16, 0, dict(golden("r34_bn_buffers256.npz"))))
     net = net.cuda().eval()
     with torch.no_grad():

@@ -39,14 +39,18 @@ def _bits_check(got, ref, band):
 
 # (fixture, keys, atol): the 64x64 fixture has logits up to 5.1 -> atol 1e-3 (observed 1.2e-4).
 # The 256x256 fixture (BN calibrated at 256x256) is checked in test_gpu_bench_geometry.py.
+@pytest.mark.parametrize("split", [True, False], ids=["split_f32", "f32_mfma"])
 @pytest.mark.parametrize("fixture,xkey,mkey,ckey,atol",
                          [("r34_fwd64.npz", "fwd64_x", "fwd64_mask", "fwd64_code", 1e-3)])
-def test_forward_fp32_matches_reference(net_and_state, golden, fixture, xkey, mkey, ckey, atol):
+def test_forward_fp32_matches_reference(net_and_state, golden, fixture, xkey, mkey, ckey, atol, split):
+    """fp32 eval forward: the split-fp32 engine (the default) and the exact-f32-MFMA engine."""
     net, _ = net_and_state
     net.set_precision("fp32")
+    net.net.f32_split = split
     f = golden(fixture)
     with torch.no_grad():
         m, c = net(torch.from_numpy(f[xkey]).cuda())
+    net.net.f32_split = True
     m, c = m.cpu().numpy(), c.cpu().numpy()
     for got, ref in ((m, f[mkey]), (c, f[ckey])):
         np.testing.assert_allclose(got, ref, atol=atol, rtol=1e-4)
@@ -55,15 +59,18 @@ def test_forward_fp32_matches_reference(net_and_state, golden, fixture, xkey, mk
         assert amb <= 0.01 * ref.size  # the ambiguous band itself (reported, tiny)
 
 
-def test_r50_forward_fp32_matches_reference(golden):
+@pytest.mark.parametrize("split", [True, False], ids=["split_f32", "f32_mfma"])
+def test_r50_forward_fp32_matches_reference(golden, split):
     """ResNet50_OS8 + ASPP_50 (340M parameters; Bottleneck stem/layer1/layer2, 1024/2048-channel
-    BasicBlock layer4/5, 2048-channel ASPP, 512-channel up2 input) through the HIP path, fp32 mode,
-    against the reference's own 64x64 forward (oracle/capture_fixtures.py capture_network(50))."""
+    BasicBlock layer4/5, 2048-channel ASPP, 512-channel up2 input) through the HIP path, fp32 mode
+    (split-fp32 eval engine and exact-f32 MFMA), against the reference's own 64x64 forward
+    (oracle/capture_fixtures.py capture_network(50))."""
     from oracle import ref_cpu
     from zebrapose_amd.model.BinaryCodeNet import BinaryCodeNet_Deeplab
     f = golden("r50_fwd64.npz")
     sd = ref_cpu.synthetic_state(50, 16, 0, dict(golden("r50_bn_buffers.npz")))
     net = BinaryCodeNet_Deeplab(50, 16, 2, concat=True, output_kernel_size=1, precision="fp32")
+    net.net.f32_split = split
     net.load_state_dict(sd)
     net = net.cuda().eval()
     with torch.no_grad():

@@ -1,0 +1,212 @@
+"""The split-fp32 engine (include/zp.h ZP_F32X3; k_conv3): fp32 values as three bf16 planes
+(hi + mid + lo, exact) and every conv product formed from its six leading terms on bf16 MFMAs.
+
+  * the split is exact: packed weights joined back equal the f32 checkpoint bit for bit;
+  * every conv geometry of the network (3x3 / dilated / strided, 1x1, the four ConvTranspose
+    phases, the merged-ASPP shapes, the NCHW head) in eval mode (BN fold, bias, residual, ReLU):
+    the split result's error against a float64 CPU reference of the same op is no larger than the
+    exact-f32-MFMA kernel's own error (2x + a 2^-24-scale floor) -- i.e. f32-accurate;
+  * the pooling / broadcast kernels on split tensors match their f32 definitions exactly.
+Network-level parity (the reference fixtures at 64x64 and 256x256, bs=32 teacher-forced) is in
+test_gpu_parity.py / test_gpu_bench_geometry.py, parametrised over both fp32 engines."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+GEOMS = [
+    # kind, cin, cout, k, s, p, d, bias, H
+    ("conv", 64, 64, 3, 1, 1, 1, False, 32),
+    ("conv", 64, 128, 3, 2, 1, 1, False, 32),
+    ("conv", 64, 128, 1, 2, 0, 1, False, 32),
+    ("conv", 128, 256, 3, 1, 2, 2, False, 16),
+    ("conv", 256, 256, 3, 1, 4, 4, False, 16),
+    ("conv", 512, 256, 3, 1, 12, 12, True, 32),
+    ("conv", 512, 256, 3, 1, 18, 18, True, 32),
+    ("conv", 1280, 256, 1, 1, 0, 1, True, 8),
+    ("conv", 320, 256, 3, 1, 1, 1, False, 24),
+    ("convT", 256, 256, 3, 2, 1, 1, False, 16),
+    ("convT", 320, 256, 3, 2, 1, 1, False, 8),
+    ("conv", 96, 48, 3, 1, 1, 1, False, 20),   # 64-channel tile, ragged Cout / pixel count
+]
+
+
+def _ref64(kind, conv, bn, x, res, relu, s, p, d):
+    w = conv.weight.detach().double().cpu()
+    b = None if conv.bias is None else conv.bias.detach().double().cpu()
+    xx = x.double()
+    y = F.conv2d(xx, w, b, s, p, d) if kind == "conv" else F.conv_transpose2d(xx, w, None, 2, 1, 1)
+    if bn is not None:
+        g, be, rm, rv = (t.detach().double().cpu() for t in (bn.weight, bn.bias, bn.running_mean, bn.running_var))
+        y = (y - rm.view(1, -1, 1, 1)) / torch.sqrt(rv.view(1, -1, 1, 1) + 1e-5) * g.view(1, -1, 1, 1) + be.view(1, -1, 1, 1)
+    if res is not None:
+        y = y + res.double()
+    return F.relu(y) if relu else y
+
+
+def _split_act(t, dev):
+    """f32 NHWC host tensor -> plane-0 view of its exact 3-plane bf16 split on the device."""
+    h = t.to(torch.bfloat16)
+    r = t - h.float()
+    m = r.to(torch.bfloat16)
+    lo = (r - m.float()).to(torch.bfloat16)
+    planes = torch.stack([h, m, lo]).to(dev)
+    assert torch.equal((planes[0].float() + planes[1].float()) + planes[2].float(), t.to(dev))
+    return planes[0]
+
+
+def test_split_weight_pack_is_exact(gpu):
+    from zebrapose_amd import _lib as L
+    from zebrapose_amd.engine import _i32arr
+    g = torch.Generator().manual_seed(3)
+    w = torch.randn(96, 40, 3, 3, generator=g) * torch.exp(torch.randn(96, 40, 3, 3, generator=g) * 4)
+    w[0, 0] = 0.0
+    w[1, 1] = -1e-30
+    w = w.to(gpu)
+    rows, kp = 128, 9 * 64
+    out = torch.empty((3, rows, kp), dtype=torch.bfloat16, device=gpu)
+    ky = [t // 3 for t in range(9)]
+    kx = [t % 3 for t in range(9)]
+    L.call("zp_pack_weight", w.data_ptr(), 96, 40, 3, 3, 0, 9, _i32arr(ky), _i32arr(kx), 64, L.ZP_F32X3,
+           out.data_ptr(), rows, kp, L.stream_ptr())
+    ref = torch.empty((rows, kp), dtype=torch.float32, device=gpu)
+    L.call("zp_pack_weight", w.data_ptr(), 96, 40, 3, 3, 0, 9, _i32arr(ky), _i32arr(kx), 64, L.ZP_F32,
+           ref.data_ptr(), rows, kp, L.stream_ptr())
+    joined = (out[0].float() + out[1].float()) + out[2].float()
+    torch.cuda.synchronize()
+    assert torch.equal(joined, ref)
+    # each plane is the round-to-nearest bf16 of what the planes above it leave
+    assert torch.equal(out[0], ref.to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("geom", GEOMS, ids=[f"{g[0]}{g[1]}-{g[2]}k{g[3]}s{g[4]}d{g[6]}h{g[8]}" for g in GEOMS])
+def test_split_conv_is_f32_accurate(gpu, geom):
+    from zebrapose_amd import _lib as L
+    from zebrapose_amd.engine import Engine, Unit, Act, joined
+    from zebrapose_amd.model import layers as LY
+    kind, cin, cout, k, s, p, d, bias, H = geom
+    torch.manual_seed(0)
+    B = 2
+    if kind == "conv":
+        conv = LY.Conv2d(cin, cout, k, s, p, d, bias=bias)
+    else:
+        conv = LY.ConvTranspose2d(cin, cout, k, s, p, output_padding=1, bias=False)
+    bn = LY.BatchNorm2d(cout)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.normal_(0, 0.1)
+        bn.running_mean.normal_(0, 0.1)
+        bn.running_var.uniform_(0.5, 1.5)
+    conv, bn = conv.to(gpu).eval(), bn.to(gpu).eval()
+    unit = Unit(conv, bn, relu=True)
+    OH, OW = unit.out_hw(H, H)
+    x = torch.randn(B, cin, H, H)
+    use_res = kind == "conv" and s == 1
+    res = torch.randn(B, cout, OH, OW) if use_res else None
+    ref = _ref64(kind, conv, bn, x, res, True, s, p, d)
+    xh = x.permute(0, 2, 3, 1).contiguous()
+    rh = None if res is None else res.permute(0, 2, 3, 1).contiguous()
+    out = {}
+    for mode in ("x3", "f32"):
+        if mode == "x3":
+            eng = Engine(torch.nn.Module(), torch.float32, x3=True)
+            xa = Act(_split_act(xh, gpu))
+            ra = None if rh is None else Act(_split_act(rh, gpu))
+            oa = Act(eng._empty((B, OH, OW, cout), gpu))
+        else:
+            eng = Engine(torch.nn.Module(), torch.float32)
+            xa = Act(xh.to(gpu))
+            ra = None if rh is None else Act(rh.to(gpu))
+            oa = Act(torch.empty(B, OH, OW, cout, device=gpu))
+        eng.unit_fwd(unit, xa, oa, None, res=ra)
+        torch.cuda.synchronize()
+        out[mode] = joined(oa.buf).permute(0, 3, 1, 2).double().cpu()
+    scale = ref.abs().max().item()
+    e3 = (out["x3"] - ref).abs().max().item()
+    e32 = (out["f32"] - ref).abs().max().item()
+    r3 = (out["x3"] - ref).pow(2).mean().sqrt().item()
+    r32 = (out["f32"] - ref).pow(2).mean().sqrt().item()
+    print(f"{geom}: max|d| split {e3:.3g} f32-MFMA {e32:.3g}; rms split {r3:.3g} f32-MFMA {r32:.3g} (scale {scale:.3g})")
+    assert e3 <= 2.0 * e32 + 2.0 ** -24 * scale, (e3, e32, scale)
+
+
+def test_split_head_nchw(gpu):
+    """The head conv (1x1, 320 -> 17, bias, no BN) on the 32-channel tile writing f32 NCHW mask / code."""
+    from zebrapose_amd.engine import Engine, Unit, Act
+    from zebrapose_amd.model import layers as LY
+    torch.manual_seed(1)
+    B, H = 2, 24
+    conv = LY.Conv2d(320, 17, 1, 1, 0, 1, bias=True).to(gpu).eval()
+    unit = Unit(conv, None, relu=False)
+    x = torch.randn(B, 320, H, H)
+    ref = _ref64("conv", conv, None, x, None, False, 1, 0, 1)
+    err = {}
+    for mode in ("x3", "f32"):
+        eng = Engine(torch.nn.Module(), torch.float32, x3=mode == "x3")
+        xh = x.permute(0, 2, 3, 1).contiguous()
+        xa = Act(_split_act(xh, gpu) if mode == "x3" else xh.to(gpu))
+        mask = torch.empty(B, 1, H, H, device=gpu)
+        code = torch.empty(B, 16, H, H, device=gpu)
+        eng.head_fwd(unit, xa, mask, code, None)
+        torch.cuda.synchronize()
+        err[mode] = (torch.cat([mask, code], 1).double().cpu() - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    print(f"head: max|d| split {err['x3']:.3g} f32-MFMA {err['f32']:.3g} (scale {scale:.3g})")
+    assert err["x3"] <= 2.0 * err["f32"] + 2.0 ** -24 * scale, err
+
+
+def test_split_pools_and_broadcast(gpu):
+    from zebrapose_amd import _lib as L
+    from zebrapose_amd.engine import joined
+    torch.manual_seed(2)
+    B, H, C = 2, 17, 64
+    x = torch.randn(B, H, H, 80)
+    xa = _split_act(x, gpu)
+    st = L.stream_ptr()
+    OH = (H - 1) // 2 + 1
+    y = torch.empty((3, B, OH, OH, C), dtype=torch.bfloat16, device=gpu)[0]
+    L.call("zp_maxpool3s2", xa.data_ptr(), B, H, H, 80, 16, C, L.ZP_F32X3, y.data_ptr(), OH, OH, C, 0, st)
+    ref = F.max_pool2d(x[..., 16:16 + C].permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1)
+    torch.cuda.synchronize()
+    assert torch.equal(joined(y).cpu(), ref)
+    pool = torch.empty((3, B, 1, 1, 80), dtype=torch.bfloat16, device=gpu)[0]
+    L.call("zp_global_avgpool", xa.data_ptr(), B, H, H, 80, 0, 80, L.ZP_F32X3, pool.data_ptr(), st)
+    pref = x.double().mean((1, 2)).float().view(B, 1, 1, 80)
+    torch.cuda.synchronize()
+    assert torch.equal(joined(pool).cpu(), pref)
+    out = torch.zeros((3, B, 5, 5, 96), dtype=torch.bfloat16, device=gpu)[0]
+    L.call("zp_broadcast_hw", pool.data_ptr(), B, 80, L.ZP_F32X3, out.data_ptr(), 5, 5, 96, 8, st)
+    torch.cuda.synchronize()
+    assert torch.equal(joined(out)[..., 8:88].cpu(), pref.expand(B, 5, 5, 80))
+
+
+@pytest.mark.parametrize("cin", [256, 1280])
+def test_split_accumulation_numerics(gpu, cin):
+    """Diagnostic: with bf16-representable inputs and weights (mid = lo = 0) the split kernel's
+    result is the plain bf16-MFMA accumulation of the exact products, the f32 kernel's the f32-MFMA
+    (fmaf chain) accumulation of the same products: their errors against float64 compare the two
+    MFMA accumulators directly (printed; the split bound is the f32 one x 2)."""
+    from zebrapose_amd.engine import Engine, Unit, Act, joined
+    from zebrapose_amd.model import layers as LY
+    torch.manual_seed(4)
+    B, H, cout = 2, 16, 256
+    conv = LY.Conv2d(cin, cout, 1, 1, 0, 1, bias=False)
+    with torch.no_grad():
+        conv.weight.copy_(conv.weight.to(torch.bfloat16).float())
+    conv = conv.to(gpu).eval()
+    unit = Unit(conv, None, relu=False)
+    x = torch.randn(B, cin, H, H).to(torch.bfloat16).float()
+    ref = F.conv2d(x.double(), conv.weight.detach().double().cpu())
+    xh = x.permute(0, 2, 3, 1).contiguous()
+    res = {}
+    for mode in ("x3", "f32"):
+        eng = Engine(torch.nn.Module(), torch.float32, x3=mode == "x3")
+        xa = Act(_split_act(xh, gpu) if mode == "x3" else xh.to(gpu))
+        oa = Act(eng._empty((B, H, H, cout), gpu) if mode == "x3" else torch.empty(B, H, H, cout, device=gpu))
+        eng.unit_fwd(unit, xa, oa, None)
+        torch.cuda.synchronize()
+        d = joined(oa.buf).permute(0, 3, 1, 2).double().cpu() - ref
+        res[mode] = (d.abs().max().item(), d.pow(2).mean().sqrt().item(), d.mean().item())
+    print(f"K={cin}: bf16-MFMA acc max/rms/mean {res['x3']}, f32-MFMA {res['f32']} (scale {ref.abs().max().item():.3g})")
+    assert res["x3"][0] <= 2.0 * res["f32"][0] + 1e-30

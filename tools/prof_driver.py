@@ -28,7 +28,11 @@ def main():
     ap.add_argument("--precision", default="bf16")
     ap.add_argument("--layer-report", default=None)
     ap.add_argument("--mode", default="train", choices=["train", "infer"])
+    ap.add_argument("--stage-log", default=None, help="infer: write the last step's conv launches (stage, kernel, "
+                                                       "flops, algorithmic bytes) in launch order here")
     a = ap.parse_args()
+    from bench import lib_sha16
+    print(f"lib_sha16 {lib_sha16()}", flush=True)
     from zebrapose_amd.model.BinaryCodeNet import BinaryCodeNet_Deeplab
     from zebrapose_amd.train import TrainStep
     dev = torch.device("cuda", 0)
@@ -50,11 +54,20 @@ def main():
         for _ in range(a.warmup):
             step()
         torch.cuda.synchronize()
+        eng = net.net.eval_engine()
         t0 = time.perf_counter()
-        for _ in range(a.steps):
+        for i in range(a.steps):
+            if a.stage_log and i == a.steps - 1:
+                eng.stage_log = []  # host-side bookkeeping only: the dispatch sequence is unchanged
             step()
         torch.cuda.synchronize()
         print(f"infer ms/step {(time.perf_counter() - t0) / a.steps * 1e3:.3f}")
+        if a.stage_log:
+            with open(a.stage_log, "w") as f:
+                json.dump({"precision": a.precision, "batch": a.batch, "lib_sha16": lib_sha16(),
+                           "launches": [{"stage": st, "kernel": k, "flops": fl, "bytes": nb, "geo": geo}
+                                        for st, k, fl, nb, geo in eng.stage_log]}, f, indent=0)
+            eng.stage_log = None
         return
     calibrate_bn(net, x)
     net.train()

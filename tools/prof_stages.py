@@ -1,0 +1,232 @@
+#!/usr/bin/env python3
+"""Per-stage MFMA utilisation and HBM traffic of the R34 inference step from a tools/prof_r03.sh run
+(gpurun_out/prof_<tag>/) -> profiles/<tag>_stages_<precision>.json / .md, plus the per-kernel PMC
+traffic file bench.py reads (profiles/<tag>_pmc_traffic.json, keyed to the libzp.so build hash) and
+the kernel-trace stats (profiles/<tag>_infer_kernel_stats.csv, <tag>_train1s_kernel_stats.csv).
+
+Attribution: every pass runs the same tools/prof_driver.py --mode infer program, whose dispatch
+sequence is identical from step 2 on.  The last step is the window from its k_nchw_to_nhwc (the
+input conversion, first kernel of a step) to the end of the run (the decode kernels end it).  Its
+conv dispatches are matched one by one, in order, to the driver's stage log (engine.stage_log:
+stage, kernel label, FLOPs); the label of every pair is checked.  Non-conv kernels are attributed
+by name (nchw_to_nhwc -> stem, maxpool -> layer1, global avgpool / broadcast -> aspp, decode).
+
+Per stage:
+  time      sum of the dispatch durations (kernel-trace pass, End - Start timestamps)
+  TFLOP/s   algorithmic FLOPs (2 M taps Cin Cout per conv) / time; frac of the dtype's
+            dense MFMA peak (bf16 2516.6, f32 157.3 TFLOP/s)
+  MFMA busy SQ_VALU_MFMA_BUSY_CYCLES (per-SIMD busy cycles, summed) / (GRBM_GUI_ACTIVE / 8 x 1024
+            SIMDs): the fraction of the stage's active cycles the matrix pipes were busy
+            (rocprofv3's MfmaUtil formula; GRBM_GUI_ACTIVE is reported summed over the 8 XCDs;
+            it reads high on dispatches shorter than ~0.3 ms, so short stages read low)
+  HBM       reads 2 x FETCH_SIZE x 1024 B + writes WRITE_SIZE x 1024 B (MI355X_MICROARCH.md §HBM:
+            FETCH_SIZE halves wide coalesced reads on gfx950), GB/s over the stage time
+"""
+import csv
+import glob
+import json
+import os
+import re
+import shutil
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+from prof_summary import bench_label  # noqa: E402
+
+PEAK = {"bf16": 2516.6, "fp32": 157.3}
+STAGES = ["stem", "layer1", "layer2", "layer4", "layer5", "aspp", "up1", "up2", "head", "decode"]
+
+
+def one(pattern):
+    f = sorted(glob.glob(pattern, recursive=True))
+    return f[0] if f else None
+
+
+def nonconv_stage(name):
+    if "nchw_to_nhwc" in name:
+        return "stem"
+    if "maxpool" in name:
+        return "layer1"
+    if "avgpool" in name or "broadcast" in name or "hw_reduce" in name:
+        return "aspp"
+    if "decode" in name or "threshold" in name or "scan" in name:
+        return "decode"
+    return None
+
+
+def is_conv(name):
+    return bench_label(name) is not None
+
+
+def last_step(rows):
+    """rows: dispatches in order [(name, ...)] -> the slice of the last step."""
+    starts = [i for i, r in enumerate(rows) if "nchw_to_nhwc" in r[0]]
+    if not starts:
+        raise SystemExit("no k_nchw_to_nhwc dispatch found")
+    return rows[starts[-1]:]
+
+
+def read_trace(path):
+    out = []
+    with open(path) as fh:
+        for r in csv.DictReader(fh):
+            if "zp::" not in r["Kernel_Name"]:
+                continue
+            out.append((r["Kernel_Name"], int(r["Dispatch_Id"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
+    out.sort(key=lambda t: t[1])
+    return out
+
+
+def read_pmc(path, names):
+    per = defaultdict(dict)
+    kn = {}
+    with open(path) as fh:
+        for r in csv.DictReader(fh):
+            if "zp::" not in r["Kernel_Name"] or r["Counter_Name"] not in names:
+                continue
+            d = int(r["Dispatch_Id"])
+            per[d][r["Counter_Name"]] = per[d].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+            kn[d] = r["Kernel_Name"]
+    return [(kn[d], d, per[d]) for d in sorted(per)]
+
+
+def attribute(rows, log):
+    """rows of the last step -> [(stage, row)], checking conv labels against the stage log."""
+    out, ci = [], 0
+    for r in rows:
+        if is_conv(r[0]):
+            if ci >= len(log):
+                raise SystemExit("more conv dispatches than stage-log entries")
+            ent = log[ci]
+            lab = bench_label(r[0])
+            if lab != ent["kernel"]:
+                raise SystemExit(f"conv dispatch {ci}: rocprof {lab} vs stage log {ent['kernel']}")
+            out.append((ent["stage"], r, ent))
+            ci += 1
+        else:
+            out.append((nonconv_stage(r[0]) or "other", r, None))
+    if ci != len(log):
+        raise SystemExit(f"{ci} conv dispatches vs {len(log)} stage-log entries")
+    return out
+
+
+def stage_table(src, prec):
+    log = json.load(open(os.path.join(src, f"stage_log_{prec}.json")))
+    tr = last_step(read_trace(one(os.path.join(src, f"trace_{prec}", "**", "*kernel_trace.csv"))))
+    fe = last_step(read_pmc(one(os.path.join(src, f"fetch_{prec}", "**", "*counter_collection.csv")),
+                            {"FETCH_SIZE"}))
+    wr = last_step(read_pmc(one(os.path.join(src, f"write_{prec}", "**", "*counter_collection.csv")),
+                            {"WRITE_SIZE"}))
+    mf = last_step(read_pmc(one(os.path.join(src, f"mfma_{prec}", "**", "*counter_collection.csv")),
+                            {"SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE", "SQ_INSTS_VALU_MFMA_MOPS_BF16",
+                             "SQ_INSTS_VALU_MFMA_MOPS_F32"}))
+    if not (len(tr) == len(fe) == len(wr) == len(mf)):
+        raise SystemExit(f"{prec}: step windows differ: trace {len(tr)} fetch {len(fe)} write {len(wr)} mfma {len(mf)}")
+    for a, b, c, d in zip(tr, fe, wr, mf):
+        if not (a[0] == b[0] == c[0] == d[0]):
+            raise SystemExit(f"{prec}: dispatch sequences differ between passes: {a[0][:60]} / {b[0][:60]}")
+    at = attribute(tr, log["launches"])
+    st = {s: defaultdict(float) for s in STAGES + ["other"]}
+    per_kernel = defaultdict(lambda: defaultdict(float))
+    for (stage, t, ent), f, w, m in zip(at, fe, wr, mf):
+        d = st[stage]
+        d["dispatches"] += 1
+        d["ns"] += t[2]
+        d["flops"] += ent["flops"] if ent else 0.0
+        d["algo_bytes"] += ent["bytes"] if ent else 0.0
+        d["read"] += 2.0 * 1024.0 * f[2].get("FETCH_SIZE", 0.0)
+        d["write"] += 1024.0 * w[2].get("WRITE_SIZE", 0.0)
+        d["mfma_busy"] += m[2].get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0)
+        d["grbm"] += m[2].get("GRBM_GUI_ACTIVE", 0.0)
+        d["mops_bf16"] += m[2].get("SQ_INSTS_VALU_MFMA_MOPS_BF16", 0.0)
+        d["mops_f32"] += m[2].get("SQ_INSTS_VALU_MFMA_MOPS_F32", 0.0)
+        k = per_kernel[bench_label(t[0]) or t[0].split("(")[0]]
+        k["n"] += 1
+        k["ns"] += t[2]
+        k["read"] += 2.0 * 1024.0 * f[2].get("FETCH_SIZE", 0.0)
+        k["write"] += 1024.0 * w[2].get("WRITE_SIZE", 0.0)
+        k["flops"] += ent["flops"] if ent else 0.0
+        k["mfma_busy"] += m[2].get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0)
+        k["grbm"] += m[2].get("GRBM_GUI_ACTIVE", 0.0)
+    rows = []
+    tot = defaultdict(float)
+    for s in STAGES + ["other"]:
+        d = st[s]
+        if not d["dispatches"]:
+            continue
+        for k, v in d.items():
+            tot[k] += v
+        rows.append(summarise(s, d, prec))
+    rows.append(summarise("total", tot, prec))
+    kern = {k: {"launches": int(v["n"]), "us_per_launch": round(v["ns"] / v["n"] / 1e3, 2),
+                "hbm_bytes_per_launch": round((v["read"] + v["write"]) / v["n"]),
+                "read_bytes_per_launch": round(v["read"] / v["n"]), "write_bytes_per_launch": round(v["write"] / v["n"]),
+                "tflops": round(v["flops"] / v["ns"] / 1e3, 1) if v["flops"] else None,
+                "mfma_busy_pct": round(100.0 * v["mfma_busy"] / (v["grbm"] / 8.0 * 1024.0), 1) if v["grbm"] else None}
+            for k, v in per_kernel.items()}
+    return {"precision": prec, "batch": log["batch"], "lib_sha16": log["lib_sha16"], "stages": rows,
+            "kernels": kern}
+
+
+def summarise(name, d, prec):
+    t = d["ns"] * 1e-9
+    busy = 100.0 * d["mfma_busy"] / (d["grbm"] / 8.0 * 1024.0) if d["grbm"] else None
+    return {"stage": name, "dispatches": int(d["dispatches"]), "us": round(d["ns"] / 1e3, 1),
+            "gflop": round(d["flops"] / 1e9, 2),
+            "tflops": round(d["flops"] / t / 1e12, 1) if t and d["flops"] else None,
+            "frac_of_peak": round(d["flops"] / t / 1e12 / PEAK[prec], 3) if t and d["flops"] else None,
+            "mfma_busy_pct": None if busy is None else round(busy, 1),
+            "hbm_mb": round((d["read"] + d["write"]) / 1e6, 1),
+            "algo_mb": round(d["algo_bytes"] / 1e6, 1),
+            "hbm_gbps": round((d["read"] + d["write"]) / t / 1e9, 1) if t else None,
+            "mfma_mops_bf16": d["mops_bf16"], "mfma_mops_f32": d["mops_f32"]}
+
+
+def md(tab):
+    p = tab["precision"]
+    out = [f"### R34 inference bs={tab['batch']}, {p} (libzp {tab['lib_sha16']})", "",
+           "| stage | dispatches | us | GFLOP | TFLOP/s | frac of peak | MFMA busy % | HBM MB (algorithmic) | HBM GB/s |",
+           "|---|---|---|---|---|---|---|---|---|"]
+    for r in tab["stages"]:
+        out.append(f"| {r['stage']} | {r['dispatches']} | {r['us']} | {r['gflop']} | {r['tflops']} | {r['frac_of_peak']} "
+                   f"| {r['mfma_busy_pct']} | {r['hbm_mb']} ({r['algo_mb']}) | {r['hbm_gbps']} |")
+    return "\n".join(out) + "\n"
+
+
+def main(tag="r03", precs=("fp32", "bf16")):
+    src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
+    dst = os.path.join(ROOT, "profiles")
+    f = one(os.path.join(src, "stats", "**", "*kernel_stats.csv"))
+    if f:
+        shutil.copy(f, os.path.join(dst, f"{tag}_infer_kernel_stats.csv"))
+    f = one(os.path.join(src, "train_1s", "**", "*kernel_stats.csv"))
+    if f:
+        shutil.copy(f, os.path.join(dst, f"{tag}_train1s_kernel_stats.csv"))
+    traffic = {"source": f"tools/prof_r03.sh: rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate runs) over "
+                         f"tools/prof_driver.py --mode infer --steps 3 --warmup 2, last step of each run",
+               "correction": "bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024 (FETCH_SIZE halves wide coalesced "
+                             "reads on gfx950, MI355X_MICROARCH.md HBM section)",
+               "by_label": {}, "kernels": {}}
+    text = []
+    for p in precs:
+        tab = stage_table(src, p)
+        traffic["lib_sha16"] = tab["lib_sha16"]
+        for k, v in tab["kernels"].items():
+            traffic["kernels"][k] = v
+            if k.startswith("k_conv"):
+                traffic["by_label"][k] = v["hbm_bytes_per_launch"]
+        with open(os.path.join(dst, f"{tag}_stages_{p}.json"), "w") as fh:
+            json.dump(tab, fh, indent=1)
+        text.append(md(tab))
+        print(md(tab))
+    with open(os.path.join(dst, f"{tag}_pmc_traffic.json"), "w") as fh:
+        json.dump(traffic, fh, indent=1)
+    with open(os.path.join(dst, f"{tag}_stages.md"), "w") as fh:
+        fh.write("\n".join(text))
+
+
+if __name__ == "__main__":
+    a = sys.argv[1:]
+    main(a[0] if a else "r03", tuple(a[1:]) or ("fp32", "bf16"))

@@ -38,6 +38,22 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   return __builtin_bit_cast(bf16_t, b);
 }
 
+// ZP_F32X3 (split fp32, zp.h): v -> (hi, mid, lo) bf16 with v == hi + mid + lo exactly for finite
+// v (each round-to-nearest step leaves a remainder exactly representable in f32 with at most 16 /
+// 8 significant bits, so lo is exact); infinities / NaN keep mid = lo = 0.
+__device__ __forceinline__ void split3(float v, bf16_t& h, bf16_t& m, bf16_t& l) {
+  h = f2bf(v);
+  const float r1 = v - bf2f(h);
+  m = f2bf(r1);
+  l = f2bf(r1 - bf2f(m));
+  if (!__builtin_isfinite(v)) {
+    m = 0;
+    l = 0;
+  }
+}
+// (hi + mid) is exact, and the exact total is an f32, so the second add rounds to it
+__device__ __forceinline__ float join3(bf16_t h, bf16_t m, bf16_t l) { return (bf2f(h) + bf2f(m)) + bf2f(l); }
+
 template <typename T> struct Elem;
 template <> struct Elem<float> {
   static __device__ __forceinline__ float ld(const float* p) { return *p; }

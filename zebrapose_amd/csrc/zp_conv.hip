@@ -265,6 +265,22 @@ __device__ __forceinline__ void conv_epilogue(const zp_conv_args& A, const zp_co
         }
         continue;
       }
+      if constexpr (sizeof(T) == 4) {
+        if (A.out_mode == ZP_OUT_NHWC_X3) {  // f32 call writing a ZP_F32X3 tensor (the split-mode stem)
+          const long psy = (long)A.N * S.OH * S.OW * S.ldy;
+          bf16_t* Y = (bf16_t*)S.y + pix * S.ldy + S.cy0 + cf;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            if (cf + r >= A.Cout) continue;
+            bf16_t h, m, l;
+            split3(v[r], h, m, l);
+            Y[r] = h;
+            Y[r + psy] = m;
+            Y[r + 2 * psy] = l;
+          }
+          continue;
+        }
+      }
       if (A.out_mode == ZP_OUT_NHWC_F32 || sizeof(T) == 4) {
         float* Y = (float*)S.y + pix * S.ldy + S.cy0 + cf;
         if (cf + 3 < A.Cout) {
@@ -2261,6 +2277,278 @@ __global__ void k_wgrad_reduce(const zp_wgrad_args A, const float* __restrict__ 
   }
 }
 
+// ------------------------------------------------------------------------------------
+// k_conv3: forward convolution on ZP_F32X3 operands (split fp32, zp.h): activations, packed weights
+// and the residual are three bf16 planes (hi, mid, lo) whose sum is the f32 value exactly.  Every
+// product a * b is formed from its six terms of magnitude >= 2^-16 |a b|:
+//   hi*hi + hi*mid + mid*hi + hi*lo + mid*mid + lo*hi
+// on v_mfma_f32_16x16x32_bf16 (f32 accumulate); the dropped terms (mid*lo, lo*mid, lo*lo) are below
+// 2^-23 |a b|, the order of f32's own product rounding.  That is f32-accurate arithmetic at 6 bf16
+// MFMAs per 16x16x32 product block = 6/16 of the v_mfma_f32_16x16x4_f32 cost, and -- since the three
+// B planes are staged once and each fragment feeds 3 / 2 / 1 MFMAs -- half the LDS traffic per MFMA
+// of the bf16 kernels.
+// Tile: 2 NWP waves = 2 (cout) x NWP (pixel) computing TC = 32 WC output channels x TP = 64 NWP
+// pixels.  A K step is one tap x 32 input channels.  Staging: per plane, a 16-row x 32-element tile
+// (1 KB) is ONE buffer_load ... lds of 64 lanes, lane l fetching (row l & 15, 8 elements at k (l >>
+// 4) * 8): the LDS image is in MFMA fragment order, so every fragment read is a lane-linear
+// conflict-free ds_read_b128.  2-deep ring (TC 128 x TP 256: 72 KB per stage); the tap walk
+// (scalar), validity masks and out-of-image zeros (offset past the buffer end) follow k_conv.
+// Ping-pong (flags & 8, 8 waves): waves 4-7 run one barrier behind, so on each SIMD one wave's MFMAs
+// overlap its partner's LDS reads and DMA wait.  Epilogue: BN scale / shift (+ bias), split
+// residual, ReLU, then split NHWC stores (3 planes) or the f32 NCHW head split.
+// ------------------------------------------------------------------------------------
+template <int WC, int NWP>
+__global__ void __launch_bounds__(128 * NWP) k_conv3(const zp_conv_args A, const conv_taps TG, const int flags) {
+  constexpr int WP = 4;
+  constexpr int TC = 32 * WC, TP = 64 * NWP, NW = 2 * NWP;
+  constexpr int NTW = TC / 16, NT = (TC + TP) / 16;  // weight tiles / all tiles (16 rows) per plane
+  constexpr int UNITS = 3 * NT;                      // (plane, tile) DMA units per stage
+  constexpr int TPW = (NT + NW - 1) / NW;            // tiles per wave (some waves idle in the last)
+  __shared__ uint4 lds[2 * UNITS * 64];
+  static_assert(2 * UNITS * 1024 <= 160 * 1024, "LDS");
+  static_assert((2 * NT + WC + 3) * 1024 < 65536, "ds_read immediate range");
+  const zp_conv_sub& S = A.sub[blockIdx.z];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wid / NWP, wp = wid % NWP;
+  const int GHW = A.GH * A.GW;
+  const int M = A.N * GHW;
+  int bx = blockIdx.x, by = blockIdx.y;
+  if (flags & 2) {  // XCD-aware order (k_conv): the cout tiles of a pixel tile meet in one L2
+    const int total = gridDim.x * gridDim.y;
+    const int bid = blockIdx.x + gridDim.x * blockIdx.y;
+    const int lin = (total & 7) ? bid : (bid & 7) * (total >> 3) + (bid >> 3);
+    bx = lin / gridDim.y;
+    by = lin - bx * gridDim.y;
+  }
+  const int p0 = bx * TP, c0 = by * TC;
+  const int tb = blockIdx.z;
+  const int CB = A.Cin / 32;
+  const int ny = TG.ny[tb], nx = TG.nx[tb], dty = TG.dty[tb], dtx = TG.dtx[tb];
+  const int nK = S.ntaps * CB;
+  const int lr = lane & 15, lk = (lane >> 4) * 8;
+  // plane strides in bytes (scalar offsets of the DMA: the three planes of a tile share the lane's
+  // offset register)
+  const unsigned psx_b = (unsigned)((long)A.N * A.IH * A.IW * A.ldx * 2);
+  const unsigned psw_b = (unsigned)((long)A.w_rows * A.k_pad * 2);
+
+  // tiles of this wave: T = wid + NW k (all three planes each); wave-uniform kind, per-lane base
+  // offset (plane 0, bytes) and tap validity masks
+  unsigned ubase[TPW], uym[TPW], uxm[TPW];
+#pragma unroll
+  for (int k = 0; k < TPW; ++k) {
+    const int t = wid + NW * k;
+    ubase[k] = 0u;
+    uym[k] = uxm[k] = 0u;
+    if (t >= NT) continue;
+    if (t < NTW) {
+      ubase[k] = (unsigned)(((long)(c0 + t * 16 + lr) * A.k_pad + lk) * 2);
+    } else {
+      const int m = p0 + (t - NTW) * 16 + lr;
+      const bool ok = m < M;
+      const int mm = ok ? m : 0;
+      const int n = mm / GHW, rr = mm - n * GHW;
+      const int gy = rr / A.GW, gx = rr - gy * A.GW;
+      const int y0 = gy * A.sy, x0 = gx * A.sx;
+      ubase[k] = (unsigned)(((((long)n * A.IH + y0) * A.IW + x0) * A.ldx + A.cx0 + lk) * 2);
+      unsigned ym = 0, xm = 0;
+      for (int q = 0; q < ny; ++q) ym |= (unsigned)((unsigned)(y0 + TG.ty0[tb] + q * dty) < (unsigned)A.IH) << q;
+      for (int q = 0; q < nx; ++q) xm |= (unsigned)((unsigned)(x0 + TG.tx0[tb] + q * dtx) < (unsigned)A.IW) << q;
+      uym[k] = ok ? ym : 0u;
+      uxm[k] = xm;
+    }
+  }
+#if defined(__HIP_DEVICE_COMPILE__)
+  const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)A.x, (short)0, (int)TG.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)S.w, (short)0, (int)TG.w_bytes[tb], 0x00020000);
+#endif
+  // scalar tap walk of the next step to issue: (tap row, tap column, chunk) -> activation offset
+  int w_tyi = 0, w_txi = 0, w_cb = 0;
+  int act_off = ((TG.ty0[tb] * A.IW + TG.tx0[tb]) * A.ldx) * 2;
+  const int step_x = dtx * A.ldx * 2, step_y = dty * A.IW * A.ldx * 2;
+  auto issue = [&](int ks, int stage) {
+    unsigned voff[TPW];
+#pragma unroll
+    for (int k = 0; k < TPW; ++k) {
+      const bool w = wid + NW * k < NTW;
+      const bool ok = (uym[k] >> w_tyi) & (uxm[k] >> w_txi) & 1u;
+      voff[k] = w ? ubase[k] : (ok ? ubase[k] + (unsigned)act_off : 0x80000000u);
+    }
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+    for (int k = 0; k < TPW; ++k) {
+      const int t = wid + NW * k;
+      if (t >= NT) continue;
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) {
+        auto* d = (__attribute__((address_space(3))) void*)&lds[(stage * UNITS + pl * NT + t) * 64];
+        if (t < NTW) __builtin_amdgcn_raw_ptr_buffer_load_lds(wrsrc, d, 16, voff[k], pl * psw_b + ks * 64, 0, 0);
+        else __builtin_amdgcn_raw_ptr_buffer_load_lds(xrsrc, d, 16, voff[k], pl * psx_b, 0, 0);
+      }
+    }
+#endif
+    act_off += 64;
+    if (++w_cb == CB) {
+      w_cb = 0;
+      act_off += step_x - CB * 64;
+      if (++w_txi == nx) {
+        w_txi = 0;
+        act_off += step_y - nx * step_x;
+        ++w_tyi;
+      }
+    }
+  };
+
+  f32x4 acc[WC][WP];
+#pragma unroll
+  for (int i = 0; i < WC; ++i)
+#pragma unroll
+    for (int j = 0; j < WP; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const unsigned l0 = lds_addr(lds) + (unsigned)lane * 16u;
+  unsigned abase[2], bbase[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    abase[s] = l0 + (unsigned)(s * UNITS + wc * WC) * 1024u;
+    bbase[s] = l0 + (unsigned)(s * UNITS + NTW + wp * WP) * 1024u;
+  }
+  const bool pingpong = NW == 8 && (flags & 8);
+  auto step = [&](auto s_c, int ks) {
+    constexpr int s = decltype(s_c)::value;
+    const bool more = ks + 1 < nK;
+    if (more) issue(ks + 1, s ^ 1);
+    uint4 af[3][WC], bfr[3][WP];
+    static_for<3>([&](auto p_c) {
+      constexpr int p = decltype(p_c)::value;
+      static_for<WC>([&](auto i) { af[p][i] = ds_read16<(p * NT + i) * 1024>(abase[s]); });
+      static_for<WP>([&](auto j) { bfr[p][j] = ds_read16<(p * NT + j) * 1024>(bbase[s]); });
+    });
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (pingpong) {
+      vm_wait<0>();
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (flags & 4) __builtin_amdgcn_s_setprio(1);
+    // term order: the small terms first, hi*hi last
+    constexpr int TA[6] = {1, 0, 2, 1, 0, 0}, TB[6] = {1, 2, 0, 0, 1, 0};
+    static_for<6>([&](auto t_c) {
+      constexpr int t = decltype(t_c)::value;
+#pragma unroll
+      for (int i = 0; i < WC; ++i)
+#pragma unroll
+        for (int j = 0; j < WP; ++j) MfmaTraits<bf16_t>::mma(acc[i][j], af[TA[t]][i], bfr[TB[t]][j]);
+    });
+    __builtin_amdgcn_sched_barrier(0);
+    if (flags & 4) __builtin_amdgcn_s_setprio(0);
+    if (!pingpong) vm_wait<0>();
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  issue(0, 0);
+  vm_wait<0>();
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  if (pingpong && wid >= 4) __builtin_amdgcn_s_barrier();
+  for (int ks = 0; ks < nK; ks += 2) {
+    step(I0{}, ks);
+    if (ks + 1 >= nK) break;
+    step(I1{}, ks + 1);
+  }
+  if (pingpong && wid < 4) __builtin_amdgcn_s_barrier();
+
+  // ---------------- epilogue ----------------
+  int pn[WP], poy[WP], pox[WP];
+  bool pok[WP];
+#pragma unroll
+  for (int j = 0; j < WP; ++j) {
+    const int p = p0 + wp * 16 * WP + j * 16 + lr;
+    pok[j] = p < M;
+    const int pp = pok[j] ? p : 0;
+    const int n = pp / GHW, rr = pp - n * GHW;
+    const int gy = rr / A.GW, gx = rr - gy * A.GW;
+    pn[j] = n;
+    poy[j] = gy * S.oys + S.oyo;
+    pox[j] = gx * S.oxs + S.oxo;
+  }
+  const long psy = (long)A.N * S.OH * S.OW * S.ldy;
+  const long psr = (long)A.N * S.OH * S.OW * A.ldr;
+  const int cbase = c0 + wc * 16 * WC + (lane >> 4) * 4;
+#pragma unroll
+  for (int i = 0; i < WC; ++i) {
+    const int cf = cbase + i * 16;
+    if (cf >= A.Cout) continue;
+    const bool full = cf + 3 < A.Cout;
+    float sc[4], sh[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      sc[r] = (S.scale && cf + r < A.Cout) ? S.scale[cf + r] : 1.f;
+      sh[r] = (S.shift && cf + r < A.Cout) ? S.shift[cf + r] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < WP; ++j) {
+      if (!pok[j]) continue;
+      const size_t pix = ((size_t)pn[j] * S.OH + poy[j]) * S.OW + pox[j];
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * sc[r] + sh[r];
+      if (A.res) {
+        const bf16_t* R = (const bf16_t*)A.res + pix * A.ldr + A.cr0 + cf;
+        if (full) {
+          const uint2 h = *(const uint2*)R, m = *(const uint2*)(R + psr), l = *(const uint2*)(R + 2 * psr);
+          const uint32_t hw[2] = {h.x, h.y}, mw[2] = {m.x, m.y}, lw[2] = {l.x, l.y};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int sft = (r & 1) * 16;
+            v[r] += join3((bf16_t)(hw[r >> 1] >> sft), (bf16_t)(mw[r >> 1] >> sft), (bf16_t)(lw[r >> 1] >> sft));
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (cf + r < A.Cout) v[r] += join3(R[r], R[r + psr], R[r + 2 * psr]);
+        }
+      }
+      if (A.relu) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+      }
+      if (A.out_mode == ZP_OUT_HEAD_NCHW) {
+        const size_t plane = (size_t)S.OH * S.OW;
+        const size_t sp = (size_t)poy[j] * S.OW + pox[j];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = cf + r;
+          if (c >= A.Cout) continue;
+          if (c == 0) ((float*)S.y)[(size_t)pn[j] * plane + sp] = v[r];
+          else ((float*)S.y2)[((size_t)pn[j] * (A.Cout - 1) + (c - 1)) * plane + sp] = v[r];
+        }
+        continue;
+      }
+      bf16_t h[4], m[4], l[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) split3(v[r], h[r], m[r], l[r]);
+      bf16_t* Y = (bf16_t*)S.y + pix * S.ldy + S.cy0 + cf;
+      if (full) {
+        *(uint2*)Y = make_uint2((uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16));
+        *(uint2*)(Y + psy) = make_uint2((uint32_t)m[0] | ((uint32_t)m[1] << 16), (uint32_t)m[2] | ((uint32_t)m[3] << 16));
+        *(uint2*)(Y + 2 * psy) =
+            make_uint2((uint32_t)l[0] | ((uint32_t)l[1] << 16), (uint32_t)l[2] | ((uint32_t)l[3] << 16));
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (cf + r < A.Cout) {
+            Y[r] = h[r];
+            Y[r + psy] = m[r];
+            Y[r + 2 * psy] = l[r];
+          }
+      }
+    }
+  }
+}
+
 }  // namespace zp
 
 using namespace zp;
@@ -2317,6 +2605,7 @@ static int strip_tc(const zp_conv_args& a) {
   return 128;
 }
 static int conv_tc(const zp_conv_args& a) {
+  if (a.dtype == ZP_F32X3) return a.Cout > 64 ? 128 : (a.Cout > 32 ? 64 : 32);  // k_conv3
   if (quad_plan(a, nullptr)) return 64;  // k_conv_quad: 64 channels x 4 phases
   // strip-eligible layers take k_conv_strip's 128-channel tile: it stages fewer bytes per FLOP than
   // the 256-channel k_conv tile, and a 256-channel strip tile does not fit the register file
@@ -2361,7 +2650,8 @@ static int conv_flags() {
 // ZP_CONV_STRIP=0 disables.
 static bool strip_eligible(const zp_conv_args& a, strip_geo* sg) {
   static const int en = getenv("ZP_CONV_STRIP") ? env_int("ZP_CONV_STRIP") : 1;
-  if (!en || a.dtype == ZP_F32 || a.nsub != 1 || a.Cin % 64 != 0 || a.Cout % 64 != 0) return false;
+  if (!en || a.dtype == ZP_F32 || a.dtype == ZP_F32X3 || a.nsub != 1 || a.Cin % 64 != 0 || a.Cout % 64 != 0)
+    return false;
   if (a.Cout <= 64 && !g_strip_c64) return false;
   if (a.sy != 1 || a.sx != 1 || a.GH != a.IH || a.GW != a.IW) return false;
   const zp_conv_sub& S = a.sub[0];
@@ -2401,7 +2691,7 @@ static bool strip_eligible(const zp_conv_args& a, strip_geo* sg) {
 // enough workgroups to cover the CUs.  qg: the byte offset of each schedule slot's tap.
 static bool quad_plan(const zp_conv_args& a, quad_geo* qg) {
   if (!(conv_flags() & 128)) return false;
-  if (a.dtype == ZP_F32 || a.nsub != 4 || a.Cin % 64 != 0 || a.Cout % 64 != 0) return false;
+  if (a.dtype == ZP_F32 || a.dtype == ZP_F32X3 || a.nsub != 4 || a.Cin % 64 != 0 || a.Cout % 64 != 0) return false;
   if (a.sy != 1 || a.sx != 1 || a.GH != a.IH || a.GW != a.IW) return false;
   if (a.GW != 32 && a.GW != 64) return false;
   if (((long)a.GH * a.GW) % 256 != 0) return false;
@@ -2427,12 +2717,83 @@ static bool quad_plan(const zp_conv_args& a, quad_geo* qg) {
   return true;
 }
 
+// k_conv3 pixel tile: 256 (8 waves, ping-pong pairs on every SIMD) for the 64- and 128-channel
+// tiles; the 32-channel tile (the head) takes 128 (32 + 256 rows = 18 tiles per plane do not split
+// over 8 waves evenly; 4 waves).  ZP_CONV3_TP=128 forces 128-pixel tiles (sweeps).
+static int conv3_tp(const zp_conv_args& a, int tc) {
+  static const int ov = env_int("ZP_CONV3_TP");
+  if (tc == 32) return 128;
+  if (ov == 128 || ov == 256) return ov;
+  return 256;
+}
+
+static int conv3_launch(const zp_conv_args& a, hipStream_t st) {
+  ZP_CHECK_ARG(a.Cin > 0 && a.Cin % 32 == 0, "zp_conv2d: ZP_F32X3 needs Cin %% 32 == 0 (got %d; the stem runs in f32 "
+               "with out_mode ZP_OUT_NHWC_X3)", a.Cin);
+  ZP_CHECK_ARG(a.ldx >= a.cx0 + a.Cin && a.cx0 % 8 == 0 && a.ldx % 8 == 0, "zp_conv2d: bad ldx/cx0");
+  ZP_CHECK_ARG(a.k_pad % 32 == 0, "zp_conv2d: k_pad %d not a multiple of 32", a.k_pad);
+  ZP_CHECK_ARG(!a.stats, "zp_conv2d: ZP_F32X3 is forward (eval) only: no train-mode statistics");
+  ZP_CHECK_ARG(a.out_mode == ZP_OUT_NHWC || a.out_mode == ZP_OUT_HEAD_NCHW,
+               "zp_conv2d: ZP_F32X3 writes split NHWC (ZP_OUT_NHWC) or the f32 head (ZP_OUT_HEAD_NCHW)");
+  const int tc = conv_tc(a);
+  ZP_CHECK_ARG(a.w_rows % tc == 0 && a.w_rows >= a.Cout, "zp_conv2d: w_rows %d", a.w_rows);
+  for (int s = 0; s < a.nsub; ++s) {
+    const zp_conv_sub& S = a.sub[s];
+    ZP_CHECK_ARG(S.w && S.y, "zp_conv2d: sub %d null w/y", s);
+    ZP_CHECK_ARG(S.ntaps >= 1 && S.ntaps <= ZP_MAX_TAPS && (long)S.ntaps * a.Cin <= a.k_pad,
+                 "zp_conv2d: sub %d ntaps %d / k_pad %d", s, S.ntaps, a.k_pad);
+    if (a.out_mode == ZP_OUT_NHWC)
+      ZP_CHECK_ARG(S.ldy >= S.cy0 + a.Cout && S.cy0 % 4 == 0 && S.ldy % 4 == 0, "zp_conv2d: bad ldy/cy0");
+    else
+      ZP_CHECK_ARG(S.y2 || a.Cout == 1, "zp_conv2d: head needs y2");
+    // the epilogue's plane strides assume every sub writes the same output tensor shape
+    ZP_CHECK_ARG(S.OH == a.sub[0].OH && S.OW == a.sub[0].OW, "zp_conv2d: ZP_F32X3 subs must share the output shape");
+  }
+  if (a.res) ZP_CHECK_ARG(a.ldr >= a.cr0 + a.Cout && a.cr0 % 4 == 0 && a.ldr % 4 == 0, "zp_conv2d: bad residual ld");
+  conv_taps tg{};
+  const long long xb = 3ll * a.N * a.IH * a.IW * a.ldx * 2;
+  const long long wb = 3ll * a.w_rows * a.k_pad * 2;
+  ZP_CHECK_ARG(xb < (1ll << 31) && wb < (1ll << 31),
+               "zp_conv2d: split input (%lld B) / weights (%lld B) must stay below 2 GiB per launch (split the batch)",
+               xb, wb);
+  tg.x_bytes = (unsigned)xb;
+  for (int s = 0; s < a.nsub; ++s) {
+    const zp_conv_sub& S = a.sub[s];
+    tg.w_bytes[s] = (unsigned)wb;
+    int nx = 1;
+    while (nx < S.ntaps && S.ty[nx] == S.ty[0]) ++nx;
+    const int ny = S.ntaps / nx;
+    tg.ny[s] = ny;
+    tg.nx[s] = nx;
+    tg.ty0[s] = S.ty[0];
+    tg.tx0[s] = S.tx[0];
+    tg.dty[s] = ny > 1 ? S.ty[nx] - S.ty[0] : 0;
+    tg.dtx[s] = nx > 1 ? S.tx[1] - S.tx[0] : 0;
+    bool grid = ny * nx == S.ntaps && ny <= 32 && nx <= 32;
+    for (int t = 0; grid && t < S.ntaps; ++t)
+      grid = S.ty[t] == tg.ty0[s] + (t / nx) * tg.dty[s] && S.tx[t] == tg.tx0[s] + (t % nx) * tg.dtx[s];
+    ZP_CHECK_ARG(grid, "zp_conv2d: sub %d taps must form a (row x column) grid of at most 32 x 32, rows outer", s);
+  }
+  const int tp = conv3_tp(a, tc);
+  const int gx = ceil_div((long)a.N * a.GH * a.GW, tp), gy = ceil_div(a.Cout, tc);
+  const dim3 grid(gx, gy, a.nsub);
+  const int fl = conv_flags();
+  if (tc == 128 && tp == 256) hipLaunchKernelGGL((k_conv3<4, 4>), grid, dim3(512), 0, st, a, tg, fl);
+  else if (tc == 128) hipLaunchKernelGGL((k_conv3<4, 2>), grid, dim3(256), 0, st, a, tg, fl);
+  else if (tc == 64 && tp == 256) hipLaunchKernelGGL((k_conv3<2, 4>), grid, dim3(512), 0, st, a, tg, fl);
+  else if (tc == 64) hipLaunchKernelGGL((k_conv3<2, 2>), grid, dim3(256), 0, st, a, tg, fl);
+  else hipLaunchKernelGGL((k_conv3<1, 2>), grid, dim3(256), 0, st, a, tg, fl);
+  ZP_LAUNCH_CHECK("zp_conv2d split-f32");
+  return ZP_OK;
+}
+
 // pixel tile: 256 (8 waves) whenever the cout tile allows it.  Measured on MI355X (R34 bs32,
 // profiles/r01_conv_sweep.md): the 8-wave 3-stage tile beats the 4-wave tiles even on the
 // 32x32 layers where it leaves part of the chip idle (fewer workgroups, but 2x the MFMA work
 // per LDS byte and deeper prefetch)
 static int conv_tp(const zp_conv_args& a) {
   int tc = a.Cout > 64 ? 128 : (a.Cout > 32 ? 64 : 32);
+  if (a.dtype == ZP_F32X3) return conv3_tp(a, tc);
   if (tc == 32) return 128;  // 32 + 256 rows do not split over 8 waves in 8-row groups
   if (strip_eligible(a, nullptr) || quad_plan(a, nullptr)) return 256;
   if (conv_tc(a) == 256) return 256;  // the 256-channel tile exists only with 256-pixel tiles
@@ -2470,10 +2831,12 @@ extern "C" int zp_conv2d_grid(const zp_conv_args* a) {
 extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
   ZP_CHECK_ARG(ap != nullptr, "zp_conv2d: null args");
   const zp_conv_args& a = *ap;
-  ZP_CHECK_ARG(a.dtype == ZP_F32 || a.dtype == ZP_BF16 || a.dtype == ZP_F16, "zp_conv2d: bad dtype %d", a.dtype);
+  ZP_CHECK_ARG(a.dtype == ZP_F32 || a.dtype == ZP_BF16 || a.dtype == ZP_F16 || a.dtype == ZP_F32X3,
+               "zp_conv2d: bad dtype %d", a.dtype);
   ZP_CHECK_ARG(a.nsub >= 1 && a.nsub <= ZP_MAX_SUB, "zp_conv2d: nsub %d", a.nsub);
   ZP_CHECK_ARG(a.x && a.N > 0 && a.GH > 0 && a.GW > 0 && a.IH > 0 && a.IW > 0 && a.Cout > 0,
                "zp_conv2d: bad geometry");
+  if (a.dtype == ZP_F32X3) return conv3_launch(a, (hipStream_t)stream);
   const int E = a.dtype == ZP_F32 ? 4 : 8, KE = 8 * E;
   const bool smallc = a.Cin < KE;
   ZP_CHECK_ARG(a.Cin > 0 && a.Cin % E == 0 && (smallc || a.Cin % KE == 0),
@@ -2481,7 +2844,8 @@ extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
   ZP_CHECK_ARG(a.ldx >= a.cx0 + a.Cin && a.cx0 % E == 0 && a.ldx % E == 0, "zp_conv2d: bad ldx/cx0");
   ZP_CHECK_ARG(a.k_pad % KE == 0, "zp_conv2d: k_pad %d not a multiple of %d", a.k_pad, KE);
   ZP_CHECK_ARG(a.w_rows % conv_tc(a) == 0 && a.w_rows >= a.Cout, "zp_conv2d: w_rows %d", a.w_rows);
-  ZP_CHECK_ARG(a.out_mode >= 0 && a.out_mode <= 2, "zp_conv2d: out_mode");
+  ZP_CHECK_ARG((a.out_mode >= 0 && a.out_mode <= 2) || (a.out_mode == ZP_OUT_NHWC_X3 && a.dtype == ZP_F32 && !a.stats),
+               "zp_conv2d: out_mode %d", a.out_mode);
   ZP_CHECK_ARG(!a.stats || (!a.res && !a.relu && a.out_mode != ZP_OUT_HEAD_NCHW && !a.sub[0].scale &&
                             !a.sub[0].shift),
                "zp_conv2d: stats are taken on the raw conv output (no scale/shift/residual/relu/head)");
@@ -2814,7 +3178,7 @@ extern "C" int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* st
   *tc = conv_tc(*a);
   *tp = conv_tp(*a);
   *stages = *tc == 256 ? 2 : conv_stages(*a, *tc);
-  *variant = quad_plan(*a, nullptr) ? 3 : *tc <= 128 && strip_eligible(*a, nullptr) ? ((conv_flags() & 64) ? 2 : 1) : 0;
+  *variant = a->dtype == ZP_F32X3 ? 4 : quad_plan(*a, nullptr) ? 3 : *tc <= 128 && strip_eligible(*a, nullptr) ? ((conv_flags() & 64) ? 2 : 1) : 0;
   return ZP_OK;
 }
 

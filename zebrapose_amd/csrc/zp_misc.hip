@@ -93,13 +93,45 @@ __global__ void k_pack(const PackArgs a) {
   }
 }
 
+// ZP_F32X3 packing: the same element map as k_pack, the f32 weight split into three bf16 planes
+// [3][rows_pad][k_pad]
+__global__ void k_pack_x3(const PackArgs a) {
+  const long total = (long)a.rows_pad * a.k_pad;
+  const int rows = a.transposed ? a.d1 : a.d0;
+  const int chans = a.transposed ? a.d0 : a.d1;
+  bf16_t* d = (bf16_t*)a.dst;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    int r = (int)(e / a.k_pad), k = (int)(e - (long)r * a.k_pad);
+    int t = k / a.cstride, c = k - t * a.cstride;
+    float v = 0.f;
+    if (r < rows && t < a.ntaps && c < chans) {
+      int ky = a.ky[t], kx = a.kx[t];
+      size_t idx = a.transposed ? (((size_t)c * a.d1 + r) * a.kh + ky) * a.kw + kx
+                                : (((size_t)r * a.d1 + c) * a.kh + ky) * a.kw + kx;
+      v = a.src[idx];
+    }
+    bf16_t h, m, l;
+    split3(v, h, m, l);
+    d[e] = h;
+    d[e + total] = m;
+    d[e + 2 * total] = l;
+  }
+}
+
 // one launch for many pack jobs: blockIdx.y = job (read once, uniform), threads over the job's
 // (row, channel) pairs; each thread reads its pair's kh x kw taps (contiguous in the checkpoint
 // layout, so a wave reads one contiguous span) and writes them at k = t * cstride + c (adjacent
 // threads -> adjacent k: coalesced 2-byte stores), then the pair's share of the k_pad tail (zeros).
 // Same result as zp_pack_weight per job.
 __device__ __forceinline__ void pack_store(const zp_pack_job& a, int d, float v) {
-  if (a.dtype == ZP_BF16) ((bf16_t*)a.dst)[d] = f2bf(v);
+  if (a.dtype == ZP_F32X3) {  // three planes of rows_pad * k_pad
+    const size_t ps = (size_t)a.rows_pad * a.k_pad;
+    bf16_t h, m, l;
+    split3(v, h, m, l);
+    ((bf16_t*)a.dst)[d] = h;
+    ((bf16_t*)a.dst)[d + ps] = m;
+    ((bf16_t*)a.dst)[d + 2 * ps] = l;
+  } else if (a.dtype == ZP_BF16) ((bf16_t*)a.dst)[d] = f2bf(v);
   else if (a.dtype == ZP_F16) ((f16_t*)a.dst)[d] = (f16_t)v;
   else ((float*)a.dst)[d] = v;
 }
@@ -707,6 +739,84 @@ __global__ void k_maxpool(const T* __restrict__ x, int B, int IH, int IW, int ld
   }
 }
 
+// ZP_F32X3 max pool: the 3x3 window max of the joined f32 values (PyTorch CPU rule), stored split
+// again (the split of a value is unique, so the winner's planes are reproduced exactly).  Planes:
+// x + p * psx, y + p * psy.
+__global__ void k_maxpool_x3(const bf16_t* __restrict__ x, long psx, int B, int IH, int IW, int ldx, int cx0, int C,
+                             bf16_t* __restrict__ y, long psy, int OH, int OW, int ldy, int cy0) {
+  const int CV = C / 8;
+  const long total = (long)B * OH * OW * CV;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    long pix = e / CV;
+    int c = (int)(e - pix * CV) * 8;
+    int ox = (int)(pix % OW);
+    long t = pix / OW;
+    int oy = (int)(t % OH), b = (int)(t / OH);
+    float m[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) m[i] = -INFINITY;
+    for (int ky = 0; ky < 3; ++ky) {
+      int iy = oy * 2 - 1 + ky;
+      if ((unsigned)iy >= (unsigned)IH) continue;
+      for (int kx = 0; kx < 3; ++kx) {
+        int ix = ox * 2 - 1 + kx;
+        if ((unsigned)ix >= (unsigned)IW) continue;
+        const size_t o = (((size_t)b * IH + iy) * IW + ix) * ldx + cx0 + c;
+        const uint4 h = *(const uint4*)(x + o), mm = *(const uint4*)(x + o + psx), l = *(const uint4*)(x + o + 2 * psx);
+        const uint32_t hw[4] = {h.x, h.y, h.z, h.w}, mw[4] = {mm.x, mm.y, mm.z, mm.w}, lw[4] = {l.x, l.y, l.z, l.w};
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int s = (i & 1) * 16;
+          const float v = join3((bf16_t)(hw[i >> 1] >> s), (bf16_t)(mw[i >> 1] >> s), (bf16_t)(lw[i >> 1] >> s));
+          if (v > m[i] || isnan(v)) m[i] = v;
+        }
+      }
+    }
+    uint32_t o[3][4];
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) {
+      bf16_t h0, m0, l0, h1, m1, l1;
+      split3(m[i], h0, m0, l0);
+      split3(m[i + 1], h1, m1, l1);
+      o[0][i >> 1] = (uint32_t)h0 | ((uint32_t)h1 << 16);
+      o[1][i >> 1] = (uint32_t)m0 | ((uint32_t)m1 << 16);
+      o[2][i >> 1] = (uint32_t)l0 | ((uint32_t)l1 << 16);
+    }
+    bf16_t* yo = y + pix * ldy + cy0 + c;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) *(uint4*)(yo + p * psy) = make_uint4(o[p][0], o[p][1], o[p][2], o[p][3]);
+  }
+}
+
+// ZP_F32X3 global average pool: block = (64 channels, image b); the joined values summed in double
+// (CPU adaptive_avg_pool2d's accumulator) over 4 pixel lanes, combined in a fixed order; the f32
+// mean stored split into y [3][B][C]
+__global__ void __launch_bounds__(256) k_avgpool_x3(const bf16_t* __restrict__ x, long psx, int H, int W, int ldx,
+                                                    int cx0, int C, bf16_t* __restrict__ y, long psy) {
+  __shared__ double red[4][64];
+  const int b = blockIdx.y;
+  const long HW = (long)H * W;
+  const int cl = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  double s = 0.0;
+  if (c < C)
+    for (long p = sl; p < HW; p += 4) {
+      const size_t o = ((size_t)b * HW + p) * ldx + cx0 + c;
+      s += (double)join3(x[o], x[o + psx], x[o + 2 * psx]);
+    }
+  red[sl][cl] = s;
+  __syncthreads();
+  if (threadIdx.x < 64 && c < C) {
+    const double t = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+    bf16_t h, m, l;
+    split3((float)(t / (double)HW), h, m, l);
+    const size_t o = (size_t)b * C + c;
+    y[o] = h;
+    y[o + psy] = m;
+    y[o + 2 * psy] = l;
+  }
+}
+
 // Window (oy, ox) of the 3x3 / stride-2 / pad-1 pool: per channel, the tap (ky*3+kx, -1 when the
 // window lies outside the output) of its first maximum in (ky, kx) scan order (PyTorch CPU rule:
 // `>` or NaN) and the window's dy.
@@ -1072,7 +1182,8 @@ extern "C" int zp_conv_rows_pad(int Cout) {
 
 extern "C" int zp_pack_weight(const float* src, int d0, int d1, int kh, int kw, int transposed, int ntaps, const int* ky,
                               const int* kx, int cstride, int dtype, void* dst, int rows_pad, int k_pad, void* stream) {
-  ZP_DTYPE_CHECK("zp_pack_weight", dtype);
+  ZP_CHECK_ARG(dtype == ZP_F32 || dtype == ZP_BF16 || dtype == ZP_F16 || dtype == ZP_F32X3,
+               "zp_pack_weight: bad dtype %d", dtype);
   ZP_CHECK_ARG(src && dst && ky && kx, "zp_pack_weight: null pointer");
   ZP_CHECK_ARG(ntaps >= 1 && ntaps <= ZP_MAX_TAPS, "zp_pack_weight: ntaps %d", ntaps);
   ZP_CHECK_ARG(cstride >= (transposed ? d0 : d1) && (long)ntaps * cstride <= k_pad, "zp_pack_weight: cstride/k_pad");
@@ -1085,7 +1196,10 @@ extern "C" int zp_pack_weight(const float* src, int d0, int d1, int kh, int kw, 
     a.ky[t] = (signed char)ky[t];
     a.kx[t] = (signed char)kx[t];
   }
-  ZP_BY_DTYPE(dtype, k_pack, dim3(grid_for((long)rows_pad * k_pad)), dim3(256), (hipStream_t)stream, a);
+  if (dtype == ZP_F32X3)
+    hipLaunchKernelGGL(k_pack_x3, dim3(grid_for((long)rows_pad * k_pad)), dim3(256), 0, (hipStream_t)stream, a);
+  else
+    ZP_BY_DTYPE(dtype, k_pack, dim3(grid_for((long)rows_pad * k_pad)), dim3(256), (hipStream_t)stream, a);
   ZP_LAUNCH_CHECK("zp_pack_weight");
   return ZP_OK;
 }
@@ -1261,6 +1375,17 @@ extern "C" int zp_nchw_to_nhwc(const float* x, int B, int C, int H, int W, int c
 
 extern "C" int zp_maxpool3s2(const void* x, int B, int IH, int IW, int ldx, int cx0, int C, int dtype, void* y, int OH,
                              int OW, int ldy, int cy0, void* stream) {
+  if (dtype == ZP_F32X3) {
+    ZP_CHECK_ARG(x && y && C % 8 == 0 && cx0 % 8 == 0 && ldx % 8 == 0 && cy0 % 8 == 0 && ldy % 8 == 0,
+                 "zp_maxpool3s2: bad args / alignment");
+    ZP_CHECK_ARG(OH == (IH - 1) / 2 + 1 && OW == (IW - 1) / 2 + 1, "zp_maxpool3s2: OH/OW");
+    const long total = (long)B * OH * OW * (C / 8);
+    hipLaunchKernelGGL(k_maxpool_x3, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
+                       (long)B * IH * IW * ldx, B, IH, IW, ldx, cx0, C, (bf16_t*)y, (long)B * OH * OW * ldy, OH, OW,
+                       ldy, cy0);
+    ZP_LAUNCH_CHECK("zp_maxpool3s2");
+    return ZP_OK;
+  }
   ZP_DTYPE_CHECK("zp_maxpool3s2", dtype);
   const int N = dtype == ZP_F32 ? 4 : 8;
   ZP_CHECK_ARG(x && y && C % N == 0 && cx0 % N == 0 && ldx % N == 0 && cy0 % N == 0 && ldy % N == 0,
@@ -1290,6 +1415,13 @@ extern "C" int zp_maxpool3s2_bwd(const void* x, int ldx, int cx0, const void* dy
 
 extern "C" int zp_global_avgpool(const void* x, int B, int H, int W, int ldx, int cx0, int C, int dtype, void* y,
                                  void* stream) {
+  if (dtype == ZP_F32X3) {  // y: [3][B][C]
+    ZP_CHECK_ARG(x && y && B > 0 && H > 0 && W > 0 && C > 0, "zp_global_avgpool: bad args");
+    hipLaunchKernelGGL(k_avgpool_x3, dim3((C + 63) / 64, B), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
+                       (long)B * H * W * ldx, H, W, ldx, cx0, C, (bf16_t*)y, (long)B * C);
+    ZP_LAUNCH_CHECK("zp_global_avgpool");
+    return ZP_OK;
+  }
   ZP_DTYPE_CHECK("zp_global_avgpool", dtype);
   ZP_CHECK_ARG(x && y && B > 0 && H > 0 && W > 0 && C > 0, "zp_global_avgpool: bad args");
   const int N = dtype == ZP_F32 ? 4 : 8;
@@ -1312,6 +1444,17 @@ extern "C" int zp_global_avgpool(const void* x, int B, int H, int W, int ldx, in
 
 extern "C" int zp_broadcast_hw(const void* src, int B, int C, int dtype, void* y, int H, int W, int ldy, int cy0,
                                void* stream) {
+  if (dtype == ZP_F32X3) {  // src [3][B][C] -> the three planes of y [3][B, H, W, ldy]
+    ZP_CHECK_ARG(src && y && B > 0 && C > 0 && C % 8 == 0 && ldy % 8 == 0 && cy0 % 8 == 0,
+                 "zp_broadcast_hw: bad args / alignment");
+    const long total = (long)B * H * W * C;
+    for (int p = 0; p < 3; ++p)
+      hipLaunchKernelGGL(k_broadcast_vec<bf16_t>, dim3(grid_for(total / 8)), dim3(256), 0, (hipStream_t)stream,
+                         (const bf16_t*)src + (long)p * B * C, B, C, (bf16_t*)y + (long)p * B * H * W * ldy, H, W,
+                         ldy, cy0);
+    ZP_LAUNCH_CHECK("zp_broadcast_hw");
+    return ZP_OK;
+  }
   ZP_DTYPE_CHECK("zp_broadcast_hw", dtype);
   ZP_CHECK_ARG(src && y && B > 0 && C > 0, "zp_broadcast_hw: bad args");
   long total = (long)B * H * W * C;

@@ -32,8 +32,10 @@ from . import _lib as L
 from . import geometry as G
 from .model.resnet import TVBottleneck
 
-_KE = {L.ZP_F32: 32, L.ZP_BF16: 64, L.ZP_F16: 64}
-_E = {L.ZP_F32: 4, L.ZP_BF16: 8, L.ZP_F16: 8}
+_KE = {L.ZP_F32: 32, L.ZP_BF16: 64, L.ZP_F16: 64, L.ZP_F32X3: 32}
+_E = {L.ZP_F32: 4, L.ZP_BF16: 8, L.ZP_F16: 8, L.ZP_F32X3: 8}
+_ES = {L.ZP_F32: 4, L.ZP_BF16: 2, L.ZP_F16: 2, L.ZP_F32X3: 6}  # bytes per element (x3: three bf16 planes)
+_TN = {L.ZP_F32: "f32", L.ZP_BF16: "bf16", L.ZP_F16: "f16", L.ZP_F32X3: "x3"}
 
 
 class Act:
@@ -50,6 +52,16 @@ class Act:
     ld = property(lambda s: s.buf.shape[3])
     P = property(lambda s: s.buf.shape[0] * s.buf.shape[1] * s.buf.shape[2])
     ptr = property(lambda s: s.buf.data_ptr())
+
+
+def joined(buf):
+    """The f32 values of an activation buffer: itself, or -- for an x3 engine's plane-0 view of a
+    [3, ...] bf16 tensor -- (hi + mid) + lo, which is exact (include/zp.h ZP_F32X3)."""
+    base = buf._base
+    if buf.dtype == torch.bfloat16 and base is not None and base.dim() == buf.dim() + 1 and base.shape[0] == 3 \
+            and base.data_ptr() == buf.data_ptr():
+        return (base[0].float() + base[1].float()) + base[2].float()
+    return buf.float()
 
 
 def _i32arr(v):
@@ -95,10 +107,15 @@ class Tape:
 class Engine:
     """Executes a BinaryCodeNet_Deeplab module tree (zebrapose_amd.model) with libzp."""
 
-    def __init__(self, net, dtype=torch.bfloat16):
+    def __init__(self, net, dtype=torch.bfloat16, x3=False):
+        """x3: fp32 in split form (include/zp.h ZP_F32X3): every activation / packed weight is three
+        bf16 planes (hi, mid, lo) summing exactly to the f32 value, and every conv product is formed
+        from its six leading terms on bf16 MFMAs (f32-accurate).  Eval-mode forward only; the
+        fp32 network's training path keeps the exact-f32 MFMA engine."""
         self._net = weakref.ref(net)
-        self.dtype = dtype
-        self.dt = L.dtype_code(dtype)
+        self.x3 = x3
+        self.dtype = torch.bfloat16 if x3 else dtype
+        self.dt = L.ZP_F32X3 if x3 else L.dtype_code(dtype)
         self._packed = {}
         self._jobs = []  # (cache key, weight, PackJob) of every cached packing, for _prepack
         self._job_table = None
@@ -137,32 +154,44 @@ class Engine:
         self._job_table = None
         self._folds.clear()
 
-    def _pack(self, unit, sub, transposed, cstride, k_pad, rows, tag, cache=True):
+    def _empty(self, shape, dev):
+        """An activation buffer of this engine's storage: plane 0 (a [B, H, W, C] view) of a
+        [3, B, H, W, C] bf16 tensor in x3 mode."""
+        if self.x3:
+            return torch.empty((3,) + tuple(shape), dtype=torch.bfloat16, device=dev)[0]
+        return torch.empty(shape, dtype=self.dtype, device=dev)
+
+    def _pack(self, unit, sub, transposed, cstride, k_pad, rows, tag, cache=True, dt=None):
         """Packed weights of one (conv, sub-problem, role), cached on the weight's version counter.
-        Every packing is also recorded as a job of the batched repack (_prepack)."""
+        Every packing is also recorded as a job of the batched repack (_prepack).  dt overrides the
+        engine's dtype code (the x3 engine's f32 stem)."""
+        dt = self.dt if dt is None else dt
         w = unit.conv.weight
-        key = (id(unit.conv), tag, tuple(sub.taps), cstride, k_pad, self.dt)
+        key = (id(unit.conv), tag, tuple(sub.taps), cstride, k_pad, dt)
         ver = (w._version, w.data_ptr())
         hit = self._packed.get(key) if cache else None
         if hit is not None and hit[0] == ver:
             return hit[1]
         d0, d1 = w.shape[0], w.shape[1]
-        if hit is not None and hit[1].shape == (rows, k_pad):
+        shape = (3, rows, k_pad) if dt == L.ZP_F32X3 else (rows, k_pad)
+        if hit is not None and tuple(hit[1].shape) == shape:
             out = hit[1]
         else:
-            out = torch.empty((rows, k_pad), dtype=self.dtype, device=w.device)
+            tdt = torch.bfloat16 if dt == L.ZP_F32X3 else {L.ZP_F32: torch.float32, L.ZP_BF16: torch.bfloat16,
+                                                             L.ZP_F16: torch.float16}[dt]
+            out = torch.empty(shape, dtype=tdt, device=w.device)
             self._cache_gen += 1
         ky = [t[0] for t in sub.taps]
         kx = [t[1] for t in sub.taps]
         L.call("zp_pack_weight", w.data_ptr(), d0, d1, w.shape[2], w.shape[3], transposed, len(sub.taps),
-               _i32arr(ky), _i32arr(kx), cstride, self.dt, out.data_ptr(), rows, k_pad, L.stream_ptr())
+               _i32arr(ky), _i32arr(kx), cstride, dt, out.data_ptr(), rows, k_pad, L.stream_ptr())
         if cache:
             if key not in self._packed:
                 j = L.PackJob()
                 j.src, j.dst = w.data_ptr(), out.data_ptr()
                 j.d0, j.d1, j.kh, j.kw = d0, d1, w.shape[2], w.shape[3]
                 j.transposed, j.ntaps, j.cstride, j.rows_pad, j.k_pad, j.dtype = \
-                    transposed, len(sub.taps), cstride, rows, k_pad, self.dt
+                    transposed, len(sub.taps), cstride, rows, k_pad, dt
                 for t, (a, b) in enumerate(zip(ky, kx)):
                     j.ky[t], j.kx[t] = a, b
                 self._jobs.append((key, w, j))
@@ -219,10 +248,12 @@ class Engine:
 
     # ------------------------------------------------------------------ conv launch
     def _conv(self, x: Act, plan, cout, weights, k_pad, rows, outs, res=None, relu=False,
-              out_mode=L.ZP_OUT_NHWC, stats=None, small=None, label=None):
-        """weights / outs: per sub.  outs[i] = (y_ptr, ldy, cy0, OH, OW, scale, shift, y2)."""
+              out_mode=L.ZP_OUT_NHWC, stats=None, small=None, label=None, dt=None):
+        """weights / outs: per sub.  outs[i] = (y_ptr, ldy, cy0, OH, OW, scale, shift, y2).  dt
+        overrides the engine's dtype code (the x3 engine's f32 stem)."""
+        dt = self.dt if dt is None else dt
         a = L.ConvArgs()
-        a.dtype = self.dt
+        a.dtype = dt
         a.x = x.ptr
         a.ldx, a.cx0, a.IH, a.IW, a.Cin = x.ld, x.c0, x.H, x.W, x.C
         a.N, a.GH, a.GW, a.sy, a.sx = x.B, plan.GH, plan.GW, plan.sy, plan.sy
@@ -260,13 +291,13 @@ class Engine:
             if self.timing is not None:
                 e1.record()
             flops = 2.0 * x.B * plan.GH * plan.GW * sum(len(sb.taps) for sb in plan.subs) * x.C * cout
-            kname = self._kname(a, plan, x)
+            kname = self._kname(a, plan, x, dt)
             geo = (f"{label}:{x.C}->{cout} taps{max(len(sb.taps) for sb in plan.subs)} "
                    f"{x.H}x{x.W}->{plan.GH}x{plan.GW}x{a.nsub}")
             # algorithmic HBM bytes: the input slice and every output read / written once, the
             # packed weights of each sub-problem once (the residual, when fused, read once)
-            es = 4 if self.dt == L.ZP_F32 else 2
-            osz = 4 if out_mode == L.ZP_OUT_HEAD_NCHW else es
+            es = _ES[dt]
+            osz = 4 if out_mode == L.ZP_OUT_HEAD_NCHW else (6 if out_mode == L.ZP_OUT_NHWC_X3 else es)
             mgrid = x.B * plan.GH * plan.GW
             nbytes = (x.P * x.C * es + len(plan.subs) * mgrid * cout * osz
                       + sum(w.numel() * w.element_size() for w in weights) + (0 if res is None else mgrid * cout * es))
@@ -278,12 +309,15 @@ class Engine:
             L.check(L.lib.zp_conv2d(C.byref(a), st), "zp_conv2d")
         return stats, parts
 
-    def _kname(self, a, plan, x):
+    def _kname(self, a, plan, x, dt=None):
         """rocprofv3's kernel instantiation of this launch, in the label form tools/prof_summary.py
         maps the demangled names to."""
+        dt = self.dt if dt is None else dt
         tc, tp, stages, var = C.c_int(), C.c_int(), C.c_int(), C.c_int()
         L.call("zp_conv2d_config", C.byref(a), C.byref(tc), C.byref(tp), C.byref(stages), C.byref(var))
-        tn = {L.ZP_F32: "f32", L.ZP_BF16: "bf16", L.ZP_F16: "f16"}[self.dt]
+        tn = _TN[dt]
+        if var.value == 4:  # rocprofv3 name: k_conv3<WC, NWP>
+            return f"k_conv3<WC={tc.value // 32},NWP={tp.value // 64}>"
         if var.value == 1:  # rocprofv3 name: k_conv_strip<T, WC, STAGES, SPW = 5>
             return f"k_conv_strip<{tn},WC={tc.value // 32},ST=3>"
         if var.value == 3:  # rocprofv3 name: k_conv_quad<T, W>
@@ -292,16 +326,17 @@ class Engine:
             return f"k_conv_strip2<{tn},WC={tc.value // 32}>"
         # rocprofv3 name: k_conv<T, WC = tc / 32, WP = 4, NWP = tp / 64, STAGES, smallC>
         return (f"k_conv<{tn},WC={tc.value // 32},WP=4,"
-                f"NWP={tp.value // 64},ST={stages.value},smallC={int(x.C < _KE[self.dt])}>")
+                f"NWP={tp.value // 64},ST={stages.value},smallC={int(x.C < _KE[dt])}>")
 
     def _kpad(self, ntaps, cin):
         return G.ceil_to(ntaps * cin, _KE[self.dt])
 
-    def _fwd_weights(self, unit, plan, cache):
-        kp = max(self._kpad(len(sb.taps), unit.cin) for sb in plan.subs)
+    def _fwd_weights(self, unit, plan, cache, dt=None):
+        dt = self.dt if dt is None else dt
+        kp = max(G.ceil_to(len(sb.taps) * unit.cin, _KE[dt]) for sb in plan.subs)
         rows = L.lib.zp_conv_rows_pad(unit.cout)
         tr = 1 if unit.kind == "convT" else 0
-        ws = [self._pack(unit, sb, tr, unit.cin, kp, rows, "fwd", cache) for sb in plan.subs]
+        ws = [self._pack(unit, sb, tr, unit.cin, kp, rows, "fwd", cache, dt=dt) for sb in plan.subs]
         return ws, kp, rows
 
     def _small(self, cin, k, d, p):
@@ -314,6 +349,18 @@ class Engine:
         OH, OW = unit.out_hw(x.H, x.W)
         assert (out.H, out.W, out.C) == (OH, OW, unit.cout), ((out.H, out.W, out.C), (OH, OW, unit.cout))
         train = tape is not None
+        if self.x3 and unit.cin < _KE[self.dt]:
+            # the split-mode stem: its 3 (-> 8) input channels are below k_conv3's 32-channel K step;
+            # it runs the exact-f32 small-Cin kernel on the f32 NHWC input and writes split output
+            assert not train, "the x3 engine runs eval forwards only"
+            ws, kp, rows = self._fwd_weights(unit, plan, cache=True, dt=L.ZP_F32)
+            scale, shift = self._fold(unit)
+            outs = [(out.ptr, out.ld, out.c0, OH, OW, scale, shift, None)] * len(plan.subs)
+            self._conv(x, plan, unit.cout, ws, kp, rows, outs, res, unit.relu, out_mode=L.ZP_OUT_NHWC_X3,
+                       small=(unit.k, unit.d, unit.p), label=label, dt=L.ZP_F32)
+            if self.trace is not None:
+                self.trace.append(("conv", unit, x, out, res))
+            return
         ws, kp, rows = self._fwd_weights(unit, plan, cache=True)
         small = self._small(unit.cin, unit.k, unit.d, unit.p)
         if not train or unit.bn is None:
@@ -610,22 +657,28 @@ class Engine:
             raise ValueError("input height / width must be multiples of 8")
         dev, dt = x.device, self.dtype
         tape = Tape() if train else None
+        if self.x3 and train:
+            raise RuntimeError("the split-fp32 (x3) engine runs eval forwards only")
 
         def new(h, w, c):
-            return Act(torch.empty((B, h, w, c), dtype=dt, device=dev))
+            return Act(self._empty((B, h, w, c), dev))
 
         self._prepack(dev)
         st = L.stream_ptr()
         self.stage = "stem"
-        xin = new(H, W, 8)
-        L.call("zp_nchw_to_nhwc", x.data_ptr(), B, 3, H, W, 8, self.dt, xin.ptr, st)
+        if self.x3:  # the stem reads f32 (exact-f32 small-Cin kernel) and writes split output
+            xin = Act(torch.empty((B, H, W, 8), dtype=torch.float32, device=dev))
+            L.call("zp_nchw_to_nhwc", x.data_ptr(), B, 3, H, W, 8, L.ZP_F32, xin.ptr, st)
+        else:
+            xin = new(H, W, 8)
+            L.call("zp_nchw_to_nhwc", x.data_ptr(), B, 3, H, W, 8, self.dt, xin.ptr, st)
         if self.trace is not None and tape is None:
             self.trace.append(("input", None, x, xin, None))
         r = rn.resnet
         H2, W2 = H // 2, W // 2
         H4, W4, H8, W8 = H // 4, W // 4, H // 8, W // 8
         c64 = 64 if rn.num_layers == 34 else 256
-        head_in = torch.empty((B, H2, W2, 320), dtype=dt, device=dev)
+        head_in = self._empty((B, H2, W2, 320), dev)
         x128 = Act(head_in, 256, 64)
         self.unit_fwd(self._u(r[0], r[1], True, cin_act=8), xin, x128, tape, label="stem")
         self.stage = "layer1"
@@ -635,7 +688,7 @@ class Engine:
             tape.recs.append(("maxpool", x128, pooled))
         elif self.trace is not None:
             self.trace.append(("maxpool", None, x128, pooled, None))
-        up2_in = torch.empty((B, H4, W4, 256 + c64), dtype=dt, device=dev)
+        up2_in = self._empty((B, H4, W4, 256 + c64), dev)
         x64 = Act(up2_in, 256, c64)
         h = self._layer(r[4], pooled, x64, tape)
         self.stage = "layer2"
@@ -646,17 +699,17 @@ class Engine:
         xh = self._layer(rn.layer5, h, None, tape)
         # ---- ASPP (aspp.py:83-99)
         self.stage = "aspp"
-        A = torch.empty((B, H8, W8, 1280), dtype=dt, device=dev)
+        A = self._empty((B, H8, W8, 1280), dev)
         br = [self._u(aspp.conv_1x1_1, aspp.bn_conv_1x1_1), self._u(aspp.conv_3x3_1, aspp.bn_conv_3x3_1),
               self._u(aspp.conv_3x3_2, aspp.bn_conv_3x3_2), self._u(aspp.conv_3x3_3, aspp.bn_conv_3x3_3)]
         self.aspp_branches_fwd(br, xh, [Act(A, 256 * i, 256) for i in range(4)], tape)
-        pool = Act(torch.empty((B, 1, 1, xh.C), dtype=dt, device=dev))
+        pool = Act(self._empty((B, 1, 1, xh.C), dev))
         L.call("zp_global_avgpool", xh.ptr, B, H8, W8, xh.ld, xh.c0, xh.C, self.dt, pool.ptr, st)
         if tape is not None:  # tape order = forward order (the backward walks it reversed)
             tape.recs.append(("avgpool", xh, pool))
         elif self.trace is not None:
             self.trace.append(("avgpool", None, xh, pool, None))
-        imgo = Act(torch.empty((B, 1, 1, 256), dtype=dt, device=dev))
+        imgo = Act(self._empty((B, 1, 1, 256), dev))
         self.unit_fwd(self._u(aspp.conv_1x1_2, aspp.bn_conv_1x1_2), pool, imgo, tape, label="aspp_pool")
         L.call("zp_broadcast_hw", imgo.ptr, B, 256, self.dt, A.data_ptr(), H8, W8, 1280, 1024, st)
         if tape is not None:
@@ -749,10 +802,10 @@ class Engine:
     def _upsample(self, seq, x: Act, out: Act, tape, cin_act=None):
         h1 = self._u(seq[0], seq[1], cin_act=cin_act)
         OH, OW = h1.out_hw(x.H, x.W)
-        dev, dt = x.buf.device, self.dtype
-        t1 = Act(torch.empty((x.B, OH, OW, 256), dtype=dt, device=dev))
+        dev = x.buf.device
+        t1 = Act(self._empty((x.B, OH, OW, 256), dev))
         self.unit_fwd(h1, x, t1, tape, label="upconvT")
-        t2 = Act(torch.empty((x.B, OH, OW, 256), dtype=dt, device=dev))
+        t2 = Act(self._empty((x.B, OH, OW, 256), dev))
         self.unit_fwd(self._u(seq[3], seq[4]), t1, t2, tape, label="upconv")
         self.unit_fwd(self._u(seq[6], seq[7]), t2, out, tape, label="upconv")
 
@@ -769,29 +822,29 @@ class Engine:
             u2 = self._u(blk.conv2, blk.bn2)
             u3 = self._u(blk.conv3, blk.bn3)
             h1, w1 = u1.out_hw(x.H, x.W)
-            t1 = Act(torch.empty((x.B, h1, w1, u1.cout), dtype=dt, device=dev))
+            t1 = Act(self._empty((x.B, h1, w1, u1.cout), dev))
             self.unit_fwd(u1, x, t1, tape, label="enc")
             h2, w2 = u2.out_hw(h1, w1)
-            t2 = Act(torch.empty((x.B, h2, w2, u2.cout), dtype=dt, device=dev))
+            t2 = Act(self._empty((x.B, h2, w2, u2.cout), dev))
             self.unit_fwd(u2, t1, t2, tape, label="enc")
             last, mid = u3, t2
         else:
             u1 = self._u(blk.conv1, blk.bn1)
             h1, w1 = u1.out_hw(x.H, x.W)
-            t1 = Act(torch.empty((x.B, h1, w1, u1.cout), dtype=dt, device=dev))
+            t1 = Act(self._empty((x.B, h1, w1, u1.cout), dev))
             self.unit_fwd(u1, x, t1, tape, label="enc")
             last, mid = self._u(blk.conv2, blk.bn2, True), t1
         ds = blk.downsample
         if ds is not None and len(ds) > 0:
             ud = self._u(ds[0], ds[1], False)
             hd, wd = ud.out_hw(x.H, x.W)
-            res = Act(torch.empty((x.B, hd, wd, ud.cout), dtype=dt, device=dev))
+            res = Act(self._empty((x.B, hd, wd, ud.cout), dev))
             self.unit_fwd(ud, x, res, tape, label="enc_ds")
         else:
             res = x
         if out is None:
             oh, ow = last.out_hw(mid.H, mid.W)
-            out = Act(torch.empty((x.B, oh, ow, last.cout), dtype=dt, device=dev))
+            out = Act(self._empty((x.B, oh, ow, last.cout), dev))
         self.unit_fwd(last, mid, out, tape, res=res, label="enc")
         return out
 

@@ -19,7 +19,13 @@ import torch
 
 
 def _engines(net):
-    return [m._engine for m in net.modules() if hasattr(m, "_engine")]
+    out = []
+    for m in net.modules():
+        for name in ("_engine", "_engine_x3"):
+            e = getattr(m, name, None)
+            if e is not None:
+                out.append(e)
+    return out
 
 
 def _state_tensors(net):

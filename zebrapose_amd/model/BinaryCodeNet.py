@@ -7,8 +7,12 @@ and loss call signatures as the reference (BinaryCodeNet.py:8-174).  The forward
 backward run in libzp (HIP kernels for gfx950) through ``zebrapose_amd.engine``; there is
 no PyTorch-op fallback.
 
-Precision: ``precision='fp32'`` (default) computes every convolution with exact-f32 MFMA
-(``v_mfma_f32_16x16x4_f32``) and f32 activations -- the parity mode; ``precision='bf16'``
+Precision: ``precision='fp32'`` (default) is the reference's own arithmetic.  Training runs every
+convolution with exact-f32 MFMA (``v_mfma_f32_16x16x4_f32``) and f32 activations; the eval forward
+runs the split-fp32 engine (include/zp.h ZP_F32X3: activations and weights as three bf16 planes
+summing exactly to the f32 value, every product from its six leading terms on bf16 MFMAs, f32
+accumulation -- f32-accurate at 6/16 of the f32-MFMA cost).  ``f32_split=False`` (or
+``ZP_F32_SPLIT=0``) keeps the eval forward on exact-f32 MFMA too.  ``precision='bf16'``
 uses bf16 MFMA with f32 accumulation and bf16 NHWC activations -- the throughput mode
 (configs 2-4); ``precision='fp16'`` is the same with IEEE fp16 (``v_mfma_f32_16x16x32_f16``),
 inference only (configs[4]: R50 multi-object inference).  Set per instance (``net.set_precision``) or with ``ZP_PRECISION``.
@@ -207,9 +211,21 @@ class DeepLabV3(nn.Module):
             raise NotImplementedError("num_resnet_layers must be 34 or 50")
         prec = precision or os.environ.get("ZP_PRECISION", "fp32")
         object.__setattr__(self, "_engine", Engine(self, _PREC[prec]))
+        object.__setattr__(self, "_engine_x3", None)
+        self.f32_split = os.environ.get("ZP_F32_SPLIT", "1") != "0"
 
     def set_precision(self, precision):
         object.__setattr__(self, "_engine", Engine(self, _PREC[precision]))
+        object.__setattr__(self, "_engine_x3", None)
+
+    def eval_engine(self):
+        """The engine that runs this network's eval (inference) forward: the split-fp32 engine for
+        precision 'fp32' (unless f32_split is off), else the precision's own engine."""
+        if self._engine.dtype == torch.float32 and self.f32_split:
+            if self._engine_x3 is None:
+                object.__setattr__(self, "_engine_x3", Engine(self, torch.float32, x3=True))
+            return self._engine_x3
+        return self._engine
 
     @property
     def precision(self):
@@ -221,7 +237,8 @@ class DeepLabV3(nn.Module):
             if self._engine.dtype == torch.float16:
                 raise RuntimeError("precision='fp16' is inference-only (configs[4]); train in 'bf16' or 'fp32'")
             return _DeepLabFn.apply(self, x, *params)
-        mask, code, _ = self._engine.forward(x, train=self.training)
+        eng = self._engine if self.training else self.eval_engine()
+        mask, code, _ = eng.forward(x, train=self.training)
         return mask, code
 
 
