@@ -262,7 +262,9 @@ def test_train_step_fp32_matches_reference(net_and_state, golden):
             got = named[name].grad.cpu().numpy()[:8]
             ref = f[k]
             rel = np.linalg.norm(got - ref) / np.linalg.norm(ref)
-            budget = 0.01 if "aspp.conv_1x1_4" in name else 0.10
+            # the random-weight model's own noise floor: a 1e-6 relative input perturbation moves
+            # these gradients by 1-3% rel-L2 in the oracle
+            budget = 0.01 if "aspp.conv_1x1_4" in name else 0.05
             assert rel <= budget, (name, rel)
     sd2 = net.state_dict()
     for k in f:

@@ -27,8 +27,10 @@ def _free_port():
 def _worker(port, mode, q):
     os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
                       ZP_QUIET="1")
-    if mode == "torch_ddp":
+    if mode in ("torch_ddp", "torch_ddp_staged"):
         os.environ["ZP_TORCH_DDP"] = "1"
+    if mode == "torch_ddp_staged":  # zebrapose_amd.staged (automatic at world size > 1)
+        os.environ["ZP_STAGED_BACKWARD"] = "1"
     try:
         torch.cuda.set_device(0)
         dev = torch.device("cuda", 0)
@@ -70,11 +72,23 @@ def _worker(port, mode, q):
             ts.buckets.timing = []
         else:
             assert ts.buckets is None and isinstance(ts.net, torch.nn.parallel.DistributedDataParallel)
+        # when each parameter's gradient reached autograd (its AccumulateGrad / DDP hook): the share
+        # of the engine's reverse pass enqueued by then
+        eng = net.net._engine
+        seen = {}
+        def hook_for(n):
+            def hook(t):
+                seen.setdefault(n, getattr(eng, "bwd_progress", (0, 1)))
+            return hook
+        hooks = [p.register_post_accumulate_grad_hook(hook_for(n)) for n, p in net.named_parameters()]
         bc0 = calls["bcast"]
         ts(x, gt, gm)
         torch.cuda.synchronize()
+        for h in hooks:
+            h.remove()
         diffs = {n: int((p.grad != local[n]).sum().item()) for n, p in net.named_parameters()}
-        res = {"mode": mode, "diffs": diffs, "bcast": calls["bcast"] - bc0, "nparams": len(local)}
+        res = {"mode": mode, "diffs": diffs, "bcast": calls["bcast"] - bc0, "nparams": len(local),
+               "hook_progress": {n: list(v) for n, v in seen.items()}}
         if mode == "buckets":
             res["nbuckets"] = len(ts.buckets.buckets)
             res["launched"] = len(works)
@@ -96,8 +110,11 @@ def _worker(port, mode, q):
             dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["buckets", "torch_ddp"])
+@pytest.mark.parametrize("mode", ["buckets", "torch_ddp", "torch_ddp_staged"])
 def test_rccl_world1_grad_exchange(gpu, mode):
+    """torch_ddp_staged: torch's DistributedDataParallel(net) -- the unchanged train_v6.py:259 line --
+    over the stage-by-stage autograd chain (zebrapose_amd.staged): the head's gradients must reach
+    DDP's hooks while most of the reverse pass is still to be enqueued, the stem's at its end."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     p = ctx.Process(target=_worker, args=(_free_port(), mode, q))
@@ -111,6 +128,17 @@ def test_rccl_world1_grad_exchange(gpu, mode):
     bad = {n: d for n, d in res["diffs"].items() if d}
     assert not bad, f"averaged gradients differ from the local ones: {bad}"
     assert res["nparams"] == 152
+    hp = res["hook_progress"]
+    assert len(hp) == 152
+    if mode == "torch_ddp_staged":
+        done, total = hp["net.aspp.conv_1x1_4.weight"]
+        assert done < total / 4, (done, total)  # head gradients handed over early
+        done, total = hp["net.resnet.layer5.2.conv2.weight"]
+        assert done < total / 2, (done, total)
+        done, total = hp["net.resnet.resnet.0.weight"]
+        assert done == total
+    elif mode == "torch_ddp":  # one autograd node: every hook after the whole reverse pass
+        assert all(d == t for d, t in hp.values())
     if mode == "buckets":
         assert res["nbuckets"] >= 4  # 116 MB of f32 gradients in ~25 MB buckets
         assert res["launched"] == res["nbuckets"] == res["completed"]

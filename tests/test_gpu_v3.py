@@ -114,7 +114,7 @@ def test_v3_train_step_fp32_matches_reference(golden):
             got = named[name].grad.cpu().numpy()[:8]
             ref = f[k]
             rel = np.linalg.norm(got - ref) / np.linalg.norm(ref)
-            budget = 0.01 if name.endswith("conv_1x1_4.weight") or name.endswith("conv_1x1_4.bias") else 0.10
+            budget = 0.01 if name.endswith("conv_1x1_4.weight") or name.endswith("conv_1x1_4.bias") else 0.05
             print(f"v3 grad {name}: rel-L2 {rel:.3g}")
             assert rel <= budget, (name, rel)
 

@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""Split-fp32 conv (k_conv3) layer timing under several schedule flag sets, one process, interleaved
+rounds (same-box A/B):  python tools/conv3_ab.py [--flags 478,470,...] [--layers ...]
+Layers: the network's heaviest split-fp32 launches at bs=32.  Algorithmic TFLOP/s are f32 FLOPs
+(2 * pixels * taps * Cin * Cout); the ceiling is 2516.6 / 6 = 419 TFLOP/s."""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ.setdefault("ZP_QUIET", "1")
+
+LAYERS = {  # name: (kind, cin, cout, k, d, hw)
+    "up2conv": ("conv", 256, 256, 3, 1, 128),
+    "l5": ("conv", 512, 512, 3, 4, 32),
+    "up2T": ("convT", 320, 256, 3, 1, 64),
+    "up1conv": ("conv", 256, 256, 3, 1, 64),
+    "l1": ("conv", 64, 64, 3, 1, 64),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--flags", default="478")
+    ap.add_argument("--layers", default="up2conv,l5,up2T")
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--rounds", type=int, default=3)
+    a = ap.parse_args()
+    from zebrapose_amd import _lib as L
+    from zebrapose_amd.engine import Engine, Unit, Act
+    from zebrapose_amd.model import layers as LY
+    dev = torch.device("cuda", 0)
+    flags = [int(f) for f in a.flags.split(",")]
+    res = {}
+    setups = []
+    for name in a.layers.split(","):
+        kind, cin, cout, k, d, hw = LAYERS[name]
+        if kind == "conv":
+            conv = LY.Conv2d(cin, cout, k, 1, d * (k // 2), d, bias=False).to(dev)
+        else:
+            conv = LY.ConvTranspose2d(cin, cout, 3, 2, 1, output_padding=1, bias=False).to(dev)
+        bn = LY.BatchNorm2d(cout).to(dev).eval()
+        unit = Unit(conv, bn, relu=True)
+        eng = Engine(torch.nn.Module(), torch.float32, x3=True)
+        xs = eng._empty((a.batch, hw, hw, cin), dev)
+        xs._base.copy_(torch.randn(3, a.batch, hw, hw, cin, device=dev).clamp(min=0).bfloat16())
+        OH, OW = unit.out_hw(hw, hw)
+        y = Act(eng._empty((a.batch, OH, OW, cout), dev))
+        taps = 9 if kind == "conv" else 9 / 4 * 4  # convT: 4 phases x 9/4 taps over the input grid
+        fl = 2.0 * a.batch * hw * hw * (9 if kind == "conv" else 9) * cin * cout
+        setups.append((name, eng, unit, Act(xs), y, fl))
+    for r in range(a.rounds):
+        for f in flags:
+            L.lib.zp_conv_tuning(1, f)
+            for name, eng, unit, x, y, fl in setups:
+                for _ in range(2):
+                    eng.unit_fwd(unit, x, y, None)
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(a.iters):
+                    eng.unit_fwd(unit, x, y, None)
+                e1.record()
+                torch.cuda.synchronize()
+                us = e0.elapsed_time(e1) * 1e3 / a.iters
+                res.setdefault((name, f), []).append(us)
+    L.lib.zp_conv_tuning(1, -1)
+    for (name, f), v in sorted(res.items()):
+        fl = [s[5] for s in setups if s[0] == name][0]
+        us = min(v)
+        print(f"{name:8s} flags {f:6d}: {us:9.1f} us  {fl / us * 1e-6:7.1f} TFLOP/s  ({fl / us * 1e-6 / 419.43:.3f} of x3 peak)")
+
+
+if __name__ == "__main__":
+    main()

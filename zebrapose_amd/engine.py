@@ -854,8 +854,24 @@ class Engine:
         resamplings add their gradient into the visible-mask head's before it runs.  ``grads`` is
         the dict the gradients are assigned into as they are enqueued (parallel.grads_sink: a
         data-parallel run starts each bucket's all-reduce from those assignments)."""
+        grads = {} if grads is None else grads
+        for _ in self.backward_iter(tape, dmask, dcode, dentire, grads):
+            pass
+        return grads
+
+    def side_join_current(self):
+        """Make the current stream wait for the weight-gradient side stream (stage boundaries of
+        the staged backward, zebrapose_amd.staged)."""
+        if self._side is not None and self._side_used:
+            torch.cuda.current_stream(self._side.device).wait_stream(self._side)
+            self._side_used = False
+
+    def backward_iter(self, tape, dmask, dcode, dentire=None, grads=None):
+        """Engine.backward as a generator: yields after each taped op's backward has been enqueued
+        (the staged autograd chain of zebrapose_amd.staged advances it stage by stage)."""
         gmap = {}
         grads = {} if grads is None else grads
+        self.bwd_progress = (0, len(tape.recs))  # taped ops whose backward is enqueued / all
         st = L.stream_ptr()
         head_rec = next(r for r in tape.recs if r[0] == "head" and r[3] == "head")
         hin = head_rec[2]
@@ -932,6 +948,7 @@ class Engine:
                        xa.H, xa.W, gx.ld, gx.c0, 1, st)
                 if self.bwd_trace is not None:
                     self.bwd_trace.append({"kind": "avgpool", "gp": gp, "gx": (before, self._snap(gx))})
+            self.bwd_progress = (self.bwd_progress[0] + 1, len(tape.recs))
+            yield rec
         self._side_join(dev)
-        return grads
 

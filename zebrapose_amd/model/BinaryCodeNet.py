@@ -25,6 +25,7 @@ import torch
 import torch.nn as nn
 
 from .. import _lib as L
+from .. import staged as _staged
 from ..engine import Engine
 from ..parallel import finish_grads, grads_sink
 from .aspp import ASPP, ASPP_50
@@ -236,6 +237,9 @@ class DeepLabV3(nn.Module):
         if self.training and torch.is_grad_enabled() and any(p.requires_grad for p in params):
             if self._engine.dtype == torch.float16:
                 raise RuntimeError("precision='fp16' is inference-only (configs[4]); train in 'bf16' or 'fp32'")
+            if _staged.enabled(self):  # torch DDP over the unchanged DistributedDataParallel(net) line
+                mask, code, tape = self._engine.forward(x, train=True)
+                return _staged.staged(self, self._engine, (mask, code), tape)
             return _DeepLabFn.apply(self, x, *params)
         eng = self._engine if self.training else self.eval_engine()
         mask, code, _ = eng.forward(x, train=self.training)

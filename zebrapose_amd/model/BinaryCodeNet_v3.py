@@ -21,6 +21,7 @@ from .BinaryCodeNet import _PREC, BinaryCodeLoss, MaskLoss  # noqa: F401  (train
 from .aspp import ASPP
 from .aspp_v3 import ASPP_v3
 from .resnet import ResNet34_OS8
+from .. import staged as _staged
 from ..engine import Engine
 from ..parallel import finish_grads, grads_sink
 
@@ -67,6 +68,9 @@ class DeepLabV3(nn.Module):
         if self.training and torch.is_grad_enabled() and any(p.requires_grad for p in params):
             if self._engine.dtype == torch.float16:
                 raise RuntimeError("precision='fp16' is inference-only; train in 'bf16' or 'fp32'")
+            if _staged.enabled(self):  # torch DDP over the unchanged DistributedDataParallel(net) line
+                mask, entire, code, tape = self._engine.forward_v3(x, train=True)
+                return _staged.staged(self, self._engine, (mask, entire, code), tape)
             return _DeepLabV3Fn.apply(self, x, *params)
         mask, entire, code, _ = self._engine.forward_v3(x, train=self.training)
         return mask, entire, code
