@@ -50,7 +50,7 @@ PEAK_X3 = PEAK["bf16"] / 6.0
 
 def peak_of(kname, precision):
     """(peak TFLOP/s, basis) for the dominant kernel instance."""
-    if kname.startswith("k_conv3"):
+    if kname.startswith("k_conv3"):  # k_conv3 / k_conv3s
         return PEAK_X3, ("split-fp32 kernel: dense bf16 MFMA peak 2516.6 / 6 bf16 products per f32 MAC "
                          "(f32 MFMA peak 157.3)")
     if "<f32" in kname:

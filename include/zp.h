@@ -121,15 +121,17 @@ int zp_conv2d_stat_parts(const zp_conv_args* a);
 /* launch configuration zp_conv2d picks: cout tile, pixel tile, LDS ring depth, kernel variant
  * (0 = k_conv, 1 = k_conv_strip: 3x3 stride-1 convs with activation-strip reuse, 2 = k_conv_strip2:
  * the same with the lean main loop, 3 = k_conv_quad: the four phases of a stride-2 transposed
- * structure in one tile, 4 = k_conv3: the split-fp32 (ZP_F32X3) kernel) */
+ * structure in one tile, 4 = k_conv3: the split-fp32 (ZP_F32X3) kernel, 5 = k_conv3s: its 3x3
+ * stride-1 form with activation-strip reuse) */
 int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* stages, int* variant);
 /* runtime tuning knobs (tests / sweeps): key 0 = minimum workgroup count for the 256-channel
  * tile (default 1024); key 1 = conv schedule flags (-1 = ZP_CONV_FLAGS or the default); key 2 =
  * 64-channel layers on the strip kernel (default 1); key 3 = the lean weight-gradient kernel
  * (default 1); key 4 = its workgroup rounds over the CUs (default 1); key 5 = the general
  * weight-gradient kernel's workgroup rounds (default 1; 0 = a ~1024-workgroup target); key 6 = the
- * fewest workgroups the four-phase kernel (k_conv_quad) runs with (default 256).  Returns the
- * previous value, -1 for an unknown key. */
+ * fewest workgroups the four-phase kernel (k_conv_quad) runs with (default 256); key 7 = the
+ * split-fp32 strip kernel k_conv3s (0 off, 1 64-channel tiles, 2 also 128-channel tiles; -1 =
+ * ZP_CONV3_STRIP or the default 1).  Returns the previous value, -1 for an unknown key. */
 int zp_conv_tuning(int key, int value);
 
 /* Pack an f32 weight tensor src[d0][d1][kh][kw] into dst[rows_pad][k_pad] (dtype), taps

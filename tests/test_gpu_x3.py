@@ -80,8 +80,44 @@ def test_split_weight_pack_is_exact(gpu):
     assert torch.equal(out[0], ref.to(torch.bfloat16))
 
 
-@pytest.mark.parametrize("geom", GEOMS, ids=[f"{g[0]}{g[1]}-{g[2]}k{g[3]}s{g[4]}d{g[6]}h{g[8]}" for g in GEOMS])
+# 3x3 stride-1 geometries the strip kernel k_conv3s takes (W 32 / 64 / 128, 256-pixel whole-row
+# tiles; dilation up to a 288-row strip), run under strip modes 0 (k_conv3), 1 (64-channel tiles
+# on k_conv3s<2>) and 2 (128-channel tiles on k_conv3s<4> too)
+STRIP_GEOMS = [
+    ("conv", 64, 64, 3, 1, 1, 1, False, 64),
+    ("conv", 64, 64, 3, 1, 2, 2, False, 32),
+    ("conv", 128, 128, 3, 1, 1, 1, False, 64),
+    ("conv", 256, 256, 3, 1, 1, 1, False, 128),
+    ("conv", 128, 256, 3, 1, 2, 2, False, 64),
+]
+
+
+def _gid(g):
+    return f"{g[0]}{g[1]}-{g[2]}k{g[3]}s{g[4]}d{g[6]}h{g[8]}"
+
+
+@pytest.mark.parametrize("geom", GEOMS, ids=[_gid(g) for g in GEOMS])
 def test_split_conv_is_f32_accurate(gpu, geom):
+    _check_geom(gpu, geom)
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("geom", STRIP_GEOMS, ids=[_gid(g) for g in STRIP_GEOMS])
+def test_split_strip_kernel(gpu, geom, mode):
+    from zebrapose_amd import _lib as L
+    old = L.lib.zp_conv_tuning(7, mode)
+    try:
+        variant = _check_geom(gpu, geom)
+    finally:
+        L.lib.zp_conv_tuning(7, old)
+    cout, H = geom[2], geom[8]
+    tc = 128 if cout > 64 else 64
+    strip = (mode == 2 or (mode == 1 and tc == 64)) and H * H >= 256
+    assert variant == (5 if strip else 4), (variant, mode)
+
+
+def _check_geom(gpu, geom):
+    """Split vs exact-f32-MFMA error against float64; returns the launch variant (zp_conv2d_config)."""
     from zebrapose_amd import _lib as L
     from zebrapose_amd.engine import Engine, Unit, Act, joined
     from zebrapose_amd.model import layers as LY
@@ -119,9 +155,13 @@ def test_split_conv_is_f32_accurate(gpu, geom):
             xa = Act(xh.to(gpu))
             ra = None if rh is None else Act(rh.to(gpu))
             oa = Act(torch.empty(B, OH, OW, cout, device=gpu))
+        eng.stage_log = []  # (stage, kernel label, ...) per launch
         eng.unit_fwd(unit, xa, oa, None, res=ra)
         torch.cuda.synchronize()
         out[mode] = joined(oa.buf).permute(0, 3, 1, 2).double().cpu()
+        if mode == "x3":
+            names = [r[1] for r in eng.stage_log]
+            variant = 5 if all(n.startswith("k_conv3s<") for n in names) else 4
     scale = ref.abs().max().item()
     e3 = (out["x3"] - ref).abs().max().item()
     e32 = (out["f32"] - ref).abs().max().item()
@@ -129,6 +169,7 @@ def test_split_conv_is_f32_accurate(gpu, geom):
     r32 = (out["f32"] - ref).pow(2).mean().sqrt().item()
     print(f"{geom}: max|d| split {e3:.3g} f32-MFMA {e32:.3g}; rms split {r3:.3g} f32-MFMA {r32:.3g} (scale {scale:.3g})")
     assert e3 <= 2.0 * e32 + 2.0 ** -24 * scale, (e3, e32, scale)
+    return variant
 
 
 def test_split_head_nchw(gpu):

@@ -35,9 +35,12 @@ def bench_label(name):
     m = re.search(r"k_conv_strip2<(unsigned short|_Float16), (\d+), (\d+), (true|false|\d+)>", name)
     if m:
         return f"k_conv_strip2<{tn[m.group(1)]},WC={m.group(2)}>"
-    m = re.search(r"k_conv3<(\d+), (\d+)>", name)
+    m = re.search(r"k_conv3s<(\d+)>", name)
     if m:
-        return f"k_conv3<WC={m.group(1)},NWP={m.group(2)}>"
+        return f"k_conv3s<WC={m.group(1)}>"
+    m = re.search(r"k_conv3<(\d+), (\d+), (\d+), (\d+), (true|false)>", name)
+    if m:
+        return f"k_conv3<WC={m.group(1)},NWP={m.group(3)}>"
     m = re.search(r"k_conv_quad<(unsigned short|_Float16), (\d+), (true|false)>", name)
     if m:
         return f"k_conv_quad<{tn[m.group(1)]},W={m.group(2)}>"

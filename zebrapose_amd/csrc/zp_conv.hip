@@ -23,89 +23,13 @@
 #define ZP_ABL 0
 #endif
 
+#include "zp_conv_kern.h"
+#include "zp_conv3.h"
+
 namespace zp {
-
-template <typename T> struct MfmaTraits;
-template <> struct MfmaTraits<bf16_t> {
-  static constexpr int E = 8;  // elements per 16 B chunk
-  static __device__ __forceinline__ void mma(f32x4& acc, const uint4& a, const uint4& b) {
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b),
-                                                  acc, 0, 0, 0);
-  }
-};
-template <> struct MfmaTraits<f16_t> {
-  static constexpr int E = 8;
-  static __device__ __forceinline__ void mma(f32x4& acc, const uint4& a, const uint4& b) {
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b),
-                                                 acc, 0, 0, 0);
-  }
-};
-template <> struct MfmaTraits<float> {
-  static constexpr int E = 4;
-  // 16 B chunk = 4 consecutive k of one row; element e is k-substep e for every lane
-  // group, so the four 16x16x4 MFMAs together cover all 16 k of the 4 lane groups.
-  static __device__ __forceinline__ void mma(f32x4& acc, const uint4& a, const uint4& b) {
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.x), __uint_as_float(b.x), acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.y), __uint_as_float(b.y), acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.z), __uint_as_float(b.z), acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.w), __uint_as_float(b.w), acc, 0, 0, 0);
-  }
-};
-
-__device__ __forceinline__ int swz(int row, int chunk) { return row * 8 + (chunk ^ (row & 7)); }
 
 // all-zero source for out-of-image / padding taps of the direct-to-LDS loads
 __device__ uint4 g_zero_page[8];
-
-// s_waitcnt vmcnt(N) only (LDS-DMA loads count on vmcnt); "memory" keeps LDS accesses in place
-template <int N>
-__device__ __forceinline__ void vm_wait() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-// Per-launch tap grids, derived on the host from the subs' tap lists (every plan of
-// geometry.py enumerates taps as a (tap row) x (tap column) grid, rows outer:
-// ty = ty0 + q * dty, tx = tx0 + r * dtx for tap q * nx + r), plus the byte extents of the
-// activation / weight buffers for the buffer-load range check.
-struct conv_taps {
-  int ny[ZP_MAX_SUB], nx[ZP_MAX_SUB], ty0[ZP_MAX_SUB], dty[ZP_MAX_SUB], tx0[ZP_MAX_SUB], dtx[ZP_MAX_SUB];
-  unsigned x_bytes, w_bytes[ZP_MAX_SUB];
-};
-
-// LDS byte address of a __shared__ pointer
-__device__ __forceinline__ unsigned lds_addr(const void* p) {
-  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
-}
-
-// ds_read_b128 with an immediate offset; the caller waits lgkmcnt itself
-template <int OFF>
-__device__ __forceinline__ uint4 ds_read16(unsigned addr) {
-  static_assert(OFF >= 0 && OFF < 65536, "ds offset range");
-  uint4 r;
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF) : "memory");
-  return r;
-}
-
-template <int N, typename F, int I = 0>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (I < N) {
-    f(std::integral_constant<int, I>{});
-    static_for<N, F, I + 1>(static_cast<F&&>(f));
-  }
-}
-
-// Sum over the 16 lanes of each DPP row (lanes 16k .. 16k + 15), the total in every lane of the row:
-// quad_perm xor 1, xor 2, then row_half_mirror and row_mirror -- the same pairing tree as
-// __shfl_xor over 1, 2, 4, 8 (bit-identical sums) as four DPP adds instead of four ds_bpermute
-// round trips through the LDS crossbar.
-__device__ __forceinline__ float row16_sum(float v) {
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));  // row_half_mirror
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false));  // row_mirror
-  return v;
-}
 
 // Conv epilogue shared by k_conv and k_conv_strip: BN scale/shift (+bias), residual, ReLU,
 // NHWC (channel slice) / NCHW-head / f32 stores, or train-mode BN partial statistics.
@@ -2277,505 +2201,6 @@ __global__ void k_wgrad_reduce(const zp_wgrad_args A, const float* __restrict__ 
   }
 }
 
-// k_conv3 epilogue: BN scale / shift (+ bias), split residual, ReLU, then split NHWC stores (3
-// planes) or the f32 NCHW head split.  acc[i][j] = 4 consecutive output channels x one pixel.
-template <int WC, int WP>
-__device__ __forceinline__ void conv3_epilogue(const zp_conv_args& A, const zp_conv_sub& S, f32x4 (&acc)[WC][WP],
-                                               const int p0, const int c0, const int wc, const int wp,
-                                               const int lane, const int M, const int GHW, const int flags) {
-  const int lr = lane & 15;
-  int pn[WP], poy[WP], pox[WP];
-  bool pok[WP];
-#pragma unroll
-  for (int j = 0; j < WP; ++j) {
-    const int p = p0 + wp * 16 * WP + j * 16 + lr;
-    pok[j] = p < M;
-    const int pp = pok[j] ? p : 0;
-    const int n = pp / GHW, rr = pp - n * GHW;
-    const int gy = rr / A.GW, gx = rr - gy * A.GW;
-    pn[j] = n;
-    poy[j] = gy * S.oys + S.oyo;
-    pox[j] = gx * S.oxs + S.oxo;
-  }
-  const long psy = (long)A.N * S.OH * S.OW * S.ldy;
-  const long psr = (long)A.N * S.OH * S.OW * A.ldr;
-  const int cbase = c0 + wc * 16 * WC + (lane >> 4) * 4;
-#pragma unroll
-  for (int i = 0; i < WC; ++i) {
-    const int cf = cbase + i * 16;
-    if (cf >= A.Cout) continue;
-    const bool full = cf + 3 < A.Cout;
-    float sc[4], sh[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      sc[r] = (S.scale && cf + r < A.Cout) ? S.scale[cf + r] : 1.f;
-      sh[r] = (S.shift && cf + r < A.Cout) ? S.shift[cf + r] : 0.f;
-    }
-#pragma unroll
-    for (int j = 0; j < WP; ++j) {
-      if (!pok[j]) continue;
-      const size_t pix = ((size_t)pn[j] * S.OH + poy[j]) * S.OW + pox[j];
-      float v[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * sc[r] + sh[r];
-      if (A.res) {
-        const bf16_t* R = (const bf16_t*)A.res + pix * A.ldr + A.cr0 + cf;
-        if (full) {
-          const uint2 h = *(const uint2*)R, m = *(const uint2*)(R + psr), l = *(const uint2*)(R + 2 * psr);
-          const uint32_t hw[2] = {h.x, h.y}, mw[2] = {m.x, m.y}, lw[2] = {l.x, l.y};
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int sft = (r & 1) * 16;
-            v[r] += join3((bf16_t)(hw[r >> 1] >> sft), (bf16_t)(mw[r >> 1] >> sft), (bf16_t)(lw[r >> 1] >> sft));
-          }
-        } else {
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (cf + r < A.Cout) v[r] += join3(R[r], R[r + psr], R[r + 2 * psr]);
-        }
-      }
-      if (A.relu) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
-      }
-      if (A.out_mode == ZP_OUT_HEAD_NCHW) {
-        const size_t plane = (size_t)S.OH * S.OW;
-        const size_t sp = (size_t)poy[j] * S.OW + pox[j];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int c = cf + r;
-          if (c >= A.Cout) continue;
-          if (c == 0) ((float*)S.y)[(size_t)pn[j] * plane + sp] = v[r];
-          else ((float*)S.y2)[((size_t)pn[j] * (A.Cout - 1) + (c - 1)) * plane + sp] = v[r];
-        }
-        continue;
-      }
-      bf16_t h[4], m[4], l[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) split3(v[r], h[r], m[r], l[r]);
-      if ((flags & 16384) && v[0] != 1.f) continue;  // diagnostic: no stores (unless a value is exactly 1)
-      bf16_t* Y = (bf16_t*)S.y + pix * S.ldy + S.cy0 + cf;
-      if (full) {
-        *(uint2*)Y = make_uint2((uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16));
-        *(uint2*)(Y + psy) = make_uint2((uint32_t)m[0] | ((uint32_t)m[1] << 16), (uint32_t)m[2] | ((uint32_t)m[3] << 16));
-        *(uint2*)(Y + 2 * psy) =
-            make_uint2((uint32_t)l[0] | ((uint32_t)l[1] << 16), (uint32_t)l[2] | ((uint32_t)l[3] << 16));
-      } else {
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (cf + r < A.Cout) {
-            Y[r] = h[r];
-            Y[r + psy] = m[r];
-            Y[r + 2 * psy] = l[r];
-          }
-      }
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------------
-// k_conv3: forward convolution on ZP_F32X3 operands (split fp32, zp.h): activations, packed weights
-// and the residual are three bf16 planes (hi, mid, lo) whose sum is the f32 value exactly.  Every
-// product a * b is formed from its six terms of magnitude >= 2^-16 |a b|:
-//   hi*hi + hi*mid + mid*hi + hi*lo + mid*mid + lo*hi
-// on v_mfma_f32_16x16x32_bf16 (f32 accumulate); the dropped terms (mid*lo, lo*mid, lo*lo) are below
-// 2^-23 |a b|, the order of f32's own product rounding.  That is f32-accurate arithmetic at 6 bf16
-// MFMAs per 16x16x32 product block = 6/16 of the v_mfma_f32_16x16x4_f32 cost, and -- since the three
-// B planes are staged once and each fragment feeds 3 / 2 / 1 MFMAs -- half the LDS traffic per MFMA
-// of the bf16 kernels.
-// Two accumulators per tile: hi*hi products in acc, the five correction terms in acc2, added once at
-// the end.  Measured (tools/x3_accuracy.py, R34 bs=32): with the correction sums added straight into
-// the full-size accumulator every conv carried a systematic NEGATIVE bias of ~-1e-7 relative (the
-// bf16 MFMA's internal alignment drops the low bits of addends far below the accumulator), which
-// compounded to 3x the exact-f32 engine's end-to-end error; accumulated among themselves the
-// correction terms keep their bits.
-// Tile: 2 NWP waves = 2 (cout) x NWP (pixel) computing TC = 32 WC output channels x TP = 64 NWP
-// pixels.  A K step is one tap x 32 input channels.  Staging: per plane, a 16-row x 32-element tile
-// (1 KB) is ONE buffer_load ... lds of 64 lanes, lane l fetching (row l & 15, 8 elements at k (l >>
-// 4) * 8): the LDS image is in MFMA fragment order, so every fragment read is a lane-linear
-// conflict-free ds_read_b128.  ST-deep ring; the tap walk (scalar), validity masks and out-of-image
-// zeros (offset past the buffer end) follow k_conv.
-// Schedules:
-//   PIPE = false (8 waves, 2 per SIMD): per step [next DMA][fragment reads][MFMAs][wait + barrier];
-//     ping-pong (flags & 8): waves 4-7 run one barrier behind, so on each SIMD one wave's MFMAs
-//     overlap its partner's reads.
-//   PIPE = true (NWP = 2: 4 waves, one per SIMD, 512-register budget): the fragments of step k + 1
-//     are read into a second register set while step k's MFMAs run, and the DMA runs ST steps
-//     ahead; per step one counted vmcnt wait + one barrier, no LDS read on the MFMA critical path.
-// ------------------------------------------------------------------------------------
-template <int WC, int WP, int NWP, int ST, bool PIPE>
-__global__ void __launch_bounds__(128 * NWP) k_conv3(const zp_conv_args A, const conv_taps TG, const int flags) {
-  constexpr int TC = 32 * WC, TP = 16 * WP * NWP, NW = 2 * NWP;
-  constexpr int NTW = TC / 16, NT = (TC + TP) / 16;  // weight tiles / all tiles (16 rows) per plane
-  constexpr int UNITS = 3 * NT;                      // (plane, tile) DMA units per stage
-  constexpr int TPW = (NT + NW - 1) / NW;            // tiles per wave (some waves idle in the last)
-  constexpr int GRP = 3 * TPW;                       // DMA instructions per wave per stage
-  static_assert(ST == 2 || ST == 3, "ring depth");
-  static_assert(ST == 2 || NT % NW == 0, "counted vmcnt waits need the same DMA count on every wave");
-  static_assert(!PIPE || NW == 4, "the register-pipelined schedule runs one wave per SIMD");
-  static_assert(WP == 4 || WP == 8, "pixel fragments per wave");
-  __shared__ uint4 lds[ST * UNITS * 64];
-  static_assert(ST * UNITS * 1024 <= 160 * 1024, "LDS");
-  static_assert((2 * NT + WC + 3) * 1024 < 65536, "ds_read immediate range");
-  const zp_conv_sub& S = A.sub[blockIdx.z];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wc = wid / NWP, wp = wid % NWP;
-  const int GHW = A.GH * A.GW;
-  const int M = A.N * GHW;
-  int bx = blockIdx.x, by = blockIdx.y;
-  if (flags & 2) {  // XCD-aware order (k_conv): the cout tiles of a pixel tile meet in one L2
-    const int total = gridDim.x * gridDim.y;
-    const int bid = blockIdx.x + gridDim.x * blockIdx.y;
-    const int lin = (total & 7) ? bid : (bid & 7) * (total >> 3) + (bid >> 3);
-    bx = lin / gridDim.y;
-    by = lin - bx * gridDim.y;
-  }
-  const int p0 = bx * TP, c0 = by * TC;
-  const int tb = blockIdx.z;
-  const int CB = A.Cin / 32;
-  const int ny = TG.ny[tb], nx = TG.nx[tb], dty = TG.dty[tb], dtx = TG.dtx[tb];
-  const int nK = S.ntaps * CB;
-  const int lr = lane & 15, lk = (lane >> 4) * 8;
-  // plane strides in bytes (scalar offsets of the DMA: the three planes of a tile share the lane's
-  // offset register)
-  const unsigned psx_b = (unsigned)((long)A.N * A.IH * A.IW * A.ldx * 2);
-  const unsigned psw_b = (unsigned)((long)A.w_rows * A.k_pad * 2);
-
-  // tiles of this wave: T = wid + NW k (all three planes each); wave-uniform kind, per-lane base
-  // offset (plane 0, bytes) and tap validity masks
-  unsigned ubase[TPW], uym[TPW], uxm[TPW];
-#pragma unroll
-  for (int k = 0; k < TPW; ++k) {
-    const int t = wid + NW * k;
-    ubase[k] = 0u;
-    uym[k] = uxm[k] = 0u;
-    if (t >= NT) continue;
-    if (t < NTW) {
-      ubase[k] = (unsigned)(((long)(c0 + t * 16 + lr) * A.k_pad + lk) * 2);
-    } else {
-      const int m = p0 + (t - NTW) * 16 + lr;
-      const bool ok = m < M;
-      const int mm = ok ? m : 0;
-      const int n = mm / GHW, rr = mm - n * GHW;
-      const int gy = rr / A.GW, gx = rr - gy * A.GW;
-      const int y0 = gy * A.sy, x0 = gx * A.sx;
-      ubase[k] = (unsigned)(((((long)n * A.IH + y0) * A.IW + x0) * A.ldx + A.cx0 + lk) * 2);
-      unsigned ym = 0, xm = 0;
-      for (int q = 0; q < ny; ++q) ym |= (unsigned)((unsigned)(y0 + TG.ty0[tb] + q * dty) < (unsigned)A.IH) << q;
-      for (int q = 0; q < nx; ++q) xm |= (unsigned)((unsigned)(x0 + TG.tx0[tb] + q * dtx) < (unsigned)A.IW) << q;
-      uym[k] = ok ? ym : 0u;
-      uxm[k] = xm;
-    }
-  }
-#if defined(__HIP_DEVICE_COMPILE__)
-  const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)A.x, (short)0, (int)TG.x_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)S.w, (short)0, (int)TG.w_bytes[tb], 0x00020000);
-#endif
-  // scalar walk of the next step to issue.  K order: 32-channel chunk OUTER, taps inner -- the taps
-  // of one chunk read nearly the same input rows (shifted by the tap offsets), so all but the
-  // first come from L2; with the taps outer (k_conv's order) each tap's sweep over every chunk of
-  // a tile evicted the rows before the next tap came back to them, and the staging ran at the
-  // Infinity-Cache / HBM rate.  act_off = ((ty * IW + tx) * ldx + cb * 32) * 2; the weight offset
-  // of (tap t, chunk cb) in the packed row (k = t * Cin + c) is w_koff = (t * Cin + cb * 32) * 2.
-  int w_tyi = 0, w_txi = 0, w_cb = 0, w_t = 0;
-  int act_off = ((TG.ty0[tb] * A.IW + TG.tx0[tb]) * A.ldx) * 2;
-  int w_koff = 0;
-  const int step_x = dtx * A.ldx * 2, step_y = dty * A.IW * A.ldx * 2;
-  const int cin2 = A.Cin * 2;
-  // diagnostic ablation flags (timing only, wrong results): 4096 no DMA after the prologue, 8192 no
-  // MFMA, 16384 no epilogue stores
-  const bool abl_dma = flags & 4096, abl_mfma = flags & 8192;
-  auto issue = [&](int ks, int stage) {
-    unsigned voff[TPW];
-#pragma unroll
-    for (int k = 0; k < TPW; ++k) {
-      const bool w = wid + NW * k < NTW;
-      const bool ok = (uym[k] >> w_tyi) & (uxm[k] >> w_txi) & 1u;
-      voff[k] = w ? ubase[k] : (ok ? ubase[k] + (unsigned)act_off : 0x80000000u);
-    }
-#if defined(__HIP_DEVICE_COMPILE__)
-#pragma unroll
-    for (int k = 0; k < TPW; ++k) {
-      const int t = wid + NW * k;
-      if (t >= NT) continue;
-#pragma unroll
-      for (int pl = 0; pl < 3; ++pl) {
-        auto* d = (__attribute__((address_space(3))) void*)&lds[(stage * UNITS + pl * NT + t) * 64];
-        if (t < NTW) __builtin_amdgcn_raw_ptr_buffer_load_lds(wrsrc, d, 16, voff[k], pl * psw_b + w_koff, 0, 0);
-        else __builtin_amdgcn_raw_ptr_buffer_load_lds(xrsrc, d, 16, voff[k], pl * psx_b, 0, 0);
-      }
-    }
-#endif
-    (void)ks;
-    ++w_t;
-    w_koff += cin2;
-    act_off += step_x;
-    if (++w_txi == nx) {
-      w_txi = 0;
-      act_off += step_y - nx * step_x;
-      if (++w_tyi == ny) {
-        w_tyi = 0;
-        w_t = 0;
-        ++w_cb;
-        act_off += 64 - ny * step_y;
-        w_koff = w_cb * 64;
-      }
-    }
-  };
-
-  // PIPE: a full second accumulator for the correction terms (one wave per SIMD has the registers);
-  // otherwise each half of the pixel fragments gets a fresh correction accumulator per K step,
-  // added into acc by VALU adds (round-to-nearest, unbiased) right after its MFMAs
-  constexpr int A2C = PIPE ? WC : 1, A2P = PIPE ? WP : 1;
-  f32x4 acc[WC][WP], acc2[A2C][A2P];
-#pragma unroll
-  for (int i = 0; i < WC; ++i)
-#pragma unroll
-    for (int j = 0; j < WP; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int i = 0; i < A2C; ++i)
-#pragma unroll
-    for (int j = 0; j < A2P; ++j) acc2[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  const unsigned l0 = lds_addr(lds) + (unsigned)lane * 16u;
-  unsigned abase[ST], bbase[ST];
-#pragma unroll
-  for (int s = 0; s < ST; ++s) {
-    abase[s] = l0 + (unsigned)(s * UNITS + wc * WC) * 1024u;
-    bbase[s] = l0 + (unsigned)(s * UNITS + NTW + wp * WP) * 1024u;
-  }
-  // fragment reads: inline-asm ds_read_b128 (waited on explicitly) in the single-register-set
-  // schedule; plain LDS loads in the register-pipelined one, whose reads stay in flight across the
-  // MFMAs -- the compiler then tracks their lgkmcnt itself (an asm read's destination registers
-  // are "written" at issue for the compiler, which may copy them before the data lands)
-  const int awo = (wc * WC) * 64 + lane, bwo = (NTW + wp * WP) * 64 + lane;
-  auto read_a = [&](auto s_c, uint4 (&af)[3][WC]) {
-    constexpr int s = decltype(s_c)::value;
-    static_for<3>([&](auto p_c) {
-      constexpr int p = decltype(p_c)::value;
-      static_for<WC>([&](auto i) {
-        if constexpr (PIPE) af[p][i] = lds[(s * UNITS + p * NT + i) * 64 + awo];
-        else af[p][i] = ds_read16<(p * NT + i) * 1024>(abase[s]);
-      });
-    });
-  };
-  auto read_b = [&](auto s_c, auto j0_c, auto j1_c, uint4 (&bfr)[3][WP]) {  // pixel fragments [J0, J1)
-    constexpr int s = decltype(s_c)::value, J0 = decltype(j0_c)::value, J1 = decltype(j1_c)::value;
-    static_for<3>([&](auto p_c) {
-      constexpr int p = decltype(p_c)::value;
-      static_for<J1 - J0>([&](auto jj) {
-        if constexpr (PIPE) bfr[p][J0 + jj] = lds[(s * UNITS + p * NT + J0 + jj) * 64 + bwo];
-        else bfr[p][J0 + jj] = ds_read16<(p * NT + J0 + jj) * 1024>(bbase[s]);
-      });
-    });
-  };
-  using J0c = std::integral_constant<int, 0>;
-  using JHc = std::integral_constant<int, WP / 2>;
-  using JWc = std::integral_constant<int, WP>;
-  auto read_frags = [&](auto s_c, uint4 (&af)[3][WC], uint4 (&bfr)[3][WP]) {
-    read_a(s_c, af);
-    read_b(s_c, J0c{}, JWc{}, bfr);
-  };
-  auto mfmas_part = [&](auto j0_c, auto j1_c, const uint4 (&af)[3][WC], const uint4 (&bfr)[3][WP]) {
-    constexpr int J0 = decltype(j0_c)::value, J1 = decltype(j1_c)::value;
-    // terms: mid*mid, hi*lo, lo*hi, mid*hi, hi*mid -> acc2; hi*hi -> acc
-    constexpr int TA[6] = {1, 0, 2, 1, 0, 0}, TB[6] = {1, 2, 0, 0, 1, 0};
-    if (!abl_mfma && PIPE) {
-      static_for<6>([&](auto t_c) {
-        constexpr int t = decltype(t_c)::value;
-#pragma unroll
-        for (int i = 0; i < WC; ++i)
-#pragma unroll
-          for (int j = J0; j < J1; ++j) {
-            if constexpr (t < 5) MfmaTraits<bf16_t>::mma(acc2[PIPE ? i : 0][PIPE ? j : 0], af[TA[t]][i], bfr[TB[t]][j]);
-            else MfmaTraits<bf16_t>::mma(acc[i][j], af[TA[t]][i], bfr[TB[t]][j]);
-          }
-      });
-    } else if (!abl_mfma) {
-      // per half of the pixel fragments: corrections into a fresh c2, hi*hi into acc, then
-      // acc += c2 on the VALU
-      static_for<2>([&](auto h_c) {
-        constexpr int H0 = J0 + decltype(h_c)::value * ((J1 - J0) / 2), HN = (J1 - J0) / 2;
-        f32x4 c2[WC][HN];
-#pragma unroll
-        for (int i = 0; i < WC; ++i)
-#pragma unroll
-          for (int jj = 0; jj < HN; ++jj) c2[i][jj] = (f32x4){0.f, 0.f, 0.f, 0.f};
-        static_for<5>([&](auto t_c) {
-          constexpr int t = decltype(t_c)::value;
-#pragma unroll
-          for (int i = 0; i < WC; ++i)
-#pragma unroll
-            for (int jj = 0; jj < HN; ++jj) MfmaTraits<bf16_t>::mma(c2[i][jj], af[TA[t]][i], bfr[TB[t]][H0 + jj]);
-        });
-#pragma unroll
-        for (int i = 0; i < WC; ++i)
-#pragma unroll
-          for (int jj = 0; jj < HN; ++jj) MfmaTraits<bf16_t>::mma(acc[i][H0 + jj], af[0][i], bfr[0][H0 + jj]);
-#pragma unroll
-        for (int i = 0; i < WC; ++i)
-#pragma unroll
-          for (int jj = 0; jj < HN; ++jj) acc[i][H0 + jj] += c2[i][jj];
-      });
-    } else {
-#pragma unroll
-      for (int p = 0; p < 3; ++p)
-#pragma unroll
-        for (int i = 0; i < WC; ++i)
-#pragma unroll
-          for (int j = J0; j < J1; ++j) acc[i][j][0] += __uint_as_float(af[p][i].x ^ bfr[p][j].y);
-    }
-  };
-  auto mfmas = [&](const uint4 (&af)[3][WC], const uint4 (&bfr)[3][WP]) { mfmas_part(J0c{}, JWc{}, af, bfr); };
-
-  if constexpr (!PIPE) {
-    const bool pingpong = NW == 8 && (flags & 8);
-    // step ks reads buffer ks % ST; the DMA of step ks + ST - 1 is issued first into the buffer
-    // step ks - 1 read (all waves passed the barrier that ended step ks - 1)
-    auto step = [&](auto s_c, int ks) {
-      constexpr int s = decltype(s_c)::value;
-      const bool more = ks + ST - 1 < nK;
-      if (more && !abl_dma) issue(ks + ST - 1, (s + ST - 1) % ST);
-      uint4 af[3][WC], bfr[3][WP];
-      // WP = 8 (one wave per SIMD): the second half of the pixel fragments is read while the
-      // first half's MFMAs run
-      read_a(s_c, af);
-      if constexpr (WP == 8) read_b(s_c, J0c{}, JHc{}, bfr);
-      else read_b(s_c, J0c{}, JWc{}, bfr);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (WP == 8) read_b(s_c, JHc{}, JWc{}, bfr);
-      auto wait_next = [&]() {  // step ks + 1's DMA landed (the newest ST - 2 groups may remain)
-        if (more && !abl_dma) vm_wait<GRP * (ST - 2)>();
-        else vm_wait<0>();
-      };
-      if (pingpong) {
-        wait_next();
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if (flags & 4) __builtin_amdgcn_s_setprio(1);
-      if constexpr (WP == 8) {
-        mfmas_part(J0c{}, JHc{}, af, bfr);
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        mfmas_part(JHc{}, JWc{}, af, bfr);
-      } else {
-        mfmas(af, bfr);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      if (flags & 4) __builtin_amdgcn_s_setprio(0);
-      if (!pingpong) wait_next();
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-    };
-    using I0 = std::integral_constant<int, 0>;
-    using I1 = std::integral_constant<int, 1>;
-    using I2 = std::integral_constant<int, 2>;
-    issue(0, 0);
-    if (ST == 3 && nK > 1) {
-      issue(1, 1);
-      vm_wait<GRP>();
-    } else {
-      vm_wait<0>();
-    }
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (pingpong && wid >= 4) __builtin_amdgcn_s_barrier();
-    if constexpr (ST == 3) {
-      for (int ks = 0; ks < nK; ks += 3) {
-        step(I0{}, ks);
-        if (ks + 1 >= nK) break;
-        step(I1{}, ks + 1);
-        if (ks + 2 >= nK) break;
-        step(I2{}, ks + 2);
-      }
-    } else {
-      for (int ks = 0; ks < nK; ks += 2) {
-        step(I0{}, ks);
-        if (ks + 1 >= nK) break;
-        step(I1{}, ks + 1);
-      }
-    }
-    if (pingpong && wid < 4) __builtin_amdgcn_s_barrier();
-  } else {
-    // Prologue: the DMA of steps 0 .. ST - 1 (buffer = step), then step 0's fragments.  Step ks
-    // (fragments F[ks & 1] loaded): wait for them; wait for step ks + 1's DMA + barrier (buffer
-    // (ks + 1) % ST complete; every wave has read buffer ks % ST); issue the DMA of step ks + ST into
-    // buffer ks % ST; issue step ks + 1's fragment reads into F[(ks + 1) & 1]; run step ks's MFMAs.
-    // two named fragment sets (a [2][3][WC] array of them was demoted to scratch memory)
-    uint4 fa0[3][WC], fb0[3][WP], fa1[3][WC], fb1[3][WP];
-    int issued = 0;
-    for (int q = 0; q < ST; ++q)
-      if (q < nK) {
-        issue(q, q);
-        ++issued;
-      }
-    if (issued == ST) vm_wait<GRP * (ST - 1)>();
-    else vm_wait<0>();
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    using Z0 = std::integral_constant<int, 0>;
-    read_frags(Z0{}, fa0, fb0);
-    auto pstep = [&](auto s_c, int ks, uint4 (&ca)[3][WC], uint4 (&cb)[3][WP], uint4 (&na)[3][WC],
-                     uint4 (&nb)[3][WP]) {
-      constexpr int s = decltype(s_c)::value;
-      constexpr int sn = (s + 1) % ST;
-      // this wave's reads of buffer s (F[ks]) have landed before the barrier below releases the
-      // buffer to the next DMA
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      const bool next = ks + 1 < nK;
-      if (next) {
-        // outstanding DMA groups: steps ks + 1 .. min(ks + ST - 1, nK - 1); the newest
-        // ST - 2 of them may stay in flight when they all exist
-        if (ks + ST - 1 < nK && !abl_dma) vm_wait<GRP * (ST - 2)>();
-        else vm_wait<0>();
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-        read_frags(std::integral_constant<int, sn>{}, na, nb);
-        if (ks + ST < nK && !abl_dma) issue(ks + ST, s);
-      }
-      if (flags & 4) __builtin_amdgcn_s_setprio(1);
-      mfmas(ca, cb);
-      if (flags & 4) __builtin_amdgcn_s_setprio(0);
-    };
-    using S0 = std::integral_constant<int, 0>;
-    using S1 = std::integral_constant<int, 1>;
-    using S2 = std::integral_constant<int, 2 % ST>;
-    if constexpr (ST == 2) {
-      for (int ks = 0; ks < nK; ks += 2) {
-        pstep(S0{}, ks, fa0, fb0, fa1, fb1);
-        if (ks + 1 >= nK) break;
-        pstep(S1{}, ks + 1, fa1, fb1, fa0, fb0);
-      }
-    } else {  // buffer period 3, fragment-set period 2: unrolled by 6
-      for (int ks = 0; ks < nK; ks += 6) {
-        pstep(S0{}, ks, fa0, fb0, fa1, fb1);
-        if (ks + 1 >= nK) break;
-        pstep(S1{}, ks + 1, fa1, fb1, fa0, fb0);
-        if (ks + 2 >= nK) break;
-        pstep(S2{}, ks + 2, fa0, fb0, fa1, fb1);
-        if (ks + 3 >= nK) break;
-        pstep(S0{}, ks + 3, fa1, fb1, fa0, fb0);
-        if (ks + 4 >= nK) break;
-        pstep(S1{}, ks + 4, fa0, fb0, fa1, fb1);
-        if (ks + 5 >= nK) break;
-        pstep(S2{}, ks + 5, fa1, fb1, fa0, fb0);
-      }
-    }
-  }
-  if constexpr (PIPE) {
-#pragma unroll
-    for (int i = 0; i < WC; ++i)
-#pragma unroll
-      for (int j = 0; j < WP; ++j) acc[i][j] += acc2[PIPE ? i : 0][PIPE ? j : 0];
-  }
-  conv3_epilogue<WC, WP>(A, S, acc, p0, c0, wc, wp, lane, M, GHW, flags);
-}
-
 }  // namespace zp
 
 using namespace zp;
@@ -2944,77 +2369,6 @@ static bool quad_plan(const zp_conv_args& a, quad_geo* qg) {
   return true;
 }
 
-// k_conv3 tiles (4 waves, one per SIMD; tools/conv3_ab.py): 128 x 256 for 128-channel tiles, 64 x 128
-// (register-pipelined, 3-deep ring) for 64-channel tiles, 32 x 128 for the head.
-static int conv3_tp(const zp_conv_args& a, int tc) {
-  static const int sched = env_int("ZP_CONV3_SCHED");
-  if (tc == 128) return sched == 1 ? 128 : 256;  // 8-wave ping-pong 128 x 256, or the pipelined 128 x 128
-  return 128;
-}
-
-static int conv3_launch(const zp_conv_args& a, hipStream_t st) {
-  ZP_CHECK_ARG(a.Cin > 0 && a.Cin % 32 == 0, "zp_conv2d: ZP_F32X3 needs Cin %% 32 == 0 (got %d; the stem runs in f32 "
-               "with out_mode ZP_OUT_NHWC_X3)", a.Cin);
-  ZP_CHECK_ARG(a.ldx >= a.cx0 + a.Cin && a.cx0 % 8 == 0 && a.ldx % 8 == 0, "zp_conv2d: bad ldx/cx0");
-  ZP_CHECK_ARG(a.k_pad % 32 == 0, "zp_conv2d: k_pad %d not a multiple of 32", a.k_pad);
-  ZP_CHECK_ARG(!a.stats, "zp_conv2d: ZP_F32X3 is forward (eval) only: no train-mode statistics");
-  ZP_CHECK_ARG(a.out_mode == ZP_OUT_NHWC || a.out_mode == ZP_OUT_HEAD_NCHW,
-               "zp_conv2d: ZP_F32X3 writes split NHWC (ZP_OUT_NHWC) or the f32 head (ZP_OUT_HEAD_NCHW)");
-  const int tc = conv_tc(a);
-  ZP_CHECK_ARG(a.w_rows % tc == 0 && a.w_rows >= a.Cout, "zp_conv2d: w_rows %d", a.w_rows);
-  for (int s = 0; s < a.nsub; ++s) {
-    const zp_conv_sub& S = a.sub[s];
-    ZP_CHECK_ARG(S.w && S.y, "zp_conv2d: sub %d null w/y", s);
-    ZP_CHECK_ARG(S.ntaps >= 1 && S.ntaps <= ZP_MAX_TAPS && (long)S.ntaps * a.Cin <= a.k_pad,
-                 "zp_conv2d: sub %d ntaps %d / k_pad %d", s, S.ntaps, a.k_pad);
-    if (a.out_mode == ZP_OUT_NHWC)
-      ZP_CHECK_ARG(S.ldy >= S.cy0 + a.Cout && S.cy0 % 4 == 0 && S.ldy % 4 == 0, "zp_conv2d: bad ldy/cy0");
-    else
-      ZP_CHECK_ARG(S.y2 || a.Cout == 1, "zp_conv2d: head needs y2");
-    // the epilogue's plane strides assume every sub writes the same output tensor shape
-    ZP_CHECK_ARG(S.OH == a.sub[0].OH && S.OW == a.sub[0].OW, "zp_conv2d: ZP_F32X3 subs must share the output shape");
-  }
-  if (a.res) ZP_CHECK_ARG(a.ldr >= a.cr0 + a.Cout && a.cr0 % 4 == 0 && a.ldr % 4 == 0, "zp_conv2d: bad residual ld");
-  conv_taps tg{};
-  const long long xb = 3ll * a.N * a.IH * a.IW * a.ldx * 2;
-  const long long wb = 3ll * a.w_rows * a.k_pad * 2;
-  ZP_CHECK_ARG(xb < (1ll << 31) && wb < (1ll << 31),
-               "zp_conv2d: split input (%lld B) / weights (%lld B) must stay below 2 GiB per launch (split the batch)",
-               xb, wb);
-  tg.x_bytes = (unsigned)xb;
-  for (int s = 0; s < a.nsub; ++s) {
-    const zp_conv_sub& S = a.sub[s];
-    tg.w_bytes[s] = (unsigned)wb;
-    int nx = 1;
-    while (nx < S.ntaps && S.ty[nx] == S.ty[0]) ++nx;
-    const int ny = S.ntaps / nx;
-    tg.ny[s] = ny;
-    tg.nx[s] = nx;
-    tg.ty0[s] = S.ty[0];
-    tg.tx0[s] = S.tx[0];
-    tg.dty[s] = ny > 1 ? S.ty[nx] - S.ty[0] : 0;
-    tg.dtx[s] = nx > 1 ? S.tx[1] - S.tx[0] : 0;
-    bool grid = ny * nx == S.ntaps && ny <= 32 && nx <= 32;
-    for (int t = 0; grid && t < S.ntaps; ++t)
-      grid = S.ty[t] == tg.ty0[s] + (t / nx) * tg.dty[s] && S.tx[t] == tg.tx0[s] + (t % nx) * tg.dtx[s];
-    ZP_CHECK_ARG(grid, "zp_conv2d: sub %d taps must form a (row x column) grid of at most 32 x 32, rows outer", s);
-  }
-  const int tp = conv3_tp(a, tc);
-  const int gx = ceil_div((long)a.N * a.GH * a.GW, tp), gy = ceil_div(a.Cout, tc);
-  const dim3 grid(gx, gy, a.nsub);
-  const int fl = conv_flags();
-  // schedule (ZP_CONV3_SCHED, tools/conv3_ab.py): register-pipelined one-wave-per-SIMD tiles over
-  // 128 pixels (128- / 64- / 32-channel), 3-deep ring; ZP_CONV3_SCHED=1: the 128-channel tile with
-  // a 2-deep ring
-  static const int sched = env_int("ZP_CONV3_SCHED");
-  if (tc == 128 && tp == 256) hipLaunchKernelGGL((k_conv3<4, 4, 4, 2, false>), grid, dim3(512), 0, st, a, tg, fl);
-  else if (tc == 128) hipLaunchKernelGGL((k_conv3<4, 4, 2, 2, true>), grid, dim3(256), 0, st, a, tg, fl);
-  else if (tc == 64) hipLaunchKernelGGL((k_conv3<2, 4, 2, 2, true>), grid, dim3(256), 0, st, a, tg, fl);
-  else hipLaunchKernelGGL((k_conv3<1, 4, 2, 2, true>), grid, dim3(256), 0, st, a, tg, fl);
-  ZP_LAUNCH_CHECK("zp_conv2d split-f32");
-  return ZP_OK;
-}
-
 // pixel tile: 256 (8 waves) whenever the cout tile allows it.  Measured on MI355X (R34 bs32,
 // profiles/r01_conv_sweep.md): the 8-wave 3-stage tile beats the 4-wave tiles even on the
 // 32x32 layers where it leaves part of the chip idle (fewer workgroups, but 2x the MFMA work
@@ -3064,7 +2418,7 @@ extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
   ZP_CHECK_ARG(a.nsub >= 1 && a.nsub <= ZP_MAX_SUB, "zp_conv2d: nsub %d", a.nsub);
   ZP_CHECK_ARG(a.x && a.N > 0 && a.GH > 0 && a.GW > 0 && a.IH > 0 && a.IW > 0 && a.Cout > 0,
                "zp_conv2d: bad geometry");
-  if (a.dtype == ZP_F32X3) return conv3_launch(a, (hipStream_t)stream);
+  if (a.dtype == ZP_F32X3) return conv3_launch(a, (hipStream_t)stream, conv_flags());
   const int E = a.dtype == ZP_F32 ? 4 : 8, KE = 8 * E;
   const bool smallc = a.Cin < KE;
   ZP_CHECK_ARG(a.Cin > 0 && a.Cin % E == 0 && (smallc || a.Cin % KE == 0),
@@ -3406,7 +2760,7 @@ extern "C" int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* st
   *tc = conv_tc(*a);
   *tp = conv_tp(*a);
   *stages = *tc == 256 ? 2 : conv_stages(*a, *tc);
-  *variant = a->dtype == ZP_F32X3 ? 4 : quad_plan(*a, nullptr) ? 3 : *tc <= 128 && strip_eligible(*a, nullptr) ? ((conv_flags() & 64) ? 2 : 1) : 0;
+  *variant = a->dtype == ZP_F32X3 ? (conv3_strip_ok(*a, *tc) ? 5 : 4) : quad_plan(*a, nullptr) ? 3 : *tc <= 128 && strip_eligible(*a, nullptr) ? ((conv_flags() & 64) ? 2 : 1) : 0;
   return ZP_OK;
 }
 
@@ -3415,7 +2769,9 @@ extern "C" int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* st
  * layers on the strip kernel (default 1); key 3: k_wgrad2 (default 1); key 4: k_wgrad2's
  * workgroup rounds over the CUs (default 1); key 5: k_wgrad_lds's workgroup rounds (default 1; 0 =
  * the older ~1024-workgroup target padded to a multiple of 8); key 6: the fewest workgroups
- * k_conv_quad runs with (default 256).  Returns the previous value. */
+ * k_conv_quad runs with (default 256); key 7: split-fp32 strip kernel k_conv3s (0 off, 1 the
+ * 64-channel tiles, 2 also the 128-channel tiles; -1 = ZP_CONV3_STRIP / default 1).  Returns the
+ * previous value. */
 extern "C" int zp_conv_tuning(int key, int value) {
   if (key == 0) {
     const int old = g_tc256_min_blocks;
@@ -3447,6 +2803,7 @@ extern "C" int zp_conv_tuning(int key, int value) {
     g_quad_min_blocks = value;
     return old;
   }
+  if (key == 7) return conv3_strip_mode(value);
   if (key == 4) {
     const int old = g_wgrad2_rounds;
     g_wgrad2_rounds = value > 0 ? value : 1;

@@ -1,0 +1,901 @@
+// Split-fp32 (ZP_F32X3, include/zp.h) forward convolutions for gfx950: k_conv3 (generic implicit
+// GEMM: strided / dilated / 1x1 convs, ConvTranspose phases, the merged ASPP, the NCHW head) and
+// k_conv3s (3x3 stride-1 convs with activation-strip reuse), their shared epilogue and the host
+// dispatch zp_conv2d calls for dtype ZP_F32X3.
+#include <stdlib.h>
+#include "zp_conv_kern.h"
+#include "zp_conv3.h"
+
+namespace zp {
+
+// k_conv3 epilogue: BN scale / shift (+ bias), split residual, ReLU, then split NHWC stores (3
+// planes) or the f32 NCHW head split.  acc[i][j] = 4 consecutive output channels x one pixel.
+template <int WC, int WP>
+__device__ __forceinline__ void conv3_epilogue(const zp_conv_args& A, const zp_conv_sub& S, f32x4 (&acc)[WC][WP],
+                                               const int p0, const int c0, const int wc, const int wp,
+                                               const int lane, const int M, const int GHW, const int flags) {
+  const int lr = lane & 15;
+  int pn[WP], poy[WP], pox[WP];
+  bool pok[WP];
+#pragma unroll
+  for (int j = 0; j < WP; ++j) {
+    const int p = p0 + wp * 16 * WP + j * 16 + lr;
+    pok[j] = p < M;
+    const int pp = pok[j] ? p : 0;
+    const int n = pp / GHW, rr = pp - n * GHW;
+    const int gy = rr / A.GW, gx = rr - gy * A.GW;
+    pn[j] = n;
+    poy[j] = gy * S.oys + S.oyo;
+    pox[j] = gx * S.oxs + S.oxo;
+  }
+  const long psy = (long)A.N * S.OH * S.OW * S.ldy;
+  const long psr = (long)A.N * S.OH * S.OW * A.ldr;
+  const int cbase = c0 + wc * 16 * WC + (lane >> 4) * 4;
+#pragma unroll
+  for (int i = 0; i < WC; ++i) {
+    const int cf = cbase + i * 16;
+    if (cf >= A.Cout) continue;
+    const bool full = cf + 3 < A.Cout;
+    float sc[4], sh[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      sc[r] = (S.scale && cf + r < A.Cout) ? S.scale[cf + r] : 1.f;
+      sh[r] = (S.shift && cf + r < A.Cout) ? S.shift[cf + r] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < WP; ++j) {
+      if (!pok[j]) continue;
+      const size_t pix = ((size_t)pn[j] * S.OH + poy[j]) * S.OW + pox[j];
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * sc[r] + sh[r];
+      if (A.res) {
+        const bf16_t* R = (const bf16_t*)A.res + pix * A.ldr + A.cr0 + cf;
+        if (full) {
+          const uint2 h = *(const uint2*)R, m = *(const uint2*)(R + psr), l = *(const uint2*)(R + 2 * psr);
+          const uint32_t hw[2] = {h.x, h.y}, mw[2] = {m.x, m.y}, lw[2] = {l.x, l.y};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int sft = (r & 1) * 16;
+            v[r] += join3((bf16_t)(hw[r >> 1] >> sft), (bf16_t)(mw[r >> 1] >> sft), (bf16_t)(lw[r >> 1] >> sft));
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (cf + r < A.Cout) v[r] += join3(R[r], R[r + psr], R[r + 2 * psr]);
+        }
+      }
+      if (A.relu) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+      }
+      if (A.out_mode == ZP_OUT_HEAD_NCHW) {
+        const size_t plane = (size_t)S.OH * S.OW;
+        const size_t sp = (size_t)poy[j] * S.OW + pox[j];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = cf + r;
+          if (c >= A.Cout) continue;
+          if (c == 0) ((float*)S.y)[(size_t)pn[j] * plane + sp] = v[r];
+          else ((float*)S.y2)[((size_t)pn[j] * (A.Cout - 1) + (c - 1)) * plane + sp] = v[r];
+        }
+        continue;
+      }
+      bf16_t h[4], m[4], l[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) split3(v[r], h[r], m[r], l[r]);
+      if ((flags & 16384) && v[0] != 1.f) continue;  // diagnostic: no stores (unless a value is exactly 1)
+      bf16_t* Y = (bf16_t*)S.y + pix * S.ldy + S.cy0 + cf;
+      if (full) {
+        *(uint2*)Y = make_uint2((uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16));
+        *(uint2*)(Y + psy) = make_uint2((uint32_t)m[0] | ((uint32_t)m[1] << 16), (uint32_t)m[2] | ((uint32_t)m[3] << 16));
+        *(uint2*)(Y + 2 * psy) =
+            make_uint2((uint32_t)l[0] | ((uint32_t)l[1] << 16), (uint32_t)l[2] | ((uint32_t)l[3] << 16));
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (cf + r < A.Cout) {
+            Y[r] = h[r];
+            Y[r + psy] = m[r];
+            Y[r + 2 * psy] = l[r];
+          }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// k_conv3: forward convolution on ZP_F32X3 operands (split fp32, zp.h): activations, packed weights
+// and the residual are three bf16 planes (hi, mid, lo) whose sum is the f32 value exactly.  Every
+// product a * b is formed from its six terms of magnitude >= 2^-16 |a b|:
+//   hi*hi + hi*mid + mid*hi + hi*lo + mid*mid + lo*hi
+// on v_mfma_f32_16x16x32_bf16 (f32 accumulate); the dropped terms (mid*lo, lo*mid, lo*lo) are below
+// 2^-23 |a b|, the order of f32's own product rounding.  That is f32-accurate arithmetic at 6 bf16
+// MFMAs per 16x16x32 product block = 6/16 of the v_mfma_f32_16x16x4_f32 cost, and -- since the three
+// B planes are staged once and each fragment feeds 3 / 2 / 1 MFMAs -- half the LDS traffic per MFMA
+// of the bf16 kernels.
+// Two accumulators per tile: hi*hi products in acc, the five correction terms in acc2, added once at
+// the end.  Measured (tools/x3_accuracy.py, R34 bs=32): with the correction sums added straight into
+// the full-size accumulator every conv carried a systematic NEGATIVE bias of ~-1e-7 relative (the
+// bf16 MFMA's internal alignment drops the low bits of addends far below the accumulator), which
+// compounded to 3x the exact-f32 engine's end-to-end error; accumulated among themselves the
+// correction terms keep their bits.
+// Tile: 2 NWP waves = 2 (cout) x NWP (pixel) computing TC = 32 WC output channels x TP = 64 NWP
+// pixels.  A K step is one tap x 32 input channels.  Staging: per plane, a 16-row x 32-element tile
+// (1 KB) is ONE buffer_load ... lds of 64 lanes, lane l fetching (row l & 15, 8 elements at k (l >>
+// 4) * 8): the LDS image is in MFMA fragment order, so every fragment read is a lane-linear
+// conflict-free ds_read_b128.  ST-deep ring; the tap walk (scalar), validity masks and out-of-image
+// zeros (offset past the buffer end) follow k_conv.
+// Schedules:
+//   PIPE = false (8 waves, 2 per SIMD): per step [next DMA][fragment reads][MFMAs][wait + barrier];
+//     ping-pong (flags & 8): waves 4-7 run one barrier behind, so on each SIMD one wave's MFMAs
+//     overlap its partner's reads.
+//   PIPE = true (NWP = 2: 4 waves, one per SIMD, 512-register budget): the fragments of step k + 1
+//     are read into a second register set while step k's MFMAs run, and the DMA runs ST steps
+//     ahead; per step one counted vmcnt wait + one barrier, no LDS read on the MFMA critical path.
+// ------------------------------------------------------------------------------------
+template <int WC, int WP, int NWP, int ST, bool PIPE>
+__global__ void __launch_bounds__(128 * NWP) k_conv3(const zp_conv_args A, const conv_taps TG, const int flags) {
+  constexpr int TC = 32 * WC, TP = 16 * WP * NWP, NW = 2 * NWP;
+  constexpr int NTW = TC / 16, NT = (TC + TP) / 16;  // weight tiles / all tiles (16 rows) per plane
+  constexpr int UNITS = 3 * NT;                      // (plane, tile) DMA units per stage
+  constexpr int TPW = (NT + NW - 1) / NW;            // tiles per wave (some waves idle in the last)
+  constexpr int GRP = 3 * TPW;                       // DMA instructions per wave per stage
+  static_assert(ST == 2 || ST == 3, "ring depth");
+  static_assert(ST == 2 || NT % NW == 0, "counted vmcnt waits need the same DMA count on every wave");
+  static_assert(!PIPE || NW == 4, "the register-pipelined schedule runs one wave per SIMD");
+  static_assert(WP == 4 || WP == 8, "pixel fragments per wave");
+  __shared__ uint4 lds[ST * UNITS * 64];
+  static_assert(ST * UNITS * 1024 <= 160 * 1024, "LDS");
+  static_assert((2 * NT + WC + 3) * 1024 < 65536, "ds_read immediate range");
+  const zp_conv_sub& S = A.sub[blockIdx.z];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wid / NWP, wp = wid % NWP;
+  const int GHW = A.GH * A.GW;
+  const int M = A.N * GHW;
+  int bx = blockIdx.x, by = blockIdx.y;
+  if (flags & 2) {  // XCD-aware order (k_conv): the cout tiles of a pixel tile meet in one L2
+    const int total = gridDim.x * gridDim.y;
+    const int bid = blockIdx.x + gridDim.x * blockIdx.y;
+    const int lin = (total & 7) ? bid : (bid & 7) * (total >> 3) + (bid >> 3);
+    bx = lin / gridDim.y;
+    by = lin - bx * gridDim.y;
+  }
+  const int p0 = bx * TP, c0 = by * TC;
+  const int tb = blockIdx.z;
+  const int CB = A.Cin / 32;
+  const int ny = TG.ny[tb], nx = TG.nx[tb], dty = TG.dty[tb], dtx = TG.dtx[tb];
+  const int nK = S.ntaps * CB;
+  const int lr = lane & 15, lk = (lane >> 4) * 8;
+  // plane strides in bytes (scalar offsets of the DMA: the three planes of a tile share the lane's
+  // offset register)
+  const unsigned psx_b = (unsigned)((long)A.N * A.IH * A.IW * A.ldx * 2);
+  const unsigned psw_b = (unsigned)((long)A.w_rows * A.k_pad * 2);
+
+  // tiles of this wave: T = wid + NW k (all three planes each); wave-uniform kind, per-lane base
+  // offset (plane 0, bytes) and tap validity masks
+  unsigned ubase[TPW], uym[TPW], uxm[TPW];
+#pragma unroll
+  for (int k = 0; k < TPW; ++k) {
+    const int t = wid + NW * k;
+    ubase[k] = 0u;
+    uym[k] = uxm[k] = 0u;
+    if (t >= NT) continue;
+    if (t < NTW) {
+      ubase[k] = (unsigned)(((long)(c0 + t * 16 + lr) * A.k_pad + lk) * 2);
+    } else {
+      const int m = p0 + (t - NTW) * 16 + lr;
+      const bool ok = m < M;
+      const int mm = ok ? m : 0;
+      const int n = mm / GHW, rr = mm - n * GHW;
+      const int gy = rr / A.GW, gx = rr - gy * A.GW;
+      const int y0 = gy * A.sy, x0 = gx * A.sx;
+      ubase[k] = (unsigned)(((((long)n * A.IH + y0) * A.IW + x0) * A.ldx + A.cx0 + lk) * 2);
+      unsigned ym = 0, xm = 0;
+      for (int q = 0; q < ny; ++q) ym |= (unsigned)((unsigned)(y0 + TG.ty0[tb] + q * dty) < (unsigned)A.IH) << q;
+      for (int q = 0; q < nx; ++q) xm |= (unsigned)((unsigned)(x0 + TG.tx0[tb] + q * dtx) < (unsigned)A.IW) << q;
+      uym[k] = ok ? ym : 0u;
+      uxm[k] = xm;
+    }
+  }
+#if defined(__HIP_DEVICE_COMPILE__)
+  const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)A.x, (short)0, (int)TG.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)S.w, (short)0, (int)TG.w_bytes[tb], 0x00020000);
+#endif
+  // scalar walk of the next step to issue.  K order: 32-channel chunk OUTER, taps inner -- the taps
+  // of one chunk read nearly the same input rows (shifted by the tap offsets), so all but the
+  // first come from L2; with the taps outer (k_conv's order) each tap's sweep over every chunk of
+  // a tile evicted the rows before the next tap came back to them, and the staging ran at the
+  // Infinity-Cache / HBM rate.  act_off = ((ty * IW + tx) * ldx + cb * 32) * 2; the weight offset
+  // of (tap t, chunk cb) in the packed row (k = t * Cin + c) is w_koff = (t * Cin + cb * 32) * 2.
+  int w_tyi = 0, w_txi = 0, w_cb = 0, w_t = 0;
+  int act_off = ((TG.ty0[tb] * A.IW + TG.tx0[tb]) * A.ldx) * 2;
+  int w_koff = 0;
+  const int step_x = dtx * A.ldx * 2, step_y = dty * A.IW * A.ldx * 2;
+  const int cin2 = A.Cin * 2;
+  // diagnostic ablation flags (timing only, wrong results): 4096 no DMA after the prologue, 8192 no
+  // MFMA, 16384 no epilogue stores
+  const bool abl_dma = flags & 4096, abl_mfma = flags & 8192;
+  auto issue = [&](int ks, int stage) {
+    unsigned voff[TPW];
+#pragma unroll
+    for (int k = 0; k < TPW; ++k) {
+      const bool w = wid + NW * k < NTW;
+      const bool ok = (uym[k] >> w_tyi) & (uxm[k] >> w_txi) & 1u;
+      voff[k] = w ? ubase[k] : (ok ? ubase[k] + (unsigned)act_off : 0x80000000u);
+    }
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+    for (int k = 0; k < TPW; ++k) {
+      const int t = wid + NW * k;
+      if (t >= NT) continue;
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) {
+        auto* d = (__attribute__((address_space(3))) void*)&lds[(stage * UNITS + pl * NT + t) * 64];
+        if (t < NTW) __builtin_amdgcn_raw_ptr_buffer_load_lds(wrsrc, d, 16, voff[k], pl * psw_b + w_koff, 0, 0);
+        else __builtin_amdgcn_raw_ptr_buffer_load_lds(xrsrc, d, 16, voff[k], pl * psx_b, 0, 0);
+      }
+    }
+#endif
+    (void)ks;
+    ++w_t;
+    w_koff += cin2;
+    act_off += step_x;
+    if (++w_txi == nx) {
+      w_txi = 0;
+      act_off += step_y - nx * step_x;
+      if (++w_tyi == ny) {
+        w_tyi = 0;
+        w_t = 0;
+        ++w_cb;
+        act_off += 64 - ny * step_y;
+        w_koff = w_cb * 64;
+      }
+    }
+  };
+
+  // PIPE: a full second accumulator for the correction terms (one wave per SIMD has the registers);
+  // otherwise each half of the pixel fragments gets a fresh correction accumulator per K step,
+  // added into acc by VALU adds (round-to-nearest, unbiased) right after its MFMAs
+  constexpr int A2C = PIPE ? WC : 1, A2P = PIPE ? WP : 1;
+  f32x4 acc[WC][WP], acc2[A2C][A2P];
+#pragma unroll
+  for (int i = 0; i < WC; ++i)
+#pragma unroll
+    for (int j = 0; j < WP; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < A2C; ++i)
+#pragma unroll
+    for (int j = 0; j < A2P; ++j) acc2[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const unsigned l0 = lds_addr(lds) + (unsigned)lane * 16u;
+  unsigned abase[ST], bbase[ST];
+#pragma unroll
+  for (int s = 0; s < ST; ++s) {
+    abase[s] = l0 + (unsigned)(s * UNITS + wc * WC) * 1024u;
+    bbase[s] = l0 + (unsigned)(s * UNITS + NTW + wp * WP) * 1024u;
+  }
+  // fragment reads: inline-asm ds_read_b128 (waited on explicitly) in the single-register-set
+  // schedule; plain LDS loads in the register-pipelined one, whose reads stay in flight across the
+  // MFMAs -- the compiler then tracks their lgkmcnt itself (an asm read's destination registers
+  // are "written" at issue for the compiler, which may copy them before the data lands)
+  const int awo = (wc * WC) * 64 + lane, bwo = (NTW + wp * WP) * 64 + lane;
+  auto read_a = [&](auto s_c, uint4 (&af)[3][WC]) {
+    constexpr int s = decltype(s_c)::value;
+    static_for<3>([&](auto p_c) {
+      constexpr int p = decltype(p_c)::value;
+      static_for<WC>([&](auto i) {
+        if constexpr (PIPE) af[p][i] = lds[(s * UNITS + p * NT + i) * 64 + awo];
+        else af[p][i] = ds_read16<(p * NT + i) * 1024>(abase[s]);
+      });
+    });
+  };
+  auto read_b = [&](auto s_c, auto j0_c, auto j1_c, uint4 (&bfr)[3][WP]) {  // pixel fragments [J0, J1)
+    constexpr int s = decltype(s_c)::value, J0 = decltype(j0_c)::value, J1 = decltype(j1_c)::value;
+    static_for<3>([&](auto p_c) {
+      constexpr int p = decltype(p_c)::value;
+      static_for<J1 - J0>([&](auto jj) {
+        if constexpr (PIPE) bfr[p][J0 + jj] = lds[(s * UNITS + p * NT + J0 + jj) * 64 + bwo];
+        else bfr[p][J0 + jj] = ds_read16<(p * NT + J0 + jj) * 1024>(bbase[s]);
+      });
+    });
+  };
+  using J0c = std::integral_constant<int, 0>;
+  using JHc = std::integral_constant<int, WP / 2>;
+  using JWc = std::integral_constant<int, WP>;
+  auto read_frags = [&](auto s_c, uint4 (&af)[3][WC], uint4 (&bfr)[3][WP]) {
+    read_a(s_c, af);
+    read_b(s_c, J0c{}, JWc{}, bfr);
+  };
+  auto mfmas_part = [&](auto j0_c, auto j1_c, const uint4 (&af)[3][WC], const uint4 (&bfr)[3][WP]) {
+    constexpr int J0 = decltype(j0_c)::value, J1 = decltype(j1_c)::value;
+    // terms: mid*mid, hi*lo, lo*hi, mid*hi, hi*mid -> acc2; hi*hi -> acc
+    constexpr int TA[6] = {1, 0, 2, 1, 0, 0}, TB[6] = {1, 2, 0, 0, 1, 0};
+    if (!abl_mfma && PIPE) {
+      static_for<6>([&](auto t_c) {
+        constexpr int t = decltype(t_c)::value;
+#pragma unroll
+        for (int i = 0; i < WC; ++i)
+#pragma unroll
+          for (int j = J0; j < J1; ++j) {
+            if constexpr (t < 5) MfmaTraits<bf16_t>::mma(acc2[PIPE ? i : 0][PIPE ? j : 0], af[TA[t]][i], bfr[TB[t]][j]);
+            else MfmaTraits<bf16_t>::mma(acc[i][j], af[TA[t]][i], bfr[TB[t]][j]);
+          }
+      });
+    } else if (!abl_mfma) {
+      // per half of the pixel fragments: corrections into a fresh c2, hi*hi into acc, then
+      // acc += c2 on the VALU
+      static_for<2>([&](auto h_c) {
+        constexpr int H0 = J0 + decltype(h_c)::value * ((J1 - J0) / 2), HN = (J1 - J0) / 2;
+        f32x4 c2[WC][HN];
+#pragma unroll
+        for (int i = 0; i < WC; ++i)
+#pragma unroll
+          for (int jj = 0; jj < HN; ++jj) c2[i][jj] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        static_for<5>([&](auto t_c) {
+          constexpr int t = decltype(t_c)::value;
+#pragma unroll
+          for (int i = 0; i < WC; ++i)
+#pragma unroll
+            for (int jj = 0; jj < HN; ++jj) MfmaTraits<bf16_t>::mma(c2[i][jj], af[TA[t]][i], bfr[TB[t]][H0 + jj]);
+        });
+#pragma unroll
+        for (int i = 0; i < WC; ++i)
+#pragma unroll
+          for (int jj = 0; jj < HN; ++jj) MfmaTraits<bf16_t>::mma(acc[i][H0 + jj], af[0][i], bfr[0][H0 + jj]);
+#pragma unroll
+        for (int i = 0; i < WC; ++i)
+#pragma unroll
+          for (int jj = 0; jj < HN; ++jj) acc[i][H0 + jj] += c2[i][jj];
+      });
+    } else {
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+#pragma unroll
+        for (int i = 0; i < WC; ++i)
+#pragma unroll
+          for (int j = J0; j < J1; ++j) acc[i][j][0] += __uint_as_float(af[p][i].x ^ bfr[p][j].y);
+    }
+  };
+  auto mfmas = [&](const uint4 (&af)[3][WC], const uint4 (&bfr)[3][WP]) { mfmas_part(J0c{}, JWc{}, af, bfr); };
+
+  if constexpr (!PIPE) {
+    const bool pingpong = NW == 8 && (flags & 8);
+    // step ks reads buffer ks % ST; the DMA of step ks + ST - 1 is issued first into the buffer
+    // step ks - 1 read (all waves passed the barrier that ended step ks - 1)
+    auto step = [&](auto s_c, int ks) {
+      constexpr int s = decltype(s_c)::value;
+      const bool more = ks + ST - 1 < nK;
+      if (more && !abl_dma) issue(ks + ST - 1, (s + ST - 1) % ST);
+      uint4 af[3][WC], bfr[3][WP];
+      // the second half of the pixel fragments is read while the first half's MFMAs run (the
+      // buffer is not refilled before the barrier that ends this step)
+      read_a(s_c, af);
+      read_b(s_c, J0c{}, JHc{}, bfr);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      read_b(s_c, JHc{}, JWc{}, bfr);
+      auto wait_next = [&]() {  // step ks + 1's DMA landed (the newest ST - 2 groups may remain)
+        if (more && !abl_dma) vm_wait<GRP * (ST - 2)>();
+        else vm_wait<0>();
+      };
+      if (pingpong) {
+        wait_next();
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (flags & 4) __builtin_amdgcn_s_setprio(1);
+      mfmas_part(J0c{}, JHc{}, af, bfr);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      mfmas_part(JHc{}, JWc{}, af, bfr);
+      __builtin_amdgcn_sched_barrier(0);
+      if (flags & 4) __builtin_amdgcn_s_setprio(0);
+      if (!pingpong) wait_next();
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    issue(0, 0);
+    if (ST == 3 && nK > 1) {
+      issue(1, 1);
+      vm_wait<GRP>();
+    } else {
+      vm_wait<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (pingpong && wid >= 4) __builtin_amdgcn_s_barrier();
+    if constexpr (ST == 3) {
+      for (int ks = 0; ks < nK; ks += 3) {
+        step(I0{}, ks);
+        if (ks + 1 >= nK) break;
+        step(I1{}, ks + 1);
+        if (ks + 2 >= nK) break;
+        step(I2{}, ks + 2);
+      }
+    } else {
+      for (int ks = 0; ks < nK; ks += 2) {
+        step(I0{}, ks);
+        if (ks + 1 >= nK) break;
+        step(I1{}, ks + 1);
+      }
+    }
+    if (pingpong && wid < 4) __builtin_amdgcn_s_barrier();
+  } else {
+    // Prologue: the DMA of steps 0 .. ST - 1 (buffer = step), then step 0's fragments.  Step ks
+    // (fragments F[ks & 1] loaded): wait for them; wait for step ks + 1's DMA + barrier (buffer
+    // (ks + 1) % ST complete; every wave has read buffer ks % ST); issue the DMA of step ks + ST into
+    // buffer ks % ST; issue step ks + 1's fragment reads into F[(ks + 1) & 1]; run step ks's MFMAs.
+    // two named fragment sets (a [2][3][WC] array of them was demoted to scratch memory)
+    uint4 fa0[3][WC], fb0[3][WP], fa1[3][WC], fb1[3][WP];
+    int issued = 0;
+    for (int q = 0; q < ST; ++q)
+      if (q < nK) {
+        issue(q, q);
+        ++issued;
+      }
+    if (issued == ST) vm_wait<GRP * (ST - 1)>();
+    else vm_wait<0>();
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    using Z0 = std::integral_constant<int, 0>;
+    read_frags(Z0{}, fa0, fb0);
+    auto pstep = [&](auto s_c, int ks, uint4 (&ca)[3][WC], uint4 (&cb)[3][WP], uint4 (&na)[3][WC],
+                     uint4 (&nb)[3][WP]) {
+      constexpr int s = decltype(s_c)::value;
+      constexpr int sn = (s + 1) % ST;
+      // this wave's reads of buffer s (F[ks]) have landed before the barrier below releases the
+      // buffer to the next DMA
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      const bool next = ks + 1 < nK;
+      if (next) {
+        // outstanding DMA groups: steps ks + 1 .. min(ks + ST - 1, nK - 1); the newest
+        // ST - 2 of them may stay in flight when they all exist
+        if (ks + ST - 1 < nK && !abl_dma) vm_wait<GRP * (ST - 2)>();
+        else vm_wait<0>();
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        read_frags(std::integral_constant<int, sn>{}, na, nb);
+        if (ks + ST < nK && !abl_dma) issue(ks + ST, s);
+      }
+      if (flags & 4) __builtin_amdgcn_s_setprio(1);
+      mfmas(ca, cb);
+      if (flags & 4) __builtin_amdgcn_s_setprio(0);
+    };
+    using S0 = std::integral_constant<int, 0>;
+    using S1 = std::integral_constant<int, 1>;
+    using S2 = std::integral_constant<int, 2 % ST>;
+    if constexpr (ST == 2) {
+      for (int ks = 0; ks < nK; ks += 2) {
+        pstep(S0{}, ks, fa0, fb0, fa1, fb1);
+        if (ks + 1 >= nK) break;
+        pstep(S1{}, ks + 1, fa1, fb1, fa0, fb0);
+      }
+    } else {  // buffer period 3, fragment-set period 2: unrolled by 6
+      for (int ks = 0; ks < nK; ks += 6) {
+        pstep(S0{}, ks, fa0, fb0, fa1, fb1);
+        if (ks + 1 >= nK) break;
+        pstep(S1{}, ks + 1, fa1, fb1, fa0, fb0);
+        if (ks + 2 >= nK) break;
+        pstep(S2{}, ks + 2, fa0, fb0, fa1, fb1);
+        if (ks + 3 >= nK) break;
+        pstep(S0{}, ks + 3, fa1, fb1, fa0, fb0);
+        if (ks + 4 >= nK) break;
+        pstep(S1{}, ks + 4, fa0, fb0, fa1, fb1);
+        if (ks + 5 >= nK) break;
+        pstep(S2{}, ks + 5, fa1, fb1, fa0, fb0);
+      }
+    }
+  }
+  if constexpr (PIPE) {
+#pragma unroll
+    for (int i = 0; i < WC; ++i)
+#pragma unroll
+      for (int j = 0; j < WP; ++j) acc[i][j] += acc2[PIPE ? i : 0][PIPE ? j : 0];
+  }
+  conv3_epilogue<WC, WP>(A, S, acc, p0, c0, wc, wp, lane, M, GHW, flags);
+}
+
+// ------------------------------------------------------------------------------------
+// k_conv3s: the split-fp32 3x3 stride-1 convolution with activation-strip reuse (k_conv_strip2's
+// idea on k_conv3's operands).  k_conv3 stages the activation tile of every tap: 9 shifted copies
+// of nearly the same rows per 32-channel chunk, and its staging (LDS-DMA, ~7 TB/s aggregate in
+// these kernels) -- not the MFMAs -- bounds it (tools/conv3_ab.py: the kernel runs as long without
+// MFMAs as with them).  Here a tile is TR = 256 / W full image rows and, per (32-channel chunk, tap
+// row) group, ONE strip of TR x (W + 2 pad) input pixels (3 planes) is staged and read by the
+// three taps of the row at column offsets 0, d, 2d; weights per tap as k_conv3.  Staged bytes per
+// three taps: weights 72 KB + strip <= 54 KB instead of 72 + 144 KB.
+// Strip image: 64 B (32 channels) per strip row and plane, its four 16 B chunks stored at
+// c ^ ((row >> 1) & 2) -- a ds_read_b128 of ANY 16 consecutive rows (a fragment at any tap column)
+// is then conflict-free (exhaustive search over the lane groups of ds_read_b128); the swizzle is
+// applied on the per-lane DMA source address (LDS-DMA writes lane-linearly).
+// Schedule per step (one tap column): next step's weights (double-buffered slot) and, at the
+// group's first step, the next group's strip (double-buffered slot) are issued first; the A tile
+// (3 planes x WC) is read whole, the strip fragments stream through a 2-deep ring (3 planes per
+// pixel fragment); per pixel fragment a flushed correction accumulator (k_conv3's numerics);
+// counted waits: at a group's first step only the weights are waited for (the strip has two more
+// steps), later steps wait for all.  244 VGPRs at WC = 4, no spills.
+// 8 waves = 2 (cout) x 4 (pixel), TC = 32 WC output channels x 256 pixels.
+// ------------------------------------------------------------------------------------
+struct strip3_geo {
+  int W, TR, SW, SR;            // width, rows per tile, strip width W + 2 pad, strip rows TR * SW
+  int ty0, dty, tx0, dtx, pad;  // tap grid (3 x 3) and the halo width
+  unsigned x_bytes, w_bytes;
+};
+
+template <int WC>
+__global__ void __launch_bounds__(512) k_conv3s(const zp_conv_args A, const strip3_geo SG, const int flags) {
+  constexpr int WP = 4, NW = 8;
+  constexpr int TC = 32 * WC, TP = 256;
+  constexpr int NTW = TC / 16;                  // weight tiles per plane
+  constexpr int SRP = 288;                      // strip rows per plane slot (>= SR, multiple of 16)
+  constexpr int SB = SRP / 16;                  // strip row blocks per plane
+  constexpr int SU = 3 * SB;                    // strip DMA units per group
+  constexpr int SUW = (SU + NW - 1) / NW;       // per wave (the last waves one fewer)
+  constexpr int WU = 3 * NTW;                   // weight DMA units per step
+  constexpr int WUW = (WU + NW - 1) / NW;
+  constexpr int WSLOT = 3 * NTW * 1024;         // bytes per weight slot
+  constexpr int SSLOT = 3 * SRP * 64;           // bytes per strip slot
+  __shared__ uint4 lds[(2 * WSLOT + 2 * SSLOT) / 16];
+  static_assert(2 * WSLOT + 2 * SSLOT <= 160 * 1024, "LDS");
+  static_assert(2 * WSLOT < 65536 && 2 * SRP * 64 + 4096 < 65536, "ds_read immediate range");
+  const zp_conv_sub& S = A.sub[0];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wid / 4, wp = wid % 4;
+  const int GHW = A.GH * A.GW;
+  const int M = A.N * GHW;
+  int bx = blockIdx.x, by = blockIdx.y;
+  if (flags & 2) {  // XCD-aware order (k_conv)
+    const int total = gridDim.x * gridDim.y;
+    const int bid = blockIdx.x + gridDim.x * blockIdx.y;
+    const int lin = (total & 7) ? bid : (bid & 7) * (total >> 3) + (bid >> 3);
+    bx = lin / gridDim.y;
+    by = lin - bx * gridDim.y;
+  }
+  const int p0 = bx * TP, c0 = by * TC;
+  const int n_img = p0 / GHW, y0 = (p0 - n_img * GHW) / SG.W;
+  const int CB = A.Cin / 32;
+  const int lr = lane & 15, lk = (lane >> 4) * 8;
+  const unsigned psx_b = (unsigned)((long)A.N * A.IH * A.IW * A.ldx * 2);
+  const long psw = (long)A.w_rows * A.k_pad;
+#if defined(__HIP_DEVICE_COMPILE__)
+  const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)A.x, (short)0, (int)SG.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)S.w, (short)0, (int)SG.w_bytes, 0x00020000);
+#endif
+  // weight units of this wave: u = wid + NW k -> (plane, tile); per-lane row offset (bytes, plane
+  // included); the (tap, chunk) offset is scalar: (t * Cin + cb * 32) * 2
+  unsigned wv[WUW];
+#pragma unroll
+  for (int k = 0; k < WUW; ++k) {
+    const int u = wid + NW * k;
+    const int pl = u / NTW, t = u - pl * NTW;
+    wv[k] = u < WU ? (unsigned)((pl * psw + (long)(c0 + t * 16 + lr) * A.k_pad + lk) * 2) : 0u;
+  }
+  // strip units of this wave: v = wid + NW k -> (plane, row block); lane -> strip row rb * 16 +
+  // lane / 4, LDS chunk position lane & 3 holding source chunk (lane & 3) ^ ((row >> 1) & 2).
+  // sv: the source offset for tap row 0 / chunk 0 (plane included, 16 B aligned) with a 3-bit
+  // "input row inside the image" mask per tap row in the low bits (0 for padding columns / rows)
+  const int rowb = A.IW * A.ldx * 2;
+  unsigned sv[SUW];
+#pragma unroll
+  for (int k = 0; k < SUW; ++k) {
+    const int v = wid + NW * k;
+    const int pl = v / SB, rb = v - pl * SB;
+    const int R = rb * 16 + (lane >> 2);
+    const int tr = R / SG.SW, col = R - tr * SG.SW;
+    const int ix = col + SG.tx0;
+    const int c = (lane & 3) ^ ((R >> 1) & 2);
+    const bool ok = v < SU && R < SG.SR && (unsigned)ix < (unsigned)A.IW;
+    unsigned m = 0;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+      m |= (unsigned)(ok && (unsigned)(y0 + tr + SG.ty0 + ky * SG.dty) < (unsigned)A.IH) << ky;
+    const long base = (long)pl * A.N * A.IH * A.IW * A.ldx +
+                      (((long)n_img * A.IH + y0 + tr + SG.ty0) * A.IW + ix) * A.ldx + A.cx0 + c * 8;
+    sv[k] = ok ? ((unsigned)(base * 2) | m) : 0u;
+  }
+  const int nw_units = (WU - wid + NW - 1) / NW;  // this wave's weight / strip DMA counts
+  const int ns_units = (SU - wid + NW - 1) / NW;
+  (void)psx_b;
+
+  const unsigned l0 = lds_addr(lds);
+  auto issue_w = [&](int slot, int t, int cb) {
+    const int koff = (t * A.Cin + cb * 32) * 2;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+    for (int k = 0; k < WUW; ++k) {
+      if (wid + NW * k >= WU) continue;
+      auto* d = (__attribute__((address_space(3))) void*)&lds[(slot * WSLOT + (wid + NW * k) * 1024) / 16];
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrsrc, d, 16, wv[k], koff, 0, 0);
+    }
+#endif
+  };
+  auto issue_s = [&](int slot, int ky, int cb) {
+    // the tap-row offset goes into the lane offset (32-bit VALU wrap: the tap-row-0 base may be
+    // "negative"), the chunk into the scalar offset
+    const unsigned rowoff = (unsigned)(ky * SG.dty * rowb);
+    const int soff = cb * 64;
+    unsigned so[SUW];
+#pragma unroll
+    for (int k = 0; k < SUW; ++k) so[k] = (sv[k] >> ky) & 1u ? (sv[k] & ~15u) + rowoff : 0x80000000u;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+    for (int k = 0; k < SUW; ++k) {
+      if (wid + NW * k >= SU) continue;
+      auto* d = (__attribute__((address_space(3))) void*)&lds[(2 * WSLOT + slot * SSLOT + (wid + NW * k) * 1024) / 16];
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrsrc, d, 16, so[k], soff, 0, 0);
+    }
+#endif
+  };
+
+  f32x4 acc[WC][WP];
+#pragma unroll
+  for (int i = 0; i < WC; ++i)
+#pragma unroll
+    for (int j = 0; j < WP; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // fragment addresses: A (weight tile wc * WC + i of plane p, slot w) = abase + immediate;
+  // B (strip, tap column kx, pixel fragment j): per-lane offsets in the strip plane
+  const unsigned abase = l0 + (unsigned)(wc * WC) * 1024u + (unsigned)lane * 16u;
+  // strip row of pixel fragment j at tap column 0 (the fragment at column kx starts kx * dtx rows
+  // later; its swizzled address is formed per read: a few VALU beside the MFMAs)
+  int brow[WP];
+#pragma unroll
+  for (int j = 0; j < WP; ++j) {
+    const int q = wp * 16 * WP + j * 16 + lr;
+    const int r = q / SG.W, x = q - r * SG.W;
+    brow[j] = r * SG.SW + x;  // strip column 0 is input column tx0
+  }
+  const unsigned lch = (unsigned)(lane >> 4);
+  // uint4 index of pixel fragment j's chunk at tap column kx in strip slot gs, plane 0
+  // (formed per read, a few VALU beside the MFMAs: hoisted out of the loop, the 24 (j, kx, slot)
+  // addresses would not fit beside the fragments -- the empty asm keeps them in the loop)
+  auto bidx = [&](int j, int kx, int gs) -> int {
+    int b = brow[j];
+    asm volatile("" : "+v"(b));
+    const unsigned R = (unsigned)(b + kx * SG.dtx);
+    return (2 * WSLOT + gs * SSLOT) / 16 + (int)(R * 4u + (lch ^ ((R >> 1) & 2u)));
+  };
+  constexpr int TA[6] = {1, 0, 2, 1, 0, 0}, TB[6] = {1, 2, 0, 0, 1, 0};
+  // one pixel fragment j: the five correction products into a flushed accumulator (WC tiles), then
+  // hi x hi into acc and the correction added by VALU (k_conv3's numerics)
+  auto frag = [&](auto j_c, const uint4 (&af)[3][WC], const uint4 (&bq)[3]) {
+    constexpr int J = decltype(j_c)::value;
+    f32x4 c2[WC];
+#pragma unroll
+    for (int i = 0; i < WC; ++i) c2[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    static_for<5>([&](auto t_c) {
+      constexpr int t = decltype(t_c)::value;
+#pragma unroll
+      for (int i = 0; i < WC; ++i) MfmaTraits<bf16_t>::mma(c2[i], af[TA[t]][i], bq[TB[t]]);
+    });
+#pragma unroll
+    for (int i = 0; i < WC; ++i) MfmaTraits<bf16_t>::mma(acc[i][J], af[0][i], bq[0]);
+#pragma unroll
+    for (int i = 0; i < WC; ++i) {
+      acc[i][J] += c2[i];
+      asm volatile("" : "+v"(acc[i][J]));  // keeps the add here (sunk to the next step's use, all
+    }                                      // 4 WP correction accumulators would stay live)
+  };
+
+  // one step: tap column kx of group (ky, cb) with strip slot GS, weight slot WS.  The A tile (3
+  // planes x WC) is read whole; the strip fragments stream through a 2-deep ring (3 planes each),
+  // plain LDS loads so the compiler counts lgkmcnt for the reads left in flight
+  auto step = [&](auto gs_c, auto ws_c, auto kx_c, int ky, int cb, bool more_w, int nt, int ncb, bool more_s,
+                  int nky, int nscb) {
+    constexpr int GS = decltype(gs_c)::value, WS = decltype(ws_c)::value, KX = decltype(kx_c)::value;
+    if (more_w) issue_w(WS ^ 1, nt, ncb);
+    if (KX == 0 && more_s) issue_s(GS ^ 1, nky, nscb);
+    uint4 af[3][WC], bq0[3], bq1[3];
+    const int aw = (WS * WSLOT + wc * WC * 1024) / 16 + lane;
+    static_for<3>([&](auto p_c) {
+      constexpr int p = decltype(p_c)::value;
+      static_for<WC>([&](auto i) { af[p][i] = lds[aw + (p * NTW + i) * 64]; });
+    });
+    const int b0 = bidx(0, KX, GS), b1 = bidx(1, KX, GS);
+    static_for<3>([&](auto p) { bq0[p] = lds[b0 + p * SRP * 4]; });
+    static_for<3>([&](auto p) { bq1[p] = lds[b1 + p * SRP * 4]; });
+    if (flags & 4) __builtin_amdgcn_s_setprio(1);
+    static_for<WP>([&](auto j_c) {
+      constexpr int J = decltype(j_c)::value;
+      if constexpr (J % 2 == 0) frag(j_c, af, bq0);
+      else frag(j_c, af, bq1);
+      if constexpr (J + 2 < WP) {
+        const int bn = bidx(J + 2, KX, GS);
+        if constexpr (J % 2 == 0) static_for<3>([&](auto p) { bq0[p] = lds[bn + p * SRP * 4]; });
+        else static_for<3>([&](auto p) { bq1[p] = lds[bn + p * SRP * 4]; });
+      }
+    });
+    __builtin_amdgcn_sched_barrier(0);
+    if (flags & 4) __builtin_amdgcn_s_setprio(0);
+    // the next step's weights must have landed; at a group's first step the strip (issued after
+    // them) may stay in flight for two more steps
+    if (KX == 0 && more_s) {
+      if (ns_units == SUW) vm_wait<SUW>();
+      else vm_wait<SUW - 1>();
+    } else {
+      vm_wait<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // groups (cb outer, ky inner): the three tap rows of one chunk read neighbouring input rows
+  const int ng = 3 * CB;
+  issue_s(0, 0, 0);
+  issue_w(0, 0, 0);
+  vm_wait<0>();
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  using Z = std::integral_constant<int, 0>;
+  using O = std::integral_constant<int, 1>;
+  using K0 = std::integral_constant<int, 0>;
+  using K1 = std::integral_constant<int, 1>;
+  using K2 = std::integral_constant<int, 2>;
+  // weight slot of step st = 3 g + kx is st & 1: unroll by 2 groups (6 steps) for compile-time slots
+  auto group = [&](auto gs_c, auto w0_c, int g) {
+    constexpr int W0 = decltype(w0_c)::value;
+    const int ky = g % 3, cb = g / 3;
+    const int gn = g + 1;
+    const bool more_s = gn < ng;
+    const int nky = gn % 3, ncb = gn / 3;
+    step(gs_c, std::integral_constant<int, W0>{}, K0{}, ky, cb, true, ky * 3 + 1, cb, more_s, nky, ncb);
+    step(gs_c, std::integral_constant<int, W0 ^ 1>{}, K1{}, ky, cb, true, ky * 3 + 2, cb, more_s, nky, ncb);
+    step(gs_c, std::integral_constant<int, W0>{}, K2{}, ky, cb, more_s, nky * 3, ncb, more_s, nky, ncb);
+  };
+  for (int g = 0; g < ng; g += 2) {
+    group(Z{}, Z{}, g);  // steps 6k, 6k+1, 6k+2: weight slots 0, 1, 0
+    if (g + 1 >= ng) break;
+    group(O{}, O{}, g + 1);  // steps 6k+3..6k+5: weight slots 1, 0, 1
+  }
+  (void)nw_units;
+  conv3_epilogue<WC, WP>(A, S, acc, p0, c0, wc, wp, lane, M, GHW, flags);
+}
+
+
+static int env_int(const char* name) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : 0;
+}
+
+int conv3_tc(const zp_conv_args& a) { return a.Cout > 64 ? 128 : (a.Cout > 32 ? 64 : 32); }
+
+// k_conv3 tiles (4 waves, one per SIMD; tools/conv3_ab.py): 128 x 256 for 128-channel tiles, 64 x 128
+// (register-pipelined, 3-deep ring) for 64-channel tiles, 32 x 128 for the head.
+int conv3_tp(const zp_conv_args& a, int tc) {
+  static const int sched = env_int("ZP_CONV3_SCHED");
+  if (tc == 128) return sched == 1 ? 128 : 256;  // 8-wave ping-pong 128 x 256, or the pipelined 128 x 128
+  return 128;
+}
+
+// k_conv3s eligibility: a 3x3 stride-1 same-size conv (one sub, the tap grid rows outer) on W 32 /
+// 64 / 128 with whole-row 256-pixel tiles inside one image, 64- or 128-channel cout tiles, and a
+// strip of TR x (W + 2 pad) <= 288 rows (layer5's dilation 4 at 32 x 32 needs 320: k_conv3).
+// ZP_CONV3_STRIP=0 disables, =2 also takes the 128-channel tiles.
+static int g_conv3_strip = -1;  // zp_conv_tuning key 7 (-1: ZP_CONV3_STRIP or the default 1)
+
+int conv3_strip_mode(int v) {
+  const int old = g_conv3_strip;
+  g_conv3_strip = v;
+  return old;
+}
+
+static bool conv3_strip(const zp_conv_args& a, int tc, strip3_geo* sg) {
+  static const int env = getenv("ZP_CONV3_STRIP") ? env_int("ZP_CONV3_STRIP") : 1;
+  const int en = g_conv3_strip >= 0 ? g_conv3_strip : env;
+  // 128-channel tiles: k_conv3 (measured 2% faster than k_conv3s<4> on up1/up2, g13 logs) unless
+  // ZP_CONV3_STRIP=2; 64-channel tiles: k_conv3s<2> (1.32x on layer1)
+  if (!en || a.nsub != 1 || (tc != 128 && tc != 64) || a.Cout % tc != 0 || a.Cin % 32 != 0) return false;
+  if (tc == 128 && en != 2) return false;
+  if (a.sy != 1 || a.sx != 1 || a.GH != a.IH || a.GW != a.IW) return false;
+  const zp_conv_sub& S = a.sub[0];
+  if (S.ntaps != 9 || S.oys != 1 || S.oxs != 1 || S.oyo != 0 || S.oxo != 0 || S.OH != a.GH || S.OW != a.GW)
+    return false;
+  const int ty0 = S.ty[0], tx0 = S.tx[0], dty = S.ty[3] - S.ty[0], dtx = S.tx[1] - S.tx[0];
+  for (int t = 0; t < 9; ++t)
+    if (S.ty[t] != ty0 + (t / 3) * dty || S.tx[t] != tx0 + (t % 3) * dtx) return false;
+  if (tx0 > 0 || tx0 + 2 * dtx < 0 || dtx < 0 || dty < 0) return false;
+  const int W = a.GW;
+  if (W != 32 && W != 64 && W != 128) return false;
+  if (((long)a.GH * a.GW) % 256 != 0) return false;
+  const int pad = max(-tx0, tx0 + 2 * dtx);  // left halo = -tx0; the strip spans [tx0, W - 1 + tx0 + 2 dtx]
+  const int SW = W + 2 * dtx;
+  const int TR = 256 / W, SR = TR * SW;
+  if (SR > 288) return false;
+  if (sg) {
+    sg->W = W;
+    sg->TR = TR;
+    sg->SW = SW;
+    sg->SR = SR;
+    sg->ty0 = ty0;
+    sg->dty = dty;
+    sg->tx0 = tx0;
+    sg->dtx = dtx;
+    sg->pad = pad;
+  }
+  return true;
+}
+
+int conv3_launch(const zp_conv_args& a, hipStream_t st, int fl) {
+  ZP_CHECK_ARG(a.Cin > 0 && a.Cin % 32 == 0, "zp_conv2d: ZP_F32X3 needs Cin %% 32 == 0 (got %d; the stem runs in f32 "
+               "with out_mode ZP_OUT_NHWC_X3)", a.Cin);
+  ZP_CHECK_ARG(a.ldx >= a.cx0 + a.Cin && a.cx0 % 8 == 0 && a.ldx % 8 == 0, "zp_conv2d: bad ldx/cx0");
+  ZP_CHECK_ARG(a.k_pad % 32 == 0, "zp_conv2d: k_pad %d not a multiple of 32", a.k_pad);
+  ZP_CHECK_ARG(!a.stats, "zp_conv2d: ZP_F32X3 is forward (eval) only: no train-mode statistics");
+  ZP_CHECK_ARG(a.out_mode == ZP_OUT_NHWC || a.out_mode == ZP_OUT_HEAD_NCHW,
+               "zp_conv2d: ZP_F32X3 writes split NHWC (ZP_OUT_NHWC) or the f32 head (ZP_OUT_HEAD_NCHW)");
+  const int tc = conv3_tc(a);
+  ZP_CHECK_ARG(a.w_rows % tc == 0 && a.w_rows >= a.Cout, "zp_conv2d: w_rows %d", a.w_rows);
+  for (int s = 0; s < a.nsub; ++s) {
+    const zp_conv_sub& S = a.sub[s];
+    ZP_CHECK_ARG(S.w && S.y, "zp_conv2d: sub %d null w/y", s);
+    ZP_CHECK_ARG(S.ntaps >= 1 && S.ntaps <= ZP_MAX_TAPS && (long)S.ntaps * a.Cin <= a.k_pad,
+                 "zp_conv2d: sub %d ntaps %d / k_pad %d", s, S.ntaps, a.k_pad);
+    if (a.out_mode == ZP_OUT_NHWC)
+      ZP_CHECK_ARG(S.ldy >= S.cy0 + a.Cout && S.cy0 % 4 == 0 && S.ldy % 4 == 0, "zp_conv2d: bad ldy/cy0");
+    else
+      ZP_CHECK_ARG(S.y2 || a.Cout == 1, "zp_conv2d: head needs y2");
+    // the epilogue's plane strides assume every sub writes the same output tensor shape
+    ZP_CHECK_ARG(S.OH == a.sub[0].OH && S.OW == a.sub[0].OW, "zp_conv2d: ZP_F32X3 subs must share the output shape");
+  }
+  if (a.res) ZP_CHECK_ARG(a.ldr >= a.cr0 + a.Cout && a.cr0 % 4 == 0 && a.ldr % 4 == 0, "zp_conv2d: bad residual ld");
+  conv_taps tg{};
+  const long long xb = 3ll * a.N * a.IH * a.IW * a.ldx * 2;
+  const long long wb = 3ll * a.w_rows * a.k_pad * 2;
+  ZP_CHECK_ARG(xb < (1ll << 31) && wb < (1ll << 31),
+               "zp_conv2d: split input (%lld B) / weights (%lld B) must stay below 2 GiB per launch (split the batch)",
+               xb, wb);
+  tg.x_bytes = (unsigned)xb;
+  for (int s = 0; s < a.nsub; ++s) {
+    const zp_conv_sub& S = a.sub[s];
+    tg.w_bytes[s] = (unsigned)wb;
+    int nx = 1;
+    while (nx < S.ntaps && S.ty[nx] == S.ty[0]) ++nx;
+    const int ny = S.ntaps / nx;
+    tg.ny[s] = ny;
+    tg.nx[s] = nx;
+    tg.ty0[s] = S.ty[0];
+    tg.tx0[s] = S.tx[0];
+    tg.dty[s] = ny > 1 ? S.ty[nx] - S.ty[0] : 0;
+    tg.dtx[s] = nx > 1 ? S.tx[1] - S.tx[0] : 0;
+    bool grid = ny * nx == S.ntaps && ny <= 32 && nx <= 32;
+    for (int t = 0; grid && t < S.ntaps; ++t)
+      grid = S.ty[t] == tg.ty0[s] + (t / nx) * tg.dty[s] && S.tx[t] == tg.tx0[s] + (t % nx) * tg.dtx[s];
+    ZP_CHECK_ARG(grid, "zp_conv2d: sub %d taps must form a (row x column) grid of at most 32 x 32, rows outer", s);
+  }
+  strip3_geo s3{};
+  if (conv3_strip(a, tc, &s3)) {
+    s3.x_bytes = tg.x_bytes;
+    s3.w_bytes = tg.w_bytes[0];
+    const dim3 sgrid((unsigned)(((long)a.N * a.GH * a.GW) / 256), (unsigned)(a.Cout / tc), 1);
+    if (tc == 128) hipLaunchKernelGGL((k_conv3s<4>), sgrid, dim3(512), 0, st, a, s3, fl);
+    else hipLaunchKernelGGL((k_conv3s<2>), sgrid, dim3(512), 0, st, a, s3, fl);
+    ZP_LAUNCH_CHECK("zp_conv2d split-f32 strip");
+    return ZP_OK;
+  }
+  const int tp = conv3_tp(a, tc);
+  const int gx = ceil_div((long)a.N * a.GH * a.GW, tp), gy = ceil_div(a.Cout, tc);
+  const dim3 grid(gx, gy, a.nsub);
+  // schedule (ZP_CONV3_SCHED, tools/conv3_ab.py): register-pipelined one-wave-per-SIMD tiles over
+  // 128 pixels (128- / 64- / 32-channel), 3-deep ring; ZP_CONV3_SCHED=1: the 128-channel tile with
+  // a 2-deep ring
+  static const int sched = env_int("ZP_CONV3_SCHED");
+  if (tc == 128 && tp == 256) hipLaunchKernelGGL((k_conv3<4, 4, 4, 2, false>), grid, dim3(512), 0, st, a, tg, fl);
+  else if (tc == 128) hipLaunchKernelGGL((k_conv3<4, 4, 2, 2, true>), grid, dim3(256), 0, st, a, tg, fl);
+  else if (tc == 64) hipLaunchKernelGGL((k_conv3<2, 4, 2, 2, true>), grid, dim3(256), 0, st, a, tg, fl);
+  else hipLaunchKernelGGL((k_conv3<1, 4, 2, 2, true>), grid, dim3(256), 0, st, a, tg, fl);
+  ZP_LAUNCH_CHECK("zp_conv2d split-f32");
+  return ZP_OK;
+}
+
+
+bool conv3_strip_ok(const zp_conv_args& a, int tc) { return conv3_strip(a, tc, nullptr); }
+
+}  // namespace zp

@@ -316,7 +316,9 @@ class Engine:
         tc, tp, stages, var = C.c_int(), C.c_int(), C.c_int(), C.c_int()
         L.call("zp_conv2d_config", C.byref(a), C.byref(tc), C.byref(tp), C.byref(stages), C.byref(var))
         tn = _TN[dt]
-        if var.value == 4:  # rocprofv3 name: k_conv3<WC, NWP>
+        if var.value == 5:  # rocprofv3 name: k_conv3s<WC>
+            return f"k_conv3s<WC={tc.value // 32}>"
+        if var.value == 4:  # rocprofv3 name: k_conv3<WC, WP, NWP, ST, PIPE>
             return f"k_conv3<WC={tc.value // 32},NWP={tp.value // 64}>"
         if var.value == 1:  # rocprofv3 name: k_conv_strip<T, WC, STAGES, SPW = 5>
             return f"k_conv_strip<{tn},WC={tc.value // 32},ST=3>"
