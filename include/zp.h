@@ -131,7 +131,9 @@ int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* stages, int* 
  * weight-gradient kernel's workgroup rounds (default 1; 0 = a ~1024-workgroup target); key 6 = the
  * fewest workgroups the four-phase kernel (k_conv_quad) runs with (default 256); key 7 = the
  * split-fp32 strip kernel k_conv3s (0 off, 1 64-channel tiles, 2 also 128-channel tiles; -1 =
- * ZP_CONV3_STRIP or the default 1).  Returns the previous value, -1 for an unknown key. */
+ * ZP_CONV3_STRIP or the default 1); key 8 = the fewest workgroups a split-fp32 launch runs
+ * 128-channel tiles with (fewer: 64-channel tiles).  Returns the previous value, -1 for an
+ * unknown key. */
 int zp_conv_tuning(int key, int value);
 
 /* Pack an f32 weight tensor src[d0][d1][kh][kw] into dst[rows_pad][k_pad] (dtype), taps

@@ -93,10 +93,13 @@ def test_forward_bf16_within_conditioning_band(net_and_state, golden):
     net.set_precision("fp32")
     for got, ref in ((m.cpu().numpy(), f["fwd64_mask"]), (c.cpu().numpy(), f["fwd64_code"])):
         rel = np.linalg.norm(got - ref) / np.linalg.norm(ref)
-        assert rel <= 0.25, rel
         out = np.abs(ref) > 0.25
         agree = ((got > THR) == (ref > THR))[out].mean()
-        assert agree >= 0.90, agree
+        print(f"bf16 @64: rel-L2 {rel:.4g}, bits agree {agree:.4f} outside |ref| <= 0.25")
+        # observed (r03, every box so far: deterministic kernels): rel-L2 0.160 / 0.118, bits 0.9975 /
+        # 0.9981 (mask / code); bound = observed + ~25%
+        assert rel <= 0.20, rel
+        assert agree >= 0.99, agree
 
 
 def test_forward_fp16_within_conditioning_band(net_and_state, golden):

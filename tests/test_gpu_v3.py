@@ -54,7 +54,9 @@ def test_v3_forward_bf16_within_band(v3, golden):
         print(f"v3 bf16 {key}: rel-L2 {rel:.3g}, bits agree {agree:.4f} outside |ref| <= 0.25")
         # 256x256 with BN calibrated on two crops conditions worse than the 64x64 main-network
         # fixture (rel-L2 0.16 there); test_main_network_bf16_at_256 below is the main-network analogue
-        assert rel <= 0.5 and agree >= 0.85, (key, rel, agree)
+        # observed (r03): rel-L2 0.309 / 0.207 / 0.191, bits 0.944 / 0.970 / 0.969 (mask / entire /
+        # code); bound = observed + ~25%
+        assert rel <= 0.38 and agree >= 0.93, (key, rel, agree)
 
 
 def test_main_network_bf16_at_256(golden):
@@ -75,7 +77,8 @@ def test_main_network_bf16_at_256(golden):
         rel = np.linalg.norm(got - ref) / np.linalg.norm(ref)
         agree = ((got > THR) == (ref > THR))[np.abs(ref) > 0.25].mean()
         print(f"main bf16 @256 {key}: rel-L2 {rel:.3g}, bits agree {agree:.4f} outside |ref| <= 0.25")
-        assert rel <= 0.35 and agree >= 0.90, (key, rel, agree)
+        # observed (r03): rel-L2 0.255 / 0.188, bits 0.981 / 0.989 (mask / code); bound = observed + ~25%
+        assert rel <= 0.32 and agree >= 0.97, (key, rel, agree)
 
 
 def test_v3_rejects_other_input_sizes(v3):

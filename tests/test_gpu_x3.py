@@ -96,9 +96,17 @@ def _gid(g):
     return f"{g[0]}{g[1]}-{g[2]}k{g[3]}s{g[4]}d{g[6]}h{g[8]}"
 
 
+@pytest.mark.parametrize("min_blocks", [0, 256], ids=["tile_by_cout", "small_grid_64"])
 @pytest.mark.parametrize("geom", GEOMS, ids=[_gid(g) for g in GEOMS])
-def test_split_conv_is_f32_accurate(gpu, geom):
-    _check_geom(gpu, geom)
+def test_split_conv_is_f32_accurate(gpu, geom, min_blocks):
+    """min_blocks = zp_conv_tuning key 8: 0 keeps the 128-channel tiles at these small batches,
+    256 (the default) moves launches of < 256 workgroups to 64-channel tiles."""
+    from zebrapose_amd import _lib as L
+    old = L.lib.zp_conv_tuning(8, min_blocks)
+    try:
+        _check_geom(gpu, geom)
+    finally:
+        L.lib.zp_conv_tuning(8, old)
 
 
 @pytest.mark.parametrize("mode", [0, 1, 2])
@@ -106,10 +114,12 @@ def test_split_conv_is_f32_accurate(gpu, geom):
 def test_split_strip_kernel(gpu, geom, mode):
     from zebrapose_amd import _lib as L
     old = L.lib.zp_conv_tuning(7, mode)
+    old_mb = L.lib.zp_conv_tuning(8, 0)  # the cout tile by Cout alone
     try:
         variant = _check_geom(gpu, geom)
     finally:
         L.lib.zp_conv_tuning(7, old)
+        L.lib.zp_conv_tuning(8, old_mb)
     cout, H = geom[2], geom[8]
     tc = 128 if cout > 64 else 64
     strip = (mode == 2 or (mode == 1 and tc == 64)) and H * H >= 256

@@ -18,6 +18,8 @@ LAYERS = {  # name: (kind, cin, cout, k, d, hw)
     "up2T": ("convT", 320, 256, 3, 1, 64),
     "up1conv": ("conv", 256, 256, 3, 1, 64),
     "l1": ("conv", 64, 64, 3, 1, 64),
+    "l2": ("conv", 128, 128, 3, 1, 32),
+    "l4": ("conv", 256, 256, 3, 2, 32),
 }
 
 
@@ -28,12 +30,15 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--strip", type=int, default=-1, help="zp_conv_tuning key 7 (k_conv3s: 0 off, 1, 2)")
+    ap.add_argument("--minblocks", default="0", help="zp_conv_tuning key 8 values to A/B (comma list)")
     a = ap.parse_args()
     from zebrapose_amd import _lib as L
     from zebrapose_amd.engine import Engine, Unit, Act
     from zebrapose_amd.model import layers as LY
     dev = torch.device("cuda", 0)
     flags = [int(f) for f in a.flags.split(",")]
+    L.lib.zp_conv_tuning(7, a.strip)
     res = {}
     setups = []
     for name in a.layers.split(","):
@@ -52,9 +57,13 @@ def main():
         taps = 9 if kind == "conv" else 9 / 4 * 4  # convT: 4 phases x 9/4 taps over the input grid
         fl = 2.0 * a.batch * hw * hw * (9 if kind == "conv" else 9) * cin * cout
         setups.append((name, eng, unit, Act(xs), y, fl))
+    mbs = [int(m) for m in a.minblocks.split(",")]
     for r in range(a.rounds):
-        for f in flags:
-            L.lib.zp_conv_tuning(1, f)
+        for f0 in flags:
+          for mb in mbs:
+            L.lib.zp_conv_tuning(1, f0)
+            L.lib.zp_conv_tuning(8, mb)
+            f = (f0, mb)
             for name, eng, unit, x, y, fl in setups:
                 for _ in range(2):
                     eng.unit_fwd(unit, x, y, None)
@@ -68,10 +77,11 @@ def main():
                 us = e0.elapsed_time(e1) * 1e3 / a.iters
                 res.setdefault((name, f), []).append(us)
     L.lib.zp_conv_tuning(1, -1)
+    L.lib.zp_conv_tuning(8, 256)
     for (name, f), v in sorted(res.items()):
         fl = [s[5] for s in setups if s[0] == name][0]
         us = min(v)
-        print(f"{name:8s} flags {f:6d}: {us:9.1f} us  {fl / us * 1e-6:7.1f} TFLOP/s  ({fl / us * 1e-6 / 419.43:.3f} of x3 peak)")
+        print(f"{name:8s} flags {f[0]:6d} minblocks {f[1]:4d}: {us:9.1f} us  {fl / us * 1e-6:7.1f} TFLOP/s  ({fl / us * 1e-6 / 419.43:.3f} of x3 peak)")
 
 
 if __name__ == "__main__":

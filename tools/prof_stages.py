@@ -36,6 +36,9 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 from prof_summary import bench_label  # noqa: E402
 
 PEAK = {"bf16": 2516.6, "fp32": 157.3}
+# the fp32 eval forward runs the split-fp32 engine (six bf16 MFMA products per f32 MAC): its
+# ceiling is the bf16 peak / 6; frac_of_peak for fp32 stays against the f32 MFMA peak (157.3)
+PEAK_SPLIT = 2516.6 / 6
 STAGES = ["stem", "layer1", "layer2", "layer4", "layer5", "aspp", "up1", "up2", "head", "decode"]
 
 
@@ -177,6 +180,8 @@ def summarise(name, d, prec):
             "gflop": round(d["flops"] / 1e9, 2),
             "tflops": round(d["flops"] / t / 1e12, 1) if t and d["flops"] else None,
             "frac_of_peak": round(d["flops"] / t / 1e12 / PEAK[prec], 3) if t and d["flops"] else None,
+            "frac_of_split_ceiling": (round(d["flops"] / t / 1e12 / PEAK_SPLIT, 3) if prec == "fp32" and t and d["flops"]
+                                      else None),
             "mfma_busy_pct": None if busy is None else round(busy, 1),
             "hbm_mb": round((d["read"] + d["write"]) / 1e6, 1),
             "algo_mb": round(d["algo_bytes"] / 1e6, 1),
@@ -186,11 +191,15 @@ def summarise(name, d, prec):
 
 def md(tab):
     p = tab["precision"]
-    out = [f"### R34 inference bs={tab['batch']}, {p} (libzp {tab['lib_sha16']})", "",
-           "| stage | dispatches | us | GFLOP | TFLOP/s | frac of peak | MFMA busy % | HBM MB (algorithmic) | HBM GB/s |",
-           "|---|---|---|---|---|---|---|---|---|"]
+    x3 = p == "fp32"
+    peak = ("frac of f32 MFMA peak 157.3 | frac of split ceiling 419.4" if x3 else "frac of bf16 peak 2516.6")
+    out = [f"### R34 inference bs={tab['batch']}, {p}{' (split-fp32 engine)' if x3 else ''} (libzp {tab['lib_sha16']})",
+           "",
+           f"| stage | dispatches | us | GFLOP | TFLOP/s | {peak} | MFMA busy % | HBM MB (algorithmic) | HBM GB/s |",
+           "|---|---|---|---|---|---|---|---|---|" + ("---|" if x3 else "")]
     for r in tab["stages"]:
-        out.append(f"| {r['stage']} | {r['dispatches']} | {r['us']} | {r['gflop']} | {r['tflops']} | {r['frac_of_peak']} "
+        fr = f"{r['frac_of_peak']} | {r.get('frac_of_split_ceiling')}" if x3 else f"{r['frac_of_peak']}"
+        out.append(f"| {r['stage']} | {r['dispatches']} | {r['us']} | {r['gflop']} | {r['tflops']} | {fr} "
                    f"| {r['mfma_busy_pct']} | {r['hbm_mb']} ({r['algo_mb']}) | {r['hbm_gbps']} |")
     return "\n".join(out) + "\n"
 

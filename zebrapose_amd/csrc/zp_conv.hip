@@ -2257,7 +2257,7 @@ static int strip_tc(const zp_conv_args& a) {
   return 128;
 }
 static int conv_tc(const zp_conv_args& a) {
-  if (a.dtype == ZP_F32X3) return a.Cout > 64 ? 128 : (a.Cout > 32 ? 64 : 32);  // k_conv3
+  if (a.dtype == ZP_F32X3) return conv3_tc(a);  // k_conv3 / k_conv3s
   if (quad_plan(a, nullptr)) return 64;  // k_conv_quad: 64 channels x 4 phases
   // strip-eligible layers take k_conv_strip's 128-channel tile: it stages fewer bytes per FLOP than
   // the 256-channel k_conv tile, and a 256-channel strip tile does not fit the register file
@@ -2374,8 +2374,8 @@ static bool quad_plan(const zp_conv_args& a, quad_geo* qg) {
 // 32x32 layers where it leaves part of the chip idle (fewer workgroups, but 2x the MFMA work
 // per LDS byte and deeper prefetch)
 static int conv_tp(const zp_conv_args& a) {
+  if (a.dtype == ZP_F32X3) return conv3_tp(a, conv3_tc(a));
   int tc = a.Cout > 64 ? 128 : (a.Cout > 32 ? 64 : 32);
-  if (a.dtype == ZP_F32X3) return conv3_tp(a, tc);
   if (tc == 32) return 128;  // 32 + 256 rows do not split over 8 waves in 8-row groups
   if (strip_eligible(a, nullptr) || quad_plan(a, nullptr)) return 256;
   if (conv_tc(a) == 256) return 256;  // the 256-channel tile exists only with 256-pixel tiles
@@ -2770,8 +2770,9 @@ extern "C" int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* st
  * workgroup rounds over the CUs (default 1); key 5: k_wgrad_lds's workgroup rounds (default 1; 0 =
  * the older ~1024-workgroup target padded to a multiple of 8); key 6: the fewest workgroups
  * k_conv_quad runs with (default 256); key 7: split-fp32 strip kernel k_conv3s (0 off, 1 the
- * 64-channel tiles, 2 also the 128-channel tiles; -1 = ZP_CONV3_STRIP / default 1).  Returns the
- * previous value. */
+ * 64-channel tiles, 2 also the 128-channel tiles; -1 = ZP_CONV3_STRIP / default 1); key 8: the
+ * fewest workgroups a split-fp32 launch runs 128-channel tiles with (fewer: 64-channel tiles).
+ * Returns the previous value. */
 extern "C" int zp_conv_tuning(int key, int value) {
   if (key == 0) {
     const int old = g_tc256_min_blocks;
@@ -2804,6 +2805,7 @@ extern "C" int zp_conv_tuning(int key, int value) {
     return old;
   }
   if (key == 7) return conv3_strip_mode(value);
+  if (key == 8) return conv3_min_blocks(value);
   if (key == 4) {
     const int old = g_wgrad2_rounds;
     g_wgrad2_rounds = value > 0 ? value : 1;

@@ -765,7 +765,27 @@ static int env_int(const char* name) {
   return v ? atoi(v) : 0;
 }
 
-int conv3_tc(const zp_conv_args& a) { return a.Cout > 64 ? 128 : (a.Cout > 32 ? 64 : 32); }
+// zp_conv_tuning key 8.  256 (one workgroup per CU): layer2's 128 -> 128 3x3 at 32 x 32, bs 32
+// (128 workgroups of 128 x 256) 107 -> 75 us on 64-channel strip tiles; 512 / 1024 also move
+// layer4 / layer5 (256 / 512 workgroups) and slow them, 198 -> 248 / 715 -> 1450 us (g16 logs)
+static int g_conv3_min_blocks = 256;
+
+int conv3_min_blocks(int v) {
+  const int old = g_conv3_min_blocks;
+  g_conv3_min_blocks = v;
+  return old;
+}
+
+// cout tile: 128 / 64 / 32 by Cout; a launch whose 128 x 256 grid would leave CUs idle (fewer
+// workgroups than zp_conv_tuning key 8) takes 64-channel tiles instead (twice the workgroups)
+int conv3_tc(const zp_conv_args& a) {
+  const int tc = a.Cout > 64 ? 128 : (a.Cout > 32 ? 64 : 32);
+  if (tc == 128 && g_conv3_min_blocks > 0) {
+    const long blocks = (((long)a.N * a.GH * a.GW + 255) / 256) * ((a.Cout + 127) / 128) * a.nsub;
+    if (blocks < g_conv3_min_blocks) return 64;
+  }
+  return tc;
+}
 
 // k_conv3 tiles (4 waves, one per SIMD; tools/conv3_ab.py): 128 x 256 for 128-channel tiles, 64 x 128
 // (register-pipelined, 3-deep ring) for 64-channel tiles, 32 x 128 for the head.
