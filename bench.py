@@ -43,13 +43,18 @@ sys.path.insert(0, ROOT)
 os.environ.setdefault("ZP_QUIET", "1")
 
 PEAK = {"bf16": 2516.6, "fp32": 157.3}  # TFLOP/s dense MFMA (256 CU x 4 SIMD x 2.4 GHz; MI355X_MICROARCH.md)
-# The split-fp32 kernel (k_conv3, include/zp.h ZP_F32X3) forms each f32 product from 6 bf16 MFMA
-# products: its MFMA ceiling in f32 FLOP/s is the dense bf16 peak / 6.
+# The split-fp32 kernels (k_conv3 / k_conv3s, include/zp.h) form each f32 product from 6 bf16 MFMA
+# products (ZP_F32X3) or 3 fp16 ones (ZP_F32H2): their MFMA ceiling in f32 FLOP/s is the dense
+# 16-bit peak / 6 or / 3 (bf16 and fp16 MFMAs take the same cycles).
 PEAK_X3 = PEAK["bf16"] / 6.0
+PEAK_H2 = PEAK["bf16"] / 3.0
 
 
 def peak_of(kname, precision):
     """(peak TFLOP/s, basis) for the dominant kernel instance."""
+    if kname.startswith("k_conv3") and "<h2" in kname:
+        return PEAK_H2, ("split-fp32 kernel (two fp16 planes): dense fp16 MFMA peak 2516.6 / 3 fp16 products "
+                         "per f32 MAC (f32 MFMA peak 157.3)")
     if kname.startswith("k_conv3"):  # k_conv3 / k_conv3s
         return PEAK_X3, ("split-fp32 kernel: dense bf16 MFMA peak 2516.6 / 6 bf16 products per f32 MAC "
                          "(f32 MFMA peak 157.3)")

@@ -59,12 +59,20 @@ extern "C" {
  * 2^-23 |a b| (f32's own product rounding is 2^-24), i.e. f32-accurate convolutions at 6/16 of the
  * f32-MFMA cost.  Forward (eval) kernels only. */
 #define ZP_F32X3 3
+/* fp32 in the two-plane fp16 split form (eval-mode inference), laid out like ZP_F32X3 with TWO
+ * planes [2][...] of IEEE fp16: hi = fp16(v), lo = fp16((v - hi) * 2^11), v = hi + lo * 2^-11 to
+ * 22 significant bits (|error| <= 2^-23 |v| in fp16's normal range; |v| must stay below 65504).
+ * zp_conv2d forms a*b from hi*hi + (hi*lo + lo*hi) * 2^-11 on fp16 MFMAs (the dropped lo*lo term is
+ * below 2^-22 |a b|): 3 MFMAs and 2 staged planes per product instead of ZP_F32X3's 6 and 3.
+ * Forward (eval) kernels only. */
+#define ZP_F32H2 4
 
 /* zp_conv_args.out_mode */
 #define ZP_OUT_NHWC 0       /* y[n, oy, ox, cy0 + c] (ldy elements per pixel), dtype of the call */
 #define ZP_OUT_HEAD_NCHW 1  /* c == 0 -> y (f32 [N,1,OH,OW]); c >= 1 -> y2 (f32 [N,Cout-1,OH,OW]) */
 #define ZP_OUT_NHWC_F32 2   /* y f32 NHWC regardless of dtype (raw conv output for train-mode BN) */
 #define ZP_OUT_NHWC_X3 3    /* y = plane 0 of a ZP_F32X3 NHWC tensor (an f32 call writing split output) */
+#define ZP_OUT_NHWC_H2 4    /* y = plane 0 of a ZP_F32H2 NHWC tensor (an f32 call writing split output) */
 
 #define ZP_MAX_TAPS 64
 #define ZP_MAX_SUB 4

@@ -224,7 +224,7 @@ def test_bf16_bench_geometry_end_to_end(setup):
         np.testing.assert_array_equal(res[b][1], p3d)
 
 
-@pytest.mark.parametrize("split", [True, False], ids=["split_f32", "f32_mfma"])
+@pytest.mark.parametrize("split", ["x3", "h2", False], ids=["split_x3", "split_h2", "f32_mfma"])
 def test_fp32_bench_geometry(setup, split):
     """fp32 mode at bs=32 -- the benched headline: the split-fp32 eval engine (ZP_F32X3, the
     default), and the exact-f32-MFMA engine: logits of crops 0, 13, 31 within the north-star 1e-3 of
@@ -266,7 +266,7 @@ def test_fp32_bench_geometry(setup, split):
     net.set_precision("bf16")
 
 
-@pytest.mark.parametrize("split", [True, False], ids=["split_f32", "f32_mfma"])
+@pytest.mark.parametrize("split", ["x3", "h2", False], ids=["split_x3", "split_h2", "f32_mfma"])
 def test_fp32_matches_reference_fixture_256(golden, split):
     """The reference's own 256x256 forward (B=2, BN calibrated at 256x256 -- r34_fwd256.npz) through
     the fp32 HIP path (split-fp32 eval engine and exact-f32 MFMA) within the north-star 1e-3."""

@@ -39,7 +39,7 @@ def _bits_check(got, ref, band):
 
 # (fixture, keys, atol): the 64x64 fixture has logits up to 5.1 -> atol 1e-3 (observed 1.2e-4).
 # The 256x256 fixture (BN calibrated at 256x256) is checked in test_gpu_bench_geometry.py.
-@pytest.mark.parametrize("split", [True, False], ids=["split_f32", "f32_mfma"])
+@pytest.mark.parametrize("split", ["x3", "h2", False], ids=["split_x3", "split_h2", "f32_mfma"])
 @pytest.mark.parametrize("fixture,xkey,mkey,ckey,atol",
                          [("r34_fwd64.npz", "fwd64_x", "fwd64_mask", "fwd64_code", 1e-3)])
 def test_forward_fp32_matches_reference(net_and_state, golden, fixture, xkey, mkey, ckey, atol, split):
@@ -59,7 +59,7 @@ def test_forward_fp32_matches_reference(net_and_state, golden, fixture, xkey, mk
         assert amb <= 0.01 * ref.size  # the ambiguous band itself (reported, tiny)
 
 
-@pytest.mark.parametrize("split", [True, False], ids=["split_f32", "f32_mfma"])
+@pytest.mark.parametrize("split", ["x3", "h2", False], ids=["split_x3", "split_h2", "f32_mfma"])
 def test_r50_forward_fp32_matches_reference(golden, split):
     """ResNet50_OS8 + ASPP_50 (340M parameters; Bottleneck stem/layer1/layer2, 1024/2048-channel
     BasicBlock layer4/5, 2048-channel ASPP, 512-channel up2 input) through the HIP path, fp32 mode

@@ -45,8 +45,17 @@ def _ref64(kind, conv, bn, x, res, relu, s, p, d):
     return F.relu(y) if relu else y
 
 
-def _split_act(t, dev):
-    """f32 NHWC host tensor -> plane-0 view of its exact 3-plane bf16 split on the device."""
+def _split_act(t, dev, form="x3"):
+    """f32 NHWC host tensor -> plane-0 view of its split on the device: x3 = the exact 3-plane bf16
+    split; h2 = fp16 hi + fp16 (residual * 2^11) (22 significant bits)."""
+    if form == "h2":
+        h = t.half()
+        lo = ((t - h.float()) * 2048.0).half()
+        planes = torch.stack([h, lo]).to(dev)
+        j = planes[0].float() + planes[1].float() / 2048.0
+        # 22 significant bits down to fp16's normal range; below it (|t| < 2^-14) an absolute 2^-36
+        assert ((j - t.to(dev)).abs() <= 2.0 ** -22 * t.to(dev).abs() + 2.0 ** -36).all()
+        return planes[0]
     h = t.to(torch.bfloat16)
     r = t - h.float()
     m = r.to(torch.bfloat16)
@@ -54,6 +63,12 @@ def _split_act(t, dev):
     planes = torch.stack([h, m, lo]).to(dev)
     assert torch.equal((planes[0].float() + planes[1].float()) + planes[2].float(), t.to(dev))
     return planes[0]
+
+
+FORMS = ["x3", "h2"]
+# split error vs float64 <= MULT x the exact-f32 kernel's + FLOOR x scale: x3 is f32-accurate (2x);
+# h2 stores 22 significant bits (its input / output rounding alone is 2^-23 relative)
+BOUND = {"x3": (2.0, 2.0 ** -24), "h2": (4.0, 2.0 ** -21)}
 
 
 def test_split_weight_pack_is_exact(gpu):
@@ -96,27 +111,53 @@ def _gid(g):
     return f"{g[0]}{g[1]}-{g[2]}k{g[3]}s{g[4]}d{g[6]}h{g[8]}"
 
 
+def test_h2_weight_pack(gpu):
+    """ZP_F32H2 packing: fp16 hi = RNE(w), lo = RNE((w - hi) * 2^11); joined within 2^-22 relative
+    (fp16's normal range), the hi plane equal to the fp16 cast of the f32 pack."""
+    from zebrapose_amd import _lib as L
+    from zebrapose_amd.engine import _i32arr
+    g = torch.Generator().manual_seed(3)
+    w = (torch.randn(96, 40, 3, 3, generator=g) * 0.05).to(gpu)
+    w[0, 0] = 0.0
+    rows, kp = 128, 9 * 64
+    out = torch.empty((2, rows, kp), dtype=torch.float16, device=gpu)
+    ky = [t // 3 for t in range(9)]
+    kx = [t % 3 for t in range(9)]
+    L.call("zp_pack_weight", w.data_ptr(), 96, 40, 3, 3, 0, 9, _i32arr(ky), _i32arr(kx), 64, L.ZP_F32H2,
+           out.data_ptr(), rows, kp, L.stream_ptr())
+    ref = torch.empty((rows, kp), dtype=torch.float32, device=gpu)
+    L.call("zp_pack_weight", w.data_ptr(), 96, 40, 3, 3, 0, 9, _i32arr(ky), _i32arr(kx), 64, L.ZP_F32,
+           ref.data_ptr(), rows, kp, L.stream_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(out[0], ref.half())
+    assert torch.equal(out[1], ((ref - out[0].float()) * 2048.0).half())
+    joined = out[0].float() + out[1].float() / 2048.0
+    assert ((joined - ref).abs() <= 2.0 ** -22 * ref.abs() + 2.0 ** -36).all()
+
+
+@pytest.mark.parametrize("form", FORMS)
 @pytest.mark.parametrize("min_blocks", [0, 256], ids=["tile_by_cout", "small_grid_64"])
 @pytest.mark.parametrize("geom", GEOMS, ids=[_gid(g) for g in GEOMS])
-def test_split_conv_is_f32_accurate(gpu, geom, min_blocks):
+def test_split_conv_is_f32_accurate(gpu, geom, min_blocks, form):
     """min_blocks = zp_conv_tuning key 8: 0 keeps the 128-channel tiles at these small batches,
     256 (the default) moves launches of < 256 workgroups to 64-channel tiles."""
     from zebrapose_amd import _lib as L
     old = L.lib.zp_conv_tuning(8, min_blocks)
     try:
-        _check_geom(gpu, geom)
+        _check_geom(gpu, geom, form)
     finally:
         L.lib.zp_conv_tuning(8, old)
 
 
+@pytest.mark.parametrize("form", FORMS)
 @pytest.mark.parametrize("mode", [0, 1, 2])
 @pytest.mark.parametrize("geom", STRIP_GEOMS, ids=[_gid(g) for g in STRIP_GEOMS])
-def test_split_strip_kernel(gpu, geom, mode):
+def test_split_strip_kernel(gpu, geom, mode, form):
     from zebrapose_amd import _lib as L
     old = L.lib.zp_conv_tuning(7, mode)
     old_mb = L.lib.zp_conv_tuning(8, 0)  # the cout tile by Cout alone
     try:
-        variant = _check_geom(gpu, geom)
+        variant = _check_geom(gpu, geom, form)
     finally:
         L.lib.zp_conv_tuning(7, old)
         L.lib.zp_conv_tuning(8, old_mb)
@@ -126,7 +167,7 @@ def test_split_strip_kernel(gpu, geom, mode):
     assert variant == (5 if strip else 4), (variant, mode)
 
 
-def _check_geom(gpu, geom):
+def _check_geom(gpu, geom, form="x3"):
     """Split vs exact-f32-MFMA error against float64; returns the launch variant (zp_conv2d_config)."""
     from zebrapose_amd import _lib as L
     from zebrapose_amd.engine import Engine, Unit, Act, joined
@@ -156,9 +197,9 @@ def _check_geom(gpu, geom):
     out = {}
     for mode in ("x3", "f32"):
         if mode == "x3":
-            eng = Engine(torch.nn.Module(), torch.float32, x3=True)
-            xa = Act(_split_act(xh, gpu))
-            ra = None if rh is None else Act(_split_act(rh, gpu))
+            eng = Engine(torch.nn.Module(), torch.float32, split=form)
+            xa = Act(_split_act(xh, gpu, form))
+            ra = None if rh is None else Act(_split_act(rh, gpu, form))
             oa = Act(eng._empty((B, OH, OW, cout), gpu))
         else:
             eng = Engine(torch.nn.Module(), torch.float32)
@@ -177,12 +218,15 @@ def _check_geom(gpu, geom):
     e32 = (out["f32"] - ref).abs().max().item()
     r3 = (out["x3"] - ref).pow(2).mean().sqrt().item()
     r32 = (out["f32"] - ref).pow(2).mean().sqrt().item()
-    print(f"{geom}: max|d| split {e3:.3g} f32-MFMA {e32:.3g}; rms split {r3:.3g} f32-MFMA {r32:.3g} (scale {scale:.3g})")
-    assert e3 <= 2.0 * e32 + 2.0 ** -24 * scale, (e3, e32, scale)
+    print(f"{geom} {form}: max|d| split {e3:.3g} f32-MFMA {e32:.3g}; rms split {r3:.3g} f32-MFMA {r32:.3g} "
+          f"(scale {scale:.3g})")
+    mult, floor = BOUND[form]
+    assert e3 <= mult * e32 + floor * scale, (e3, e32, scale)
     return variant
 
 
-def test_split_head_nchw(gpu):
+@pytest.mark.parametrize("form", FORMS)
+def test_split_head_nchw(gpu, form):
     """The head conv (1x1, 320 -> 17, bias, no BN) on the 32-channel tile writing f32 NCHW mask / code."""
     from zebrapose_amd.engine import Engine, Unit, Act
     from zebrapose_amd.model import layers as LY
@@ -194,42 +238,52 @@ def test_split_head_nchw(gpu):
     ref = _ref64("conv", conv, None, x, None, False, 1, 0, 1)
     err = {}
     for mode in ("x3", "f32"):
-        eng = Engine(torch.nn.Module(), torch.float32, x3=mode == "x3")
+        eng = Engine(torch.nn.Module(), torch.float32, split=form if mode == "x3" else None)
         xh = x.permute(0, 2, 3, 1).contiguous()
-        xa = Act(_split_act(xh, gpu) if mode == "x3" else xh.to(gpu))
+        xa = Act(_split_act(xh, gpu, form) if mode == "x3" else xh.to(gpu))
         mask = torch.empty(B, 1, H, H, device=gpu)
         code = torch.empty(B, 16, H, H, device=gpu)
         eng.head_fwd(unit, xa, mask, code, None)
         torch.cuda.synchronize()
         err[mode] = (torch.cat([mask, code], 1).double().cpu() - ref).abs().max().item()
     scale = ref.abs().max().item()
-    print(f"head: max|d| split {err['x3']:.3g} f32-MFMA {err['f32']:.3g} (scale {scale:.3g})")
-    assert err["x3"] <= 2.0 * err["f32"] + 2.0 ** -24 * scale, err
+    print(f"head {form}: max|d| split {err['x3']:.3g} f32-MFMA {err['f32']:.3g} (scale {scale:.3g})")
+    mult, floor = BOUND[form]
+    assert err["x3"] <= mult * err["f32"] + floor * scale, err
 
 
-def test_split_pools_and_broadcast(gpu):
+@pytest.mark.parametrize("form", FORMS)
+def test_split_pools_and_broadcast(gpu, form):
+    """Max pool, global average pool and broadcast on split tensors: exactly their f32 definitions
+    on the joined values (the pooled values re-split: x3 exactly; h2 the split of the f32 result)."""
     from zebrapose_amd import _lib as L
-    from zebrapose_amd.engine import joined
+    from zebrapose_amd.engine import joined, SPLIT
     torch.manual_seed(2)
     B, H, C = 2, 17, 64
+    dt = L.ZP_F32X3 if form == "x3" else L.ZP_F32H2
+    npl, tdt, _ = SPLIT[dt]
     x = torch.randn(B, H, H, 80)
-    xa = _split_act(x, gpu)
+    xa = _split_act(x, gpu, form)
+    xj = joined(xa).cpu()  # the values the kernels see (h2: 22-bit)
     st = L.stream_ptr()
     OH = (H - 1) // 2 + 1
-    y = torch.empty((3, B, OH, OH, C), dtype=torch.bfloat16, device=gpu)[0]
-    L.call("zp_maxpool3s2", xa.data_ptr(), B, H, H, 80, 16, C, L.ZP_F32X3, y.data_ptr(), OH, OH, C, 0, st)
-    ref = F.max_pool2d(x[..., 16:16 + C].permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1)
+    y = torch.empty((npl, B, OH, OH, C), dtype=tdt, device=gpu)[0]
+    L.call("zp_maxpool3s2", xa.data_ptr(), B, H, H, 80, 16, C, dt, y.data_ptr(), OH, OH, C, 0, st)
+    ref = F.max_pool2d(xj[..., 16:16 + C].permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1)
     torch.cuda.synchronize()
     assert torch.equal(joined(y).cpu(), ref)
-    pool = torch.empty((3, B, 1, 1, 80), dtype=torch.bfloat16, device=gpu)[0]
-    L.call("zp_global_avgpool", xa.data_ptr(), B, H, H, 80, 0, 80, L.ZP_F32X3, pool.data_ptr(), st)
-    pref = x.double().mean((1, 2)).float().view(B, 1, 1, 80)
+    pool = torch.empty((npl, B, 1, 1, 80), dtype=tdt, device=gpu)[0]
+    L.call("zp_global_avgpool", xa.data_ptr(), B, H, H, 80, 0, 80, dt, pool.data_ptr(), st)
+    pref = xj.double().mean((1, 2)).float().view(B, 1, 1, 80)
     torch.cuda.synchronize()
-    assert torch.equal(joined(pool).cpu(), pref)
-    out = torch.zeros((3, B, 5, 5, 96), dtype=torch.bfloat16, device=gpu)[0]
-    L.call("zp_broadcast_hw", pool.data_ptr(), B, 80, L.ZP_F32X3, out.data_ptr(), 5, 5, 96, 8, st)
+    if form == "x3":
+        assert torch.equal(joined(pool).cpu(), pref)
+    else:  # the f32 mean stored in 22 bits
+        assert ((joined(pool).cpu() - pref).abs() <= 2.0 ** -22 * pref.abs() + 2.0 ** -36).all()
+    out = torch.zeros((npl, B, 5, 5, 96), dtype=tdt, device=gpu)[0]
+    L.call("zp_broadcast_hw", pool.data_ptr(), B, 80, dt, out.data_ptr(), 5, 5, 96, 8, st)
     torch.cuda.synchronize()
-    assert torch.equal(joined(out)[..., 8:88].cpu(), pref.expand(B, 5, 5, 80))
+    assert torch.equal(joined(out)[..., 8:88].cpu(), joined(pool).cpu().expand(B, 5, 5, 80))
 
 
 @pytest.mark.parametrize("cin", [256, 1280])

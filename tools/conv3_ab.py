@@ -31,7 +31,8 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--strip", type=int, default=-1, help="zp_conv_tuning key 7 (k_conv3s: 0 off, 1, 2)")
-    ap.add_argument("--minblocks", default="0", help="zp_conv_tuning key 8 values to A/B (comma list)")
+    ap.add_argument("--form", default="x3", choices=["x3", "h2"])
+    ap.add_argument("--minblocks", default="256", help="zp_conv_tuning key 8 values to A/B (comma list)")
     a = ap.parse_args()
     from zebrapose_amd import _lib as L
     from zebrapose_amd.engine import Engine, Unit, Act
@@ -49,9 +50,9 @@ def main():
             conv = LY.ConvTranspose2d(cin, cout, 3, 2, 1, output_padding=1, bias=False).to(dev)
         bn = LY.BatchNorm2d(cout).to(dev).eval()
         unit = Unit(conv, bn, relu=True)
-        eng = Engine(torch.nn.Module(), torch.float32, x3=True)
+        eng = Engine(torch.nn.Module(), torch.float32, split=a.form)
         xs = eng._empty((a.batch, hw, hw, cin), dev)
-        xs._base.copy_(torch.randn(3, a.batch, hw, hw, cin, device=dev).clamp(min=0).bfloat16())
+        xs._base.copy_(torch.randn(xs._base.shape, device=dev).clamp(min=0).to(xs.dtype))
         OH, OW = unit.out_hw(hw, hw)
         y = Act(eng._empty((a.batch, OH, OW, cout), dev))
         taps = 9 if kind == "conv" else 9 / 4 * 4  # convT: 4 phases x 9/4 taps over the input grid
@@ -81,7 +82,7 @@ def main():
     for (name, f), v in sorted(res.items()):
         fl = [s[5] for s in setups if s[0] == name][0]
         us = min(v)
-        print(f"{name:8s} flags {f[0]:6d} minblocks {f[1]:4d}: {us:9.1f} us  {fl / us * 1e-6:7.1f} TFLOP/s  ({fl / us * 1e-6 / 419.43:.3f} of x3 peak)")
+        print(f"{name:8s} flags {f[0]:6d} minblocks {f[1]:4d}: {us:9.1f} us  {fl / us * 1e-6:7.1f} TFLOP/s  ({fl / us * 1e-6 / (2516.6 / (6 if a.form == 'x3' else 3)):.3f} of the {a.form} ceiling)")
 
 
 if __name__ == "__main__":

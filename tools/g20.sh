@@ -1,0 +1,5 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+chk() { rc=$1; echo "$2 rc $rc"; if [ $rc -ge 124 ]; then exit $rc; fi; }
+timeout -k 10 300 python -u tools/h2_debug.py > gpurun_out/g20_dbg.log 2>&1; chk $? dbg

@@ -35,12 +35,13 @@ def bench_label(name):
     m = re.search(r"k_conv_strip2<(unsigned short|_Float16), (\d+), (\d+), (true|false|\d+)>", name)
     if m:
         return f"k_conv_strip2<{tn[m.group(1)]},WC={m.group(2)}>"
-    m = re.search(r"k_conv3s<(\d+)>", name)
+    sp = {"3": "x3", "2": "h2"}  # split-fp32 planes -> engine label
+    m = re.search(r"k_conv3s<(\d+), (\d+)>", name)
     if m:
-        return f"k_conv3s<WC={m.group(1)}>"
-    m = re.search(r"k_conv3<(\d+), (\d+), (\d+), (\d+), (true|false)>", name)
+        return f"k_conv3s<{sp[m.group(1)]},WC={m.group(2)}>"
+    m = re.search(r"k_conv3<(\d+), (\d+), (\d+), (\d+), (\d+), (true|false)>", name)
     if m:
-        return f"k_conv3<WC={m.group(1)},NWP={m.group(3)}>"
+        return f"k_conv3<{sp[m.group(1)]},WC={m.group(2)},NWP={m.group(4)}>"
     m = re.search(r"k_conv_quad<(unsigned short|_Float16), (\d+), (true|false)>", name)
     if m:
         return f"k_conv_quad<{tn[m.group(1)]},W={m.group(2)}>"

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-op accuracy of the two fp32 eval engines (split-fp32 ZP_F32X3 vs exact-f32 MFMA) at the bench
+"""Per-op accuracy of the fp32 eval engines (split-fp32 ZP_F32X3 and ZP_F32H2, exact-f32 MFMA) at the bench
 geometry (R34, bs=32, 256x256, BN calibrated at 256): every traced op of crop 13 replayed in float64
 from the device's own stored (joined) inputs; per op the rms and max error relative to the op's
 rms / max output, side by side; then the end-to-end logits against a float64 forward."""
@@ -27,7 +27,8 @@ def main():
     x = bench_crops().cuda()
     b = 13
     res = {}
-    for split in (True, False):
+    forms = ("x3", "h2", False)
+    for split in forms:
         net.net.f32_split = split
         eng = net.net.eval_engine()
         eng.trace = []
@@ -67,18 +68,21 @@ def main():
                          (d.abs().max() / exp.abs().max()).item(), d.mean().item() / exp.abs().mean().item()))
         eng.trace = None
         res[split] = (rows, m.cpu(), c.cpu())
-    print(f"{'op':48s} {'split rms':>10s} {'f32 rms':>10s} {'split max':>10s} {'f32 max':>10s} {'split bias':>11s} {'f32 bias':>10s}")
-    for a, bb in zip(res[True][0], res[False][0]):
-        print(f"{a[1][:48]:48s} {a[2]:10.3g} {bb[2]:10.3g} {a[3]:10.3g} {bb[3]:10.3g} {a[4]:11.3g} {bb[4]:10.3g}")
+    name = {"x3": "x3", "h2": "h2", False: "f32"}
+    print(f"{'op':44s}" + "".join(f" {name[k] + ' rms':>10s}" for k in forms) + "".join(f" {name[k] + ' max':>10s}" for k in forms)
+          + "".join(f" {name[k] + ' bias':>10s}" for k in forms))
+    for rows in zip(*(res[k][0] for k in forms)):
+        print(f"{rows[0][1][:44]:44s}" + "".join(f" {r[2]:10.3g}" for r in rows) + "".join(f" {r[3]:10.3g}" for r in rows)
+              + "".join(f" {r[4]:10.3g}" for r in rows))
     idx = [0, 13, 31]
     with torch.no_grad():
         sd64 = {k: (v.double() if v.is_floating_point() else v) for k, v in sd.items()}
         dm, dc = ref_cpu.forward(sd64, x.cpu()[idx].double(), 34)
-    for split in (True, False):
+    for split in forms:
         _, m, c = res[split]
-        for name, got, ref in (("mask", m[idx], dm), ("code", c[idx], dc)):
+        for nm, got, ref in (("mask", m[idx], dm), ("code", c[idx], dc)):
             d = got.double() - ref
-            print(f"{'split' if split else 'f32  '} {name}: vs float64 max {d.abs().max().item():.3g} rms "
+            print(f"{name[split]:4s} {nm}: vs float64 max {d.abs().max().item():.3g} rms "
                   f"{d.pow(2).mean().sqrt().item():.3g} mean {d.mean().item():.3g}")
 
 

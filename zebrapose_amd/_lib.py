@@ -14,8 +14,8 @@ import torch  # noqa: F401  (load torch's HIP runtime first; libzp binds to the 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ZP_LIB", os.path.join(_HERE, "libzp.so"))
 
-ZP_F32, ZP_BF16, ZP_F16, ZP_F32X3 = 0, 1, 2, 3
-ZP_OUT_NHWC, ZP_OUT_HEAD_NCHW, ZP_OUT_NHWC_F32, ZP_OUT_NHWC_X3 = 0, 1, 2, 3
+ZP_F32, ZP_BF16, ZP_F16, ZP_F32X3, ZP_F32H2 = 0, 1, 2, 3, 4
+ZP_OUT_NHWC, ZP_OUT_HEAD_NCHW, ZP_OUT_NHWC_F32, ZP_OUT_NHWC_X3, ZP_OUT_NHWC_H2 = 0, 1, 2, 3, 4
 MAX_TAPS, MAX_SUB = 64, 4
 
 vp = C.c_void_p

@@ -54,6 +54,34 @@ __device__ __forceinline__ void split3(float v, bf16_t& h, bf16_t& m, bf16_t& l)
 // (hi + mid) is exact, and the exact total is an f32, so the second add rounds to it
 __device__ __forceinline__ float join3(bf16_t h, bf16_t m, bf16_t l) { return (bf2f(h) + bf2f(m)) + bf2f(l); }
 
+// The two split-fp32 storage forms as NPL planes of 16-bit words (zp.h ZP_F32X3 / ZP_F32H2):
+//   SplitF32<3>: bf16 hi + mid + lo, exact (split3 / join3);
+//   SplitF32<2>: IEEE fp16 hi + lo' with v ~ hi + lo' * 2^-11: hi = RNE(v), lo' = RNE((v - hi) * 2^11)
+//     (the residual is scaled into fp16's normal range; 22 significant bits, |v - join| <= 2^-23 |v|
+//     for |v| in fp16's normal range).  Finite |v| > 65504 rounds hi to infinity (the network's
+//     activations and weights are far below); non-finite values keep lo' = 0.
+// CS: the factor the lo-plane products carry (k_conv3 scales its correction accumulator by it).
+template <int NPL> struct SplitF32;
+template <> struct SplitF32<3> {
+  static constexpr float CS = 1.f;
+  static __device__ __forceinline__ void split(float v, unsigned short (&p)[3]) { split3(v, p[0], p[1], p[2]); }
+  static __device__ __forceinline__ float join(const unsigned short (&p)[3]) { return join3(p[0], p[1], p[2]); }
+};
+template <> struct SplitF32<2> {
+  static constexpr float CS = 1.f / 2048.f;
+  static __device__ __forceinline__ void split(float v, unsigned short (&p)[2]) {
+    const f16_t h = (f16_t)v;
+    const float r = v - (float)h;
+    f16_t l = (f16_t)(r * 2048.f);
+    if (!__builtin_isfinite((float)h)) l = (f16_t)0.f;
+    p[0] = __builtin_bit_cast(unsigned short, h);
+    p[1] = __builtin_bit_cast(unsigned short, l);
+  }
+  static __device__ __forceinline__ float join(const unsigned short (&p)[2]) {
+    return __builtin_fmaf((float)__builtin_bit_cast(f16_t, p[1]), CS, (float)__builtin_bit_cast(f16_t, p[0]));
+  }
+};
+
 template <typename T> struct Elem;
 template <> struct Elem<float> {
   static __device__ __forceinline__ float ld(const float* p) { return *p; }

@@ -190,17 +190,25 @@ __device__ __forceinline__ void conv_epilogue(const zp_conv_args& A, const zp_co
         continue;
       }
       if constexpr (sizeof(T) == 4) {
-        if (A.out_mode == ZP_OUT_NHWC_X3) {  // f32 call writing a ZP_F32X3 tensor (the split-mode stem)
+        if (A.out_mode == ZP_OUT_NHWC_X3 || A.out_mode == ZP_OUT_NHWC_H2) {
+          // f32 call writing a split-fp32 tensor (the split-mode stem)
           const long psy = (long)A.N * S.OH * S.OW * S.ldy;
-          bf16_t* Y = (bf16_t*)S.y + pix * S.ldy + S.cy0 + cf;
+          unsigned short* Y = (unsigned short*)S.y + pix * S.ldy + S.cy0 + cf;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             if (cf + r >= A.Cout) continue;
-            bf16_t h, m, l;
-            split3(v[r], h, m, l);
-            Y[r] = h;
-            Y[r + psy] = m;
-            Y[r + 2 * psy] = l;
+            if (A.out_mode == ZP_OUT_NHWC_X3) {
+              unsigned short q[3];
+              SplitF32<3>::split(v[r], q);
+              Y[r] = q[0];
+              Y[r + psy] = q[1];
+              Y[r + 2 * psy] = q[2];
+            } else {
+              unsigned short q[2];
+              SplitF32<2>::split(v[r], q);
+              Y[r] = q[0];
+              Y[r + psy] = q[1];
+            }
           }
           continue;
         }
@@ -2257,7 +2265,7 @@ static int strip_tc(const zp_conv_args& a) {
   return 128;
 }
 static int conv_tc(const zp_conv_args& a) {
-  if (a.dtype == ZP_F32X3) return conv3_tc(a);  // k_conv3 / k_conv3s
+  if (a.dtype == ZP_F32X3 || a.dtype == ZP_F32H2) return conv3_tc(a);  // k_conv3 / k_conv3s
   if (quad_plan(a, nullptr)) return 64;  // k_conv_quad: 64 channels x 4 phases
   // strip-eligible layers take k_conv_strip's 128-channel tile: it stages fewer bytes per FLOP than
   // the 256-channel k_conv tile, and a 256-channel strip tile does not fit the register file
@@ -2302,7 +2310,7 @@ static int conv_flags() {
 // ZP_CONV_STRIP=0 disables.
 static bool strip_eligible(const zp_conv_args& a, strip_geo* sg) {
   static const int en = getenv("ZP_CONV_STRIP") ? env_int("ZP_CONV_STRIP") : 1;
-  if (!en || a.dtype == ZP_F32 || a.dtype == ZP_F32X3 || a.nsub != 1 || a.Cin % 64 != 0 || a.Cout % 64 != 0)
+  if (!en || a.dtype == ZP_F32 || a.dtype == ZP_F32X3 || a.dtype == ZP_F32H2 || a.nsub != 1 || a.Cin % 64 != 0 || a.Cout % 64 != 0)
     return false;
   if (a.Cout <= 64 && !g_strip_c64) return false;
   if (a.sy != 1 || a.sx != 1 || a.GH != a.IH || a.GW != a.IW) return false;
@@ -2343,7 +2351,7 @@ static bool strip_eligible(const zp_conv_args& a, strip_geo* sg) {
 // enough workgroups to cover the CUs.  qg: the byte offset of each schedule slot's tap.
 static bool quad_plan(const zp_conv_args& a, quad_geo* qg) {
   if (!(conv_flags() & 128)) return false;
-  if (a.dtype == ZP_F32 || a.dtype == ZP_F32X3 || a.nsub != 4 || a.Cin % 64 != 0 || a.Cout % 64 != 0) return false;
+  if (a.dtype == ZP_F32 || a.dtype == ZP_F32X3 || a.dtype == ZP_F32H2 || a.nsub != 4 || a.Cin % 64 != 0 || a.Cout % 64 != 0) return false;
   if (a.sy != 1 || a.sx != 1 || a.GH != a.IH || a.GW != a.IW) return false;
   if (a.GW != 32 && a.GW != 64) return false;
   if (((long)a.GH * a.GW) % 256 != 0) return false;
@@ -2374,7 +2382,7 @@ static bool quad_plan(const zp_conv_args& a, quad_geo* qg) {
 // 32x32 layers where it leaves part of the chip idle (fewer workgroups, but 2x the MFMA work
 // per LDS byte and deeper prefetch)
 static int conv_tp(const zp_conv_args& a) {
-  if (a.dtype == ZP_F32X3) return conv3_tp(a, conv3_tc(a));
+  if (a.dtype == ZP_F32X3 || a.dtype == ZP_F32H2) return conv3_tp(a, conv3_tc(a));
   int tc = a.Cout > 64 ? 128 : (a.Cout > 32 ? 64 : 32);
   if (tc == 32) return 128;  // 32 + 256 rows do not split over 8 waves in 8-row groups
   if (strip_eligible(a, nullptr) || quad_plan(a, nullptr)) return 256;
@@ -2413,12 +2421,13 @@ extern "C" int zp_conv2d_grid(const zp_conv_args* a) {
 extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
   ZP_CHECK_ARG(ap != nullptr, "zp_conv2d: null args");
   const zp_conv_args& a = *ap;
-  ZP_CHECK_ARG(a.dtype == ZP_F32 || a.dtype == ZP_BF16 || a.dtype == ZP_F16 || a.dtype == ZP_F32X3,
+  ZP_CHECK_ARG(a.dtype == ZP_F32 || a.dtype == ZP_BF16 || a.dtype == ZP_F16 || a.dtype == ZP_F32X3 ||
+                   a.dtype == ZP_F32H2,
                "zp_conv2d: bad dtype %d", a.dtype);
   ZP_CHECK_ARG(a.nsub >= 1 && a.nsub <= ZP_MAX_SUB, "zp_conv2d: nsub %d", a.nsub);
   ZP_CHECK_ARG(a.x && a.N > 0 && a.GH > 0 && a.GW > 0 && a.IH > 0 && a.IW > 0 && a.Cout > 0,
                "zp_conv2d: bad geometry");
-  if (a.dtype == ZP_F32X3) return conv3_launch(a, (hipStream_t)stream, conv_flags());
+  if (a.dtype == ZP_F32X3 || a.dtype == ZP_F32H2) return conv3_launch(a, (hipStream_t)stream, conv_flags());
   const int E = a.dtype == ZP_F32 ? 4 : 8, KE = 8 * E;
   const bool smallc = a.Cin < KE;
   ZP_CHECK_ARG(a.Cin > 0 && a.Cin % E == 0 && (smallc || a.Cin % KE == 0),
@@ -2426,7 +2435,7 @@ extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
   ZP_CHECK_ARG(a.ldx >= a.cx0 + a.Cin && a.cx0 % E == 0 && a.ldx % E == 0, "zp_conv2d: bad ldx/cx0");
   ZP_CHECK_ARG(a.k_pad % KE == 0, "zp_conv2d: k_pad %d not a multiple of %d", a.k_pad, KE);
   ZP_CHECK_ARG(a.w_rows % conv_tc(a) == 0 && a.w_rows >= a.Cout, "zp_conv2d: w_rows %d", a.w_rows);
-  ZP_CHECK_ARG((a.out_mode >= 0 && a.out_mode <= 2) || (a.out_mode == ZP_OUT_NHWC_X3 && a.dtype == ZP_F32 && !a.stats),
+  ZP_CHECK_ARG((a.out_mode >= 0 && a.out_mode <= 2) || ((a.out_mode == ZP_OUT_NHWC_X3 || a.out_mode == ZP_OUT_NHWC_H2) && a.dtype == ZP_F32 && !a.stats),
                "zp_conv2d: out_mode %d", a.out_mode);
   ZP_CHECK_ARG(!a.stats || (!a.res && !a.relu && a.out_mode != ZP_OUT_HEAD_NCHW && !a.sub[0].scale &&
                             !a.sub[0].shift),
@@ -2760,7 +2769,7 @@ extern "C" int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* st
   *tc = conv_tc(*a);
   *tp = conv_tp(*a);
   *stages = *tc == 256 ? 2 : conv_stages(*a, *tc);
-  *variant = a->dtype == ZP_F32X3 ? (conv3_strip_ok(*a, *tc) ? 5 : 4) : quad_plan(*a, nullptr) ? 3 : *tc <= 128 && strip_eligible(*a, nullptr) ? ((conv_flags() & 64) ? 2 : 1) : 0;
+  *variant = (a->dtype == ZP_F32X3 || a->dtype == ZP_F32H2) ? (conv3_strip_ok(*a, *tc) ? 5 : 4) : quad_plan(*a, nullptr) ? 3 : *tc <= 128 && strip_eligible(*a, nullptr) ? ((conv_flags() & 64) ? 2 : 1) : 0;
   return ZP_OK;
 }
 

@@ -8,12 +8,24 @@
 
 namespace zp {
 
-// k_conv3 epilogue: BN scale / shift (+ bias), split residual, ReLU, then split NHWC stores (3
-// planes) or the f32 NCHW head split.  acc[i][j] = 4 consecutive output channels x one pixel.
-template <int WC, int WP>
+// s_barrier + a compiler memory fence: the barrier intrinsic does not order memory accesses for
+// the compiler, so a plain (C++) LDS load after it -- the fragment reads of the register-pipelined
+// schedule and of k_conv3s -- could be hoisted above it and read a buffer another wave's LDS-DMA is
+// still filling (seen as wrong 32-pixel groups in ~2% of the head's tiles at bs=32 with the fp16
+// split).  The empty asm with a "memory" clobber pins every later memory access below the barrier.
+__device__ __forceinline__ void block_barrier() {
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// k_conv3 epilogue: BN scale / shift (+ bias), split residual, ReLU, then split NHWC stores (NPL
+// planes, SplitF32<NPL>) or the f32 NCHW head split.  acc[i][j] = 4 consecutive output channels x
+// one pixel.
+template <int NPL, int WC, int WP>
 __device__ __forceinline__ void conv3_epilogue(const zp_conv_args& A, const zp_conv_sub& S, f32x4 (&acc)[WC][WP],
                                                const int p0, const int c0, const int wc, const int wp,
                                                const int lane, const int M, const int GHW, const int flags) {
+  using SP = SplitF32<NPL>;
   const int lr = lane & 15;
   int pn[WP], poy[WP], pox[WP];
   bool pok[WP];
@@ -50,19 +62,31 @@ __device__ __forceinline__ void conv3_epilogue(const zp_conv_args& A, const zp_c
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * sc[r] + sh[r];
       if (A.res) {
-        const bf16_t* R = (const bf16_t*)A.res + pix * A.ldr + A.cr0 + cf;
+        const unsigned short* R = (const unsigned short*)A.res + pix * A.ldr + A.cr0 + cf;
         if (full) {
-          const uint2 h = *(const uint2*)R, m = *(const uint2*)(R + psr), l = *(const uint2*)(R + 2 * psr);
-          const uint32_t hw[2] = {h.x, h.y}, mw[2] = {m.x, m.y}, lw[2] = {l.x, l.y};
+          uint32_t w[NPL][2];
+#pragma unroll
+          for (int p = 0; p < NPL; ++p) {
+            const uint2 q = *(const uint2*)(R + p * psr);
+            w[p][0] = q.x;
+            w[p][1] = q.y;
+          }
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int sft = (r & 1) * 16;
-            v[r] += join3((bf16_t)(hw[r >> 1] >> sft), (bf16_t)(mw[r >> 1] >> sft), (bf16_t)(lw[r >> 1] >> sft));
+            unsigned short q[NPL];
+#pragma unroll
+            for (int p = 0; p < NPL; ++p) q[p] = (unsigned short)(w[p][r >> 1] >> ((r & 1) * 16));
+            v[r] += SP::join(q);
           }
         } else {
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            if (cf + r < A.Cout) v[r] += join3(R[r], R[r + psr], R[r + 2 * psr]);
+            if (cf + r < A.Cout) {
+              unsigned short q[NPL];
+#pragma unroll
+              for (int p = 0; p < NPL; ++p) q[p] = R[r + p * psr];
+              v[r] += SP::join(q);
+            }
         }
       }
       if (A.relu) {
@@ -81,26 +105,48 @@ __device__ __forceinline__ void conv3_epilogue(const zp_conv_args& A, const zp_c
         }
         continue;
       }
-      bf16_t h[4], m[4], l[4];
+      unsigned short q[4][NPL];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) split3(v[r], h[r], m[r], l[r]);
+      for (int r = 0; r < 4; ++r) SP::split(v[r], q[r]);
       if ((flags & 16384) && v[0] != 1.f) continue;  // diagnostic: no stores (unless a value is exactly 1)
-      bf16_t* Y = (bf16_t*)S.y + pix * S.ldy + S.cy0 + cf;
+      unsigned short* Y = (unsigned short*)S.y + pix * S.ldy + S.cy0 + cf;
       if (full) {
-        *(uint2*)Y = make_uint2((uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16));
-        *(uint2*)(Y + psy) = make_uint2((uint32_t)m[0] | ((uint32_t)m[1] << 16), (uint32_t)m[2] | ((uint32_t)m[3] << 16));
-        *(uint2*)(Y + 2 * psy) =
-            make_uint2((uint32_t)l[0] | ((uint32_t)l[1] << 16), (uint32_t)l[2] | ((uint32_t)l[3] << 16));
+#pragma unroll
+        for (int p = 0; p < NPL; ++p)
+          *(uint2*)(Y + p * psy) = make_uint2((uint32_t)q[0][p] | ((uint32_t)q[1][p] << 16),
+                                              (uint32_t)q[2][p] | ((uint32_t)q[3][p] << 16));
       } else {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          if (cf + r < A.Cout) {
-            Y[r] = h[r];
-            Y[r + psy] = m[r];
-            Y[r + 2 * psy] = l[r];
-          }
+          if (cf + r < A.Cout)
+#pragma unroll
+            for (int p = 0; p < NPL; ++p) Y[r + p * psy] = q[r][p];
       }
     }
+  }
+}
+
+// The correction terms of a split product (besides hi*hi, plane 0 x plane 0, into the main
+// accumulator): plane pairs (A[t], B[t]) of (weight, activation)
+template <int NPL> struct Terms;
+template <> struct Terms<3> {  // mid*mid, hi*lo, lo*hi, mid*hi, hi*mid
+  static constexpr int N = 5;
+  static constexpr int A[5] = {1, 0, 2, 1, 0}, B[5] = {1, 2, 0, 0, 1};
+};
+template <> struct Terms<2> {  // hi*lo', lo'*hi (scaled by 2^-11 at the flush)
+  static constexpr int N = 2;
+  static constexpr int A[2] = {0, 1}, B[2] = {1, 0};
+};
+template <int NPL> using SplitMfma = MfmaTraits<std::conditional_t<NPL == 3, bf16_t, f16_t>>;
+
+// acc += c2 * CS (the correction accumulator's flush; CS = 1 for the bf16 split)
+template <int NPL>
+__device__ __forceinline__ void flush_corr(f32x4& acc, const f32x4& c2) {
+  if constexpr (NPL == 3) {
+    acc += c2;
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[r] = __builtin_fmaf(c2[r], SplitF32<NPL>::CS, acc[r]);
   }
 }
 
@@ -134,20 +180,22 @@ __device__ __forceinline__ void conv3_epilogue(const zp_conv_args& A, const zp_c
 //     are read into a second register set while step k's MFMAs run, and the DMA runs ST steps
 //     ahead; per step one counted vmcnt wait + one barrier, no LDS read on the MFMA critical path.
 // ------------------------------------------------------------------------------------
-template <int WC, int WP, int NWP, int ST, bool PIPE>
+template <int NPL, int WC, int WP, int NWP, int ST, bool PIPE>
 __global__ void __launch_bounds__(128 * NWP) k_conv3(const zp_conv_args A, const conv_taps TG, const int flags) {
   constexpr int TC = 32 * WC, TP = 16 * WP * NWP, NW = 2 * NWP;
   constexpr int NTW = TC / 16, NT = (TC + TP) / 16;  // weight tiles / all tiles (16 rows) per plane
-  constexpr int UNITS = 3 * NT;                      // (plane, tile) DMA units per stage
+  constexpr int UNITS = NPL * NT;                    // (plane, tile) DMA units per stage
   constexpr int TPW = (NT + NW - 1) / NW;            // tiles per wave (some waves idle in the last)
-  constexpr int GRP = 3 * TPW;                       // DMA instructions per wave per stage
+  constexpr int GRP = NPL * TPW;                     // DMA instructions per wave per stage
+  using MT = SplitMfma<NPL>;
+  using TM = Terms<NPL>;
   static_assert(ST == 2 || ST == 3, "ring depth");
   static_assert(ST == 2 || NT % NW == 0, "counted vmcnt waits need the same DMA count on every wave");
   static_assert(!PIPE || NW == 4, "the register-pipelined schedule runs one wave per SIMD");
   static_assert(WP == 4 || WP == 8, "pixel fragments per wave");
   __shared__ uint4 lds[ST * UNITS * 64];
   static_assert(ST * UNITS * 1024 <= 160 * 1024, "LDS");
-  static_assert((2 * NT + WC + 3) * 1024 < 65536, "ds_read immediate range");
+  static_assert(((NPL - 1) * NT + WC + 3) * 1024 < 65536, "ds_read immediate range");
   const zp_conv_sub& S = A.sub[blockIdx.z];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -231,7 +279,7 @@ __global__ void __launch_bounds__(128 * NWP) k_conv3(const zp_conv_args A, const
       const int t = wid + NW * k;
       if (t >= NT) continue;
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl) {
+      for (int pl = 0; pl < NPL; ++pl) {
         auto* d = (__attribute__((address_space(3))) void*)&lds[(stage * UNITS + pl * NT + t) * 64];
         if (t < NTW) __builtin_amdgcn_raw_ptr_buffer_load_lds(wrsrc, d, 16, voff[k], pl * psw_b + w_koff, 0, 0);
         else __builtin_amdgcn_raw_ptr_buffer_load_lds(xrsrc, d, 16, voff[k], pl * psx_b, 0, 0);
@@ -281,9 +329,9 @@ __global__ void __launch_bounds__(128 * NWP) k_conv3(const zp_conv_args A, const
   // MFMAs -- the compiler then tracks their lgkmcnt itself (an asm read's destination registers
   // are "written" at issue for the compiler, which may copy them before the data lands)
   const int awo = (wc * WC) * 64 + lane, bwo = (NTW + wp * WP) * 64 + lane;
-  auto read_a = [&](auto s_c, uint4 (&af)[3][WC]) {
+  auto read_a = [&](auto s_c, uint4 (&af)[NPL][WC]) {
     constexpr int s = decltype(s_c)::value;
-    static_for<3>([&](auto p_c) {
+    static_for<NPL>([&](auto p_c) {
       constexpr int p = decltype(p_c)::value;
       static_for<WC>([&](auto i) {
         if constexpr (PIPE) af[p][i] = lds[(s * UNITS + p * NT + i) * 64 + awo];
@@ -291,9 +339,9 @@ __global__ void __launch_bounds__(128 * NWP) k_conv3(const zp_conv_args A, const
       });
     });
   };
-  auto read_b = [&](auto s_c, auto j0_c, auto j1_c, uint4 (&bfr)[3][WP]) {  // pixel fragments [J0, J1)
+  auto read_b = [&](auto s_c, auto j0_c, auto j1_c, uint4 (&bfr)[NPL][WP]) {  // pixel fragments [J0, J1)
     constexpr int s = decltype(s_c)::value, J0 = decltype(j0_c)::value, J1 = decltype(j1_c)::value;
-    static_for<3>([&](auto p_c) {
+    static_for<NPL>([&](auto p_c) {
       constexpr int p = decltype(p_c)::value;
       static_for<J1 - J0>([&](auto jj) {
         if constexpr (PIPE) bfr[p][J0 + jj] = lds[(s * UNITS + p * NT + J0 + jj) * 64 + bwo];
@@ -304,23 +352,22 @@ __global__ void __launch_bounds__(128 * NWP) k_conv3(const zp_conv_args A, const
   using J0c = std::integral_constant<int, 0>;
   using JHc = std::integral_constant<int, WP / 2>;
   using JWc = std::integral_constant<int, WP>;
-  auto read_frags = [&](auto s_c, uint4 (&af)[3][WC], uint4 (&bfr)[3][WP]) {
+  auto read_frags = [&](auto s_c, uint4 (&af)[NPL][WC], uint4 (&bfr)[NPL][WP]) {
     read_a(s_c, af);
     read_b(s_c, J0c{}, JWc{}, bfr);
   };
-  auto mfmas_part = [&](auto j0_c, auto j1_c, const uint4 (&af)[3][WC], const uint4 (&bfr)[3][WP]) {
+  auto mfmas_part = [&](auto j0_c, auto j1_c, const uint4 (&af)[NPL][WC], const uint4 (&bfr)[NPL][WP]) {
     constexpr int J0 = decltype(j0_c)::value, J1 = decltype(j1_c)::value;
-    // terms: mid*mid, hi*lo, lo*hi, mid*hi, hi*mid -> acc2; hi*hi -> acc
-    constexpr int TA[6] = {1, 0, 2, 1, 0, 0}, TB[6] = {1, 2, 0, 0, 1, 0};
+    // the correction terms (Terms<NPL>) -> acc2 / c2; hi*hi -> acc
     if (!abl_mfma && PIPE) {
-      static_for<6>([&](auto t_c) {
+      static_for<TM::N + 1>([&](auto t_c) {
         constexpr int t = decltype(t_c)::value;
 #pragma unroll
         for (int i = 0; i < WC; ++i)
 #pragma unroll
           for (int j = J0; j < J1; ++j) {
-            if constexpr (t < 5) MfmaTraits<bf16_t>::mma(acc2[PIPE ? i : 0][PIPE ? j : 0], af[TA[t]][i], bfr[TB[t]][j]);
-            else MfmaTraits<bf16_t>::mma(acc[i][j], af[TA[t]][i], bfr[TB[t]][j]);
+            if constexpr (t < TM::N) MT::mma(acc2[PIPE ? i : 0][PIPE ? j : 0], af[TM::A[t]][i], bfr[TM::B[t]][j]);
+            else MT::mma(acc[i][j], af[0][i], bfr[0][j]);
           }
       });
     } else if (!abl_mfma) {
@@ -333,32 +380,32 @@ __global__ void __launch_bounds__(128 * NWP) k_conv3(const zp_conv_args A, const
         for (int i = 0; i < WC; ++i)
 #pragma unroll
           for (int jj = 0; jj < HN; ++jj) c2[i][jj] = (f32x4){0.f, 0.f, 0.f, 0.f};
-        static_for<5>([&](auto t_c) {
+        static_for<TM::N>([&](auto t_c) {
           constexpr int t = decltype(t_c)::value;
 #pragma unroll
           for (int i = 0; i < WC; ++i)
 #pragma unroll
-            for (int jj = 0; jj < HN; ++jj) MfmaTraits<bf16_t>::mma(c2[i][jj], af[TA[t]][i], bfr[TB[t]][H0 + jj]);
+            for (int jj = 0; jj < HN; ++jj) MT::mma(c2[i][jj], af[TM::A[t]][i], bfr[TM::B[t]][H0 + jj]);
         });
 #pragma unroll
         for (int i = 0; i < WC; ++i)
 #pragma unroll
-          for (int jj = 0; jj < HN; ++jj) MfmaTraits<bf16_t>::mma(acc[i][H0 + jj], af[0][i], bfr[0][H0 + jj]);
+          for (int jj = 0; jj < HN; ++jj) MT::mma(acc[i][H0 + jj], af[0][i], bfr[0][H0 + jj]);
 #pragma unroll
         for (int i = 0; i < WC; ++i)
 #pragma unroll
-          for (int jj = 0; jj < HN; ++jj) acc[i][H0 + jj] += c2[i][jj];
+          for (int jj = 0; jj < HN; ++jj) flush_corr<NPL>(acc[i][H0 + jj], c2[i][jj]);
       });
     } else {
 #pragma unroll
-      for (int p = 0; p < 3; ++p)
+      for (int p = 0; p < NPL; ++p)
 #pragma unroll
         for (int i = 0; i < WC; ++i)
 #pragma unroll
           for (int j = J0; j < J1; ++j) acc[i][j][0] += __uint_as_float(af[p][i].x ^ bfr[p][j].y);
     }
   };
-  auto mfmas = [&](const uint4 (&af)[3][WC], const uint4 (&bfr)[3][WP]) { mfmas_part(J0c{}, JWc{}, af, bfr); };
+  auto mfmas = [&](const uint4 (&af)[NPL][WC], const uint4 (&bfr)[NPL][WP]) { mfmas_part(J0c{}, JWc{}, af, bfr); };
 
   if constexpr (!PIPE) {
     const bool pingpong = NW == 8 && (flags & 8);
@@ -368,7 +415,7 @@ __global__ void __launch_bounds__(128 * NWP) k_conv3(const zp_conv_args A, const
       constexpr int s = decltype(s_c)::value;
       const bool more = ks + ST - 1 < nK;
       if (more && !abl_dma) issue(ks + ST - 1, (s + ST - 1) % ST);
-      uint4 af[3][WC], bfr[3][WP];
+      uint4 af[NPL][WC], bfr[NPL][WP];
       // the second half of the pixel fragments is read while the first half's MFMAs run (the
       // buffer is not refilled before the barrier that ends this step)
       read_a(s_c, af);
@@ -382,7 +429,7 @@ __global__ void __launch_bounds__(128 * NWP) k_conv3(const zp_conv_args A, const
       };
       if (pingpong) {
         wait_next();
-        __builtin_amdgcn_s_barrier();
+        block_barrier();
         __builtin_amdgcn_sched_barrier(0);
       }
       if (flags & 4) __builtin_amdgcn_s_setprio(1);
@@ -394,7 +441,7 @@ __global__ void __launch_bounds__(128 * NWP) k_conv3(const zp_conv_args A, const
       __builtin_amdgcn_sched_barrier(0);
       if (flags & 4) __builtin_amdgcn_s_setprio(0);
       if (!pingpong) wait_next();
-      __builtin_amdgcn_s_barrier();
+      block_barrier();
       __builtin_amdgcn_sched_barrier(0);
     };
     using I0 = std::integral_constant<int, 0>;
@@ -407,9 +454,9 @@ __global__ void __launch_bounds__(128 * NWP) k_conv3(const zp_conv_args A, const
     } else {
       vm_wait<0>();
     }
-    __builtin_amdgcn_s_barrier();
+    block_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (pingpong && wid >= 4) __builtin_amdgcn_s_barrier();
+    if (pingpong && wid >= 4) block_barrier();
     if constexpr (ST == 3) {
       for (int ks = 0; ks < nK; ks += 3) {
         step(I0{}, ks);
@@ -425,28 +472,35 @@ __global__ void __launch_bounds__(128 * NWP) k_conv3(const zp_conv_args A, const
         step(I1{}, ks + 1);
       }
     }
-    if (pingpong && wid < 4) __builtin_amdgcn_s_barrier();
+    if (pingpong && wid < 4) block_barrier();
   } else {
     // Prologue: the DMA of steps 0 .. ST - 1 (buffer = step), then step 0's fragments.  Step ks
     // (fragments F[ks & 1] loaded): wait for them; wait for step ks + 1's DMA + barrier (buffer
     // (ks + 1) % ST complete; every wave has read buffer ks % ST); issue the DMA of step ks + ST into
     // buffer ks % ST; issue step ks + 1's fragment reads into F[(ks + 1) & 1]; run step ks's MFMAs.
     // two named fragment sets (a [2][3][WC] array of them was demoted to scratch memory)
-    uint4 fa0[3][WC], fb0[3][WP], fa1[3][WC], fb1[3][WP];
+    uint4 fa0[NPL][WC], fb0[NPL][WP], fa1[NPL][WC], fb1[NPL][WP];
     int issued = 0;
     for (int q = 0; q < ST; ++q)
       if (q < nK) {
         issue(q, q);
         ++issued;
       }
-    if (issued == ST) vm_wait<GRP * (ST - 1)>();
-    else vm_wait<0>();
-    __builtin_amdgcn_s_barrier();
+    // counted only when every wave issues the same DMA count per stage (NT % NW == 0): the head's
+    // 10-tile stage (NT = 2 + 8 over 4 waves) gives waves 2 / 3 fewer pieces, and a count of GRP
+    // left their first stage's second tile in flight (wrong 32-pixel groups, fp16 split)
+    if constexpr (NT % NW == 0) {
+      if (issued == ST) vm_wait<GRP * (ST - 1)>();
+      else vm_wait<0>();
+    } else {
+      vm_wait<0>();
+    }
+    block_barrier();
     __builtin_amdgcn_sched_barrier(0);
     using Z0 = std::integral_constant<int, 0>;
     read_frags(Z0{}, fa0, fb0);
-    auto pstep = [&](auto s_c, int ks, uint4 (&ca)[3][WC], uint4 (&cb)[3][WP], uint4 (&na)[3][WC],
-                     uint4 (&nb)[3][WP]) {
+    auto pstep = [&](auto s_c, int ks, uint4 (&ca)[NPL][WC], uint4 (&cb)[NPL][WP], uint4 (&na)[NPL][WC],
+                     uint4 (&nb)[NPL][WP]) {
       constexpr int s = decltype(s_c)::value;
       constexpr int sn = (s + 1) % ST;
       // this wave's reads of buffer s (F[ks]) have landed before the barrier below releases the
@@ -459,7 +513,7 @@ __global__ void __launch_bounds__(128 * NWP) k_conv3(const zp_conv_args A, const
         // ST - 2 of them may stay in flight when they all exist
         if (ks + ST - 1 < nK && !abl_dma) vm_wait<GRP * (ST - 2)>();
         else vm_wait<0>();
-        __builtin_amdgcn_s_barrier();
+        block_barrier();
         __builtin_amdgcn_sched_barrier(0);
         read_frags(std::integral_constant<int, sn>{}, na, nb);
         if (ks + ST < nK && !abl_dma) issue(ks + ST, s);
@@ -497,9 +551,9 @@ __global__ void __launch_bounds__(128 * NWP) k_conv3(const zp_conv_args A, const
 #pragma unroll
     for (int i = 0; i < WC; ++i)
 #pragma unroll
-      for (int j = 0; j < WP; ++j) acc[i][j] += acc2[PIPE ? i : 0][PIPE ? j : 0];
+      for (int j = 0; j < WP; ++j) flush_corr<NPL>(acc[i][j], acc2[PIPE ? i : 0][PIPE ? j : 0]);
   }
-  conv3_epilogue<WC, WP>(A, S, acc, p0, c0, wc, wp, lane, M, GHW, flags);
+  conv3_epilogue<NPL, WC, WP>(A, S, acc, p0, c0, wc, wp, lane, M, GHW, flags);
 }
 
 // ------------------------------------------------------------------------------------
@@ -529,19 +583,19 @@ struct strip3_geo {
   unsigned x_bytes, w_bytes;
 };
 
-template <int WC>
+template <int NPL, int WC>
 __global__ void __launch_bounds__(512) k_conv3s(const zp_conv_args A, const strip3_geo SG, const int flags) {
   constexpr int WP = 4, NW = 8;
   constexpr int TC = 32 * WC, TP = 256;
   constexpr int NTW = TC / 16;                  // weight tiles per plane
   constexpr int SRP = 288;                      // strip rows per plane slot (>= SR, multiple of 16)
   constexpr int SB = SRP / 16;                  // strip row blocks per plane
-  constexpr int SU = 3 * SB;                    // strip DMA units per group
+  constexpr int SU = NPL * SB;                    // strip DMA units per group
   constexpr int SUW = (SU + NW - 1) / NW;       // per wave (the last waves one fewer)
-  constexpr int WU = 3 * NTW;                   // weight DMA units per step
+  constexpr int WU = NPL * NTW;                   // weight DMA units per step
   constexpr int WUW = (WU + NW - 1) / NW;
-  constexpr int WSLOT = 3 * NTW * 1024;         // bytes per weight slot
-  constexpr int SSLOT = 3 * SRP * 64;           // bytes per strip slot
+  constexpr int WSLOT = NPL * NTW * 1024;         // bytes per weight slot
+  constexpr int SSLOT = NPL * SRP * 64;           // bytes per strip slot
   __shared__ uint4 lds[(2 * WSLOT + 2 * SSLOT) / 16];
   static_assert(2 * WSLOT + 2 * SSLOT <= 160 * 1024, "LDS");
   static_assert(2 * WSLOT < 65536 && 2 * SRP * 64 + 4096 < 65536, "ds_read immediate range");
@@ -663,24 +717,25 @@ __global__ void __launch_bounds__(512) k_conv3s(const zp_conv_args A, const stri
     const unsigned R = (unsigned)(b + kx * SG.dtx);
     return (2 * WSLOT + gs * SSLOT) / 16 + (int)(R * 4u + (lch ^ ((R >> 1) & 2u)));
   };
-  constexpr int TA[6] = {1, 0, 2, 1, 0, 0}, TB[6] = {1, 2, 0, 0, 1, 0};
+  using MT = SplitMfma<NPL>;
+  using TM = Terms<NPL>;
   // one pixel fragment j: the five correction products into a flushed accumulator (WC tiles), then
   // hi x hi into acc and the correction added by VALU (k_conv3's numerics)
-  auto frag = [&](auto j_c, const uint4 (&af)[3][WC], const uint4 (&bq)[3]) {
+  auto frag = [&](auto j_c, const uint4 (&af)[NPL][WC], const uint4 (&bq)[NPL]) {
     constexpr int J = decltype(j_c)::value;
     f32x4 c2[WC];
 #pragma unroll
     for (int i = 0; i < WC; ++i) c2[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    static_for<5>([&](auto t_c) {
+    static_for<TM::N>([&](auto t_c) {
       constexpr int t = decltype(t_c)::value;
 #pragma unroll
-      for (int i = 0; i < WC; ++i) MfmaTraits<bf16_t>::mma(c2[i], af[TA[t]][i], bq[TB[t]]);
+      for (int i = 0; i < WC; ++i) MT::mma(c2[i], af[TM::A[t]][i], bq[TM::B[t]]);
     });
 #pragma unroll
-    for (int i = 0; i < WC; ++i) MfmaTraits<bf16_t>::mma(acc[i][J], af[0][i], bq[0]);
+    for (int i = 0; i < WC; ++i) MT::mma(acc[i][J], af[0][i], bq[0]);
 #pragma unroll
     for (int i = 0; i < WC; ++i) {
-      acc[i][J] += c2[i];
+      flush_corr<NPL>(acc[i][J], c2[i]);
       asm volatile("" : "+v"(acc[i][J]));  // keeps the add here (sunk to the next step's use, all
     }                                      // 4 WP correction accumulators would stay live)
   };
@@ -693,15 +748,15 @@ __global__ void __launch_bounds__(512) k_conv3s(const zp_conv_args A, const stri
     constexpr int GS = decltype(gs_c)::value, WS = decltype(ws_c)::value, KX = decltype(kx_c)::value;
     if (more_w) issue_w(WS ^ 1, nt, ncb);
     if (KX == 0 && more_s) issue_s(GS ^ 1, nky, nscb);
-    uint4 af[3][WC], bq0[3], bq1[3];
+    uint4 af[NPL][WC], bq0[NPL], bq1[NPL];
     const int aw = (WS * WSLOT + wc * WC * 1024) / 16 + lane;
-    static_for<3>([&](auto p_c) {
+    static_for<NPL>([&](auto p_c) {
       constexpr int p = decltype(p_c)::value;
       static_for<WC>([&](auto i) { af[p][i] = lds[aw + (p * NTW + i) * 64]; });
     });
     const int b0 = bidx(0, KX, GS), b1 = bidx(1, KX, GS);
-    static_for<3>([&](auto p) { bq0[p] = lds[b0 + p * SRP * 4]; });
-    static_for<3>([&](auto p) { bq1[p] = lds[b1 + p * SRP * 4]; });
+    static_for<NPL>([&](auto p) { bq0[p] = lds[b0 + p * SRP * 4]; });
+    static_for<NPL>([&](auto p) { bq1[p] = lds[b1 + p * SRP * 4]; });
     if (flags & 4) __builtin_amdgcn_s_setprio(1);
     static_for<WP>([&](auto j_c) {
       constexpr int J = decltype(j_c)::value;
@@ -709,8 +764,8 @@ __global__ void __launch_bounds__(512) k_conv3s(const zp_conv_args A, const stri
       else frag(j_c, af, bq1);
       if constexpr (J + 2 < WP) {
         const int bn = bidx(J + 2, KX, GS);
-        if constexpr (J % 2 == 0) static_for<3>([&](auto p) { bq0[p] = lds[bn + p * SRP * 4]; });
-        else static_for<3>([&](auto p) { bq1[p] = lds[bn + p * SRP * 4]; });
+        if constexpr (J % 2 == 0) static_for<NPL>([&](auto p) { bq0[p] = lds[bn + p * SRP * 4]; });
+        else static_for<NPL>([&](auto p) { bq1[p] = lds[bn + p * SRP * 4]; });
       }
     });
     __builtin_amdgcn_sched_barrier(0);
@@ -723,7 +778,7 @@ __global__ void __launch_bounds__(512) k_conv3s(const zp_conv_args A, const stri
     } else {
       vm_wait<0>();
     }
-    __builtin_amdgcn_s_barrier();
+    block_barrier();
     __builtin_amdgcn_sched_barrier(0);
   };
 
@@ -732,7 +787,7 @@ __global__ void __launch_bounds__(512) k_conv3s(const zp_conv_args A, const stri
   issue_s(0, 0, 0);
   issue_w(0, 0, 0);
   vm_wait<0>();
-  __builtin_amdgcn_s_barrier();
+  block_barrier();
   __builtin_amdgcn_sched_barrier(0);
   using Z = std::integral_constant<int, 0>;
   using O = std::integral_constant<int, 1>;
@@ -756,7 +811,7 @@ __global__ void __launch_bounds__(512) k_conv3s(const zp_conv_args A, const stri
     group(O{}, O{}, g + 1);  // steps 6k+3..6k+5: weight slots 1, 0, 1
   }
   (void)nw_units;
-  conv3_epilogue<WC, WP>(A, S, acc, p0, c0, wc, wp, lane, M, GHW, flags);
+  conv3_epilogue<NPL, WC, WP>(A, S, acc, p0, c0, wc, wp, lane, M, GHW, flags);
 }
 
 
@@ -843,14 +898,40 @@ static bool conv3_strip(const zp_conv_args& a, int tc, strip3_geo* sg) {
   return true;
 }
 
+// kernel launches for one split form (NPL planes: 3 = ZP_F32X3, 2 = ZP_F32H2)
+template <int NPL>
+static void conv3_dispatch(const zp_conv_args& a, const conv_taps& tg, int tc, hipStream_t st, int fl) {
+  strip3_geo s3{};
+  if (conv3_strip(a, tc, &s3)) {
+    s3.x_bytes = tg.x_bytes;
+    s3.w_bytes = tg.w_bytes[0];
+    const dim3 sgrid((unsigned)(((long)a.N * a.GH * a.GW) / 256), (unsigned)(a.Cout / tc), 1);
+    if (tc == 128) hipLaunchKernelGGL((k_conv3s<NPL, 4>), sgrid, dim3(512), 0, st, a, s3, fl);
+    else hipLaunchKernelGGL((k_conv3s<NPL, 2>), sgrid, dim3(512), 0, st, a, s3, fl);
+    return;
+  }
+  const int tp = conv3_tp(a, tc);
+  const int gx = ceil_div((long)a.N * a.GH * a.GW, tp), gy = ceil_div(a.Cout, tc);
+  const dim3 grid(gx, gy, a.nsub);
+  // 128-channel layers: 8 waves, 128 x 256, 2-deep ring (two planes: 3-deep, the same LDS);
+  // smaller tiles: register-pipelined one wave per SIMD over 128 pixels (ZP_CONV3_SCHED=1: the
+  // 128-channel tile that way too)
+  constexpr int ST8 = NPL == 2 ? 3 : 2;
+  if (tc == 128 && tp == 256) hipLaunchKernelGGL((k_conv3<NPL, 4, 4, 4, ST8, false>), grid, dim3(512), 0, st, a, tg, fl);
+  else if (tc == 128) hipLaunchKernelGGL((k_conv3<NPL, 4, 4, 2, 2, true>), grid, dim3(256), 0, st, a, tg, fl);
+  else if (tc == 64) hipLaunchKernelGGL((k_conv3<NPL, 2, 4, 2, 2, true>), grid, dim3(256), 0, st, a, tg, fl);
+  else hipLaunchKernelGGL((k_conv3<NPL, 1, 4, 2, 2, true>), grid, dim3(256), 0, st, a, tg, fl);
+}
+
 int conv3_launch(const zp_conv_args& a, hipStream_t st, int fl) {
-  ZP_CHECK_ARG(a.Cin > 0 && a.Cin % 32 == 0, "zp_conv2d: ZP_F32X3 needs Cin %% 32 == 0 (got %d; the stem runs in f32 "
-               "with out_mode ZP_OUT_NHWC_X3)", a.Cin);
+  const int npl = a.dtype == ZP_F32H2 ? 2 : 3;
+  ZP_CHECK_ARG(a.Cin > 0 && a.Cin % 32 == 0, "zp_conv2d: split fp32 needs Cin %% 32 == 0 (got %d; the stem runs in f32 "
+               "with out_mode ZP_OUT_NHWC_X3 / _H2)", a.Cin);
   ZP_CHECK_ARG(a.ldx >= a.cx0 + a.Cin && a.cx0 % 8 == 0 && a.ldx % 8 == 0, "zp_conv2d: bad ldx/cx0");
   ZP_CHECK_ARG(a.k_pad % 32 == 0, "zp_conv2d: k_pad %d not a multiple of 32", a.k_pad);
-  ZP_CHECK_ARG(!a.stats, "zp_conv2d: ZP_F32X3 is forward (eval) only: no train-mode statistics");
+  ZP_CHECK_ARG(!a.stats, "zp_conv2d: split fp32 is forward (eval) only: no train-mode statistics");
   ZP_CHECK_ARG(a.out_mode == ZP_OUT_NHWC || a.out_mode == ZP_OUT_HEAD_NCHW,
-               "zp_conv2d: ZP_F32X3 writes split NHWC (ZP_OUT_NHWC) or the f32 head (ZP_OUT_HEAD_NCHW)");
+               "zp_conv2d: split fp32 writes split NHWC (ZP_OUT_NHWC) or the f32 head (ZP_OUT_HEAD_NCHW)");
   const int tc = conv3_tc(a);
   ZP_CHECK_ARG(a.w_rows % tc == 0 && a.w_rows >= a.Cout, "zp_conv2d: w_rows %d", a.w_rows);
   for (int s = 0; s < a.nsub; ++s) {
@@ -863,12 +944,12 @@ int conv3_launch(const zp_conv_args& a, hipStream_t st, int fl) {
     else
       ZP_CHECK_ARG(S.y2 || a.Cout == 1, "zp_conv2d: head needs y2");
     // the epilogue's plane strides assume every sub writes the same output tensor shape
-    ZP_CHECK_ARG(S.OH == a.sub[0].OH && S.OW == a.sub[0].OW, "zp_conv2d: ZP_F32X3 subs must share the output shape");
+    ZP_CHECK_ARG(S.OH == a.sub[0].OH && S.OW == a.sub[0].OW, "zp_conv2d: split-fp32 subs must share the output shape");
   }
   if (a.res) ZP_CHECK_ARG(a.ldr >= a.cr0 + a.Cout && a.cr0 % 4 == 0 && a.ldr % 4 == 0, "zp_conv2d: bad residual ld");
   conv_taps tg{};
-  const long long xb = 3ll * a.N * a.IH * a.IW * a.ldx * 2;
-  const long long wb = 3ll * a.w_rows * a.k_pad * 2;
+  const long long xb = (long long)npl * a.N * a.IH * a.IW * a.ldx * 2;
+  const long long wb = (long long)npl * a.w_rows * a.k_pad * 2;
   ZP_CHECK_ARG(xb < (1ll << 31) && wb < (1ll << 31),
                "zp_conv2d: split input (%lld B) / weights (%lld B) must stay below 2 GiB per launch (split the batch)",
                xb, wb);
@@ -890,27 +971,8 @@ int conv3_launch(const zp_conv_args& a, hipStream_t st, int fl) {
       grid = S.ty[t] == tg.ty0[s] + (t / nx) * tg.dty[s] && S.tx[t] == tg.tx0[s] + (t % nx) * tg.dtx[s];
     ZP_CHECK_ARG(grid, "zp_conv2d: sub %d taps must form a (row x column) grid of at most 32 x 32, rows outer", s);
   }
-  strip3_geo s3{};
-  if (conv3_strip(a, tc, &s3)) {
-    s3.x_bytes = tg.x_bytes;
-    s3.w_bytes = tg.w_bytes[0];
-    const dim3 sgrid((unsigned)(((long)a.N * a.GH * a.GW) / 256), (unsigned)(a.Cout / tc), 1);
-    if (tc == 128) hipLaunchKernelGGL((k_conv3s<4>), sgrid, dim3(512), 0, st, a, s3, fl);
-    else hipLaunchKernelGGL((k_conv3s<2>), sgrid, dim3(512), 0, st, a, s3, fl);
-    ZP_LAUNCH_CHECK("zp_conv2d split-f32 strip");
-    return ZP_OK;
-  }
-  const int tp = conv3_tp(a, tc);
-  const int gx = ceil_div((long)a.N * a.GH * a.GW, tp), gy = ceil_div(a.Cout, tc);
-  const dim3 grid(gx, gy, a.nsub);
-  // schedule (ZP_CONV3_SCHED, tools/conv3_ab.py): register-pipelined one-wave-per-SIMD tiles over
-  // 128 pixels (128- / 64- / 32-channel), 3-deep ring; ZP_CONV3_SCHED=1: the 128-channel tile with
-  // a 2-deep ring
-  static const int sched = env_int("ZP_CONV3_SCHED");
-  if (tc == 128 && tp == 256) hipLaunchKernelGGL((k_conv3<4, 4, 4, 2, false>), grid, dim3(512), 0, st, a, tg, fl);
-  else if (tc == 128) hipLaunchKernelGGL((k_conv3<4, 4, 2, 2, true>), grid, dim3(256), 0, st, a, tg, fl);
-  else if (tc == 64) hipLaunchKernelGGL((k_conv3<2, 4, 2, 2, true>), grid, dim3(256), 0, st, a, tg, fl);
-  else hipLaunchKernelGGL((k_conv3<1, 4, 2, 2, true>), grid, dim3(256), 0, st, a, tg, fl);
+  if (npl == 2) conv3_dispatch<2>(a, tg, tc, st, fl);
+  else conv3_dispatch<3>(a, tg, tc, st, fl);
   ZP_LAUNCH_CHECK("zp_conv2d split-f32");
   return ZP_OK;
 }

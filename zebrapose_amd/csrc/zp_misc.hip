@@ -93,13 +93,14 @@ __global__ void k_pack(const PackArgs a) {
   }
 }
 
-// ZP_F32X3 packing: the same element map as k_pack, the f32 weight split into three bf16 planes
-// [3][rows_pad][k_pad]
-__global__ void k_pack_x3(const PackArgs a) {
+// split-fp32 packing (ZP_F32X3 / ZP_F32H2): the same element map as k_pack, the f32 weight split
+// into NPL planes [NPL][rows_pad][k_pad] (SplitF32<NPL>)
+template <int NPL>
+__global__ void k_pack_split(const PackArgs a) {
   const long total = (long)a.rows_pad * a.k_pad;
   const int rows = a.transposed ? a.d1 : a.d0;
   const int chans = a.transposed ? a.d0 : a.d1;
-  bf16_t* d = (bf16_t*)a.dst;
+  unsigned short* d = (unsigned short*)a.dst;
   for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
     int r = (int)(e / a.k_pad), k = (int)(e - (long)r * a.k_pad);
     int t = k / a.cstride, c = k - t * a.cstride;
@@ -110,11 +111,10 @@ __global__ void k_pack_x3(const PackArgs a) {
                                 : (((size_t)r * a.d1 + c) * a.kh + ky) * a.kw + kx;
       v = a.src[idx];
     }
-    bf16_t h, m, l;
-    split3(v, h, m, l);
-    d[e] = h;
-    d[e + total] = m;
-    d[e + 2 * total] = l;
+    unsigned short q[NPL];
+    SplitF32<NPL>::split(v, q);
+#pragma unroll
+    for (int p = 0; p < NPL; ++p) d[e + p * total] = q[p];
   }
 }
 
@@ -126,11 +126,14 @@ __global__ void k_pack_x3(const PackArgs a) {
 __device__ __forceinline__ void pack_store(const zp_pack_job& a, int d, float v) {
   if (a.dtype == ZP_F32X3) {  // three planes of rows_pad * k_pad
     const size_t ps = (size_t)a.rows_pad * a.k_pad;
-    bf16_t h, m, l;
-    split3(v, h, m, l);
-    ((bf16_t*)a.dst)[d] = h;
-    ((bf16_t*)a.dst)[d + ps] = m;
-    ((bf16_t*)a.dst)[d + 2 * ps] = l;
+    unsigned short q[3];
+    SplitF32<3>::split(v, q);
+    for (int p = 0; p < 3; ++p) ((unsigned short*)a.dst)[d + p * ps] = q[p];
+  } else if (a.dtype == ZP_F32H2) {  // two planes
+    const size_t ps = (size_t)a.rows_pad * a.k_pad;
+    unsigned short q[2];
+    SplitF32<2>::split(v, q);
+    for (int p = 0; p < 2; ++p) ((unsigned short*)a.dst)[d + p * ps] = q[p];
   } else if (a.dtype == ZP_BF16) ((bf16_t*)a.dst)[d] = f2bf(v);
   else if (a.dtype == ZP_F16) ((f16_t*)a.dst)[d] = (f16_t)v;
   else ((float*)a.dst)[d] = v;
@@ -739,11 +742,12 @@ __global__ void k_maxpool(const T* __restrict__ x, int B, int IH, int IW, int ld
   }
 }
 
-// ZP_F32X3 max pool: the 3x3 window max of the joined f32 values (PyTorch CPU rule), stored split
-// again (the split of a value is unique, so the winner's planes are reproduced exactly).  Planes:
-// x + p * psx, y + p * psy.
-__global__ void k_maxpool_x3(const bf16_t* __restrict__ x, long psx, int B, int IH, int IW, int ldx, int cx0, int C,
-                             bf16_t* __restrict__ y, long psy, int OH, int OW, int ldy, int cy0) {
+// Split-fp32 max pool (NPL planes, SplitF32<NPL>): the 3x3 window max of the joined f32 values
+// (PyTorch CPU rule), stored split again (joining is exact, so the winner's value is reproduced
+// exactly).  Planes: x + p * psx, y + p * psy.
+template <int NPL>
+__global__ void k_maxpool_split(const unsigned short* __restrict__ x, long psx, int B, int IH, int IW, int ldx, int cx0,
+                                int C, unsigned short* __restrict__ y, long psy, int OH, int OW, int ldy, int cy0) {
   const int CV = C / 8;
   const long total = (long)B * OH * OW * CV;
   for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
@@ -762,37 +766,48 @@ __global__ void k_maxpool_x3(const bf16_t* __restrict__ x, long psx, int B, int 
         int ix = ox * 2 - 1 + kx;
         if ((unsigned)ix >= (unsigned)IW) continue;
         const size_t o = (((size_t)b * IH + iy) * IW + ix) * ldx + cx0 + c;
-        const uint4 h = *(const uint4*)(x + o), mm = *(const uint4*)(x + o + psx), l = *(const uint4*)(x + o + 2 * psx);
-        const uint32_t hw[4] = {h.x, h.y, h.z, h.w}, mw[4] = {mm.x, mm.y, mm.z, mm.w}, lw[4] = {l.x, l.y, l.z, l.w};
+        uint32_t w[NPL][4];
+#pragma unroll
+        for (int p = 0; p < NPL; ++p) {
+          const uint4 q = *(const uint4*)(x + o + p * psx);
+          w[p][0] = q.x;
+          w[p][1] = q.y;
+          w[p][2] = q.z;
+          w[p][3] = q.w;
+        }
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           const int s = (i & 1) * 16;
-          const float v = join3((bf16_t)(hw[i >> 1] >> s), (bf16_t)(mw[i >> 1] >> s), (bf16_t)(lw[i >> 1] >> s));
+          unsigned short q[NPL];
+#pragma unroll
+          for (int p = 0; p < NPL; ++p) q[p] = (unsigned short)(w[p][i >> 1] >> s);
+          const float v = SplitF32<NPL>::join(q);
           if (v > m[i] || isnan(v)) m[i] = v;
         }
       }
     }
-    uint32_t o[3][4];
+    uint32_t o[NPL][4];
 #pragma unroll
     for (int i = 0; i < 8; i += 2) {
-      bf16_t h0, m0, l0, h1, m1, l1;
-      split3(m[i], h0, m0, l0);
-      split3(m[i + 1], h1, m1, l1);
-      o[0][i >> 1] = (uint32_t)h0 | ((uint32_t)h1 << 16);
-      o[1][i >> 1] = (uint32_t)m0 | ((uint32_t)m1 << 16);
-      o[2][i >> 1] = (uint32_t)l0 | ((uint32_t)l1 << 16);
-    }
-    bf16_t* yo = y + pix * ldy + cy0 + c;
+      unsigned short q0[NPL], q1[NPL];
+      SplitF32<NPL>::split(m[i], q0);
+      SplitF32<NPL>::split(m[i + 1], q1);
 #pragma unroll
-    for (int p = 0; p < 3; ++p) *(uint4*)(yo + p * psy) = make_uint4(o[p][0], o[p][1], o[p][2], o[p][3]);
+      for (int p = 0; p < NPL; ++p) o[p][i >> 1] = (uint32_t)q0[p] | ((uint32_t)q1[p] << 16);
+    }
+    unsigned short* yo = y + pix * ldy + cy0 + c;
+#pragma unroll
+    for (int p = 0; p < NPL; ++p) *(uint4*)(yo + p * psy) = make_uint4(o[p][0], o[p][1], o[p][2], o[p][3]);
   }
 }
 
-// ZP_F32X3 global average pool: block = (64 channels, image b); the joined values summed in double
-// (CPU adaptive_avg_pool2d's accumulator) over 4 pixel lanes, combined in a fixed order; the f32
-// mean stored split into y [3][B][C]
-__global__ void __launch_bounds__(256) k_avgpool_x3(const bf16_t* __restrict__ x, long psx, int H, int W, int ldx,
-                                                    int cx0, int C, bf16_t* __restrict__ y, long psy) {
+// Split-fp32 global average pool: block = (64 channels, image b); the joined values summed in
+// double (CPU adaptive_avg_pool2d's accumulator) over 4 pixel lanes, combined in a fixed order; the
+// f32 mean stored split into y [NPL][B][C]
+template <int NPL>
+__global__ void __launch_bounds__(256) k_avgpool_split(const unsigned short* __restrict__ x, long psx, int H, int W,
+                                                       int ldx, int cx0, int C, unsigned short* __restrict__ y,
+                                                       long psy) {
   __shared__ double red[4][64];
   const int b = blockIdx.y;
   const long HW = (long)H * W;
@@ -802,18 +817,20 @@ __global__ void __launch_bounds__(256) k_avgpool_x3(const bf16_t* __restrict__ x
   if (c < C)
     for (long p = sl; p < HW; p += 4) {
       const size_t o = ((size_t)b * HW + p) * ldx + cx0 + c;
-      s += (double)join3(x[o], x[o + psx], x[o + 2 * psx]);
+      unsigned short q[NPL];
+#pragma unroll
+      for (int pl = 0; pl < NPL; ++pl) q[pl] = x[o + pl * psx];
+      s += (double)SplitF32<NPL>::join(q);
     }
   red[sl][cl] = s;
   __syncthreads();
   if (threadIdx.x < 64 && c < C) {
     const double t = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
-    bf16_t h, m, l;
-    split3((float)(t / (double)HW), h, m, l);
+    unsigned short q[NPL];
+    SplitF32<NPL>::split((float)(t / (double)HW), q);
     const size_t o = (size_t)b * C + c;
-    y[o] = h;
-    y[o + psy] = m;
-    y[o + 2 * psy] = l;
+#pragma unroll
+    for (int pl = 0; pl < NPL; ++pl) y[o + pl * psy] = q[pl];
   }
 }
 
@@ -1182,7 +1199,7 @@ extern "C" int zp_conv_rows_pad(int Cout) {
 
 extern "C" int zp_pack_weight(const float* src, int d0, int d1, int kh, int kw, int transposed, int ntaps, const int* ky,
                               const int* kx, int cstride, int dtype, void* dst, int rows_pad, int k_pad, void* stream) {
-  ZP_CHECK_ARG(dtype == ZP_F32 || dtype == ZP_BF16 || dtype == ZP_F16 || dtype == ZP_F32X3,
+  ZP_CHECK_ARG(dtype == ZP_F32 || dtype == ZP_BF16 || dtype == ZP_F16 || dtype == ZP_F32X3 || dtype == ZP_F32H2,
                "zp_pack_weight: bad dtype %d", dtype);
   ZP_CHECK_ARG(src && dst && ky && kx, "zp_pack_weight: null pointer");
   ZP_CHECK_ARG(ntaps >= 1 && ntaps <= ZP_MAX_TAPS, "zp_pack_weight: ntaps %d", ntaps);
@@ -1197,7 +1214,9 @@ extern "C" int zp_pack_weight(const float* src, int d0, int d1, int kh, int kw, 
     a.kx[t] = (signed char)kx[t];
   }
   if (dtype == ZP_F32X3)
-    hipLaunchKernelGGL(k_pack_x3, dim3(grid_for((long)rows_pad * k_pad)), dim3(256), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(k_pack_split<3>, dim3(grid_for((long)rows_pad * k_pad)), dim3(256), 0, (hipStream_t)stream, a);
+  else if (dtype == ZP_F32H2)
+    hipLaunchKernelGGL(k_pack_split<2>, dim3(grid_for((long)rows_pad * k_pad)), dim3(256), 0, (hipStream_t)stream, a);
   else
     ZP_BY_DTYPE(dtype, k_pack, dim3(grid_for((long)rows_pad * k_pad)), dim3(256), (hipStream_t)stream, a);
   ZP_LAUNCH_CHECK("zp_pack_weight");
@@ -1375,14 +1394,19 @@ extern "C" int zp_nchw_to_nhwc(const float* x, int B, int C, int H, int W, int c
 
 extern "C" int zp_maxpool3s2(const void* x, int B, int IH, int IW, int ldx, int cx0, int C, int dtype, void* y, int OH,
                              int OW, int ldy, int cy0, void* stream) {
-  if (dtype == ZP_F32X3) {
+  if (dtype == ZP_F32X3 || dtype == ZP_F32H2) {
     ZP_CHECK_ARG(x && y && C % 8 == 0 && cx0 % 8 == 0 && ldx % 8 == 0 && cy0 % 8 == 0 && ldy % 8 == 0,
                  "zp_maxpool3s2: bad args / alignment");
     ZP_CHECK_ARG(OH == (IH - 1) / 2 + 1 && OW == (IW - 1) / 2 + 1, "zp_maxpool3s2: OH/OW");
     const long total = (long)B * OH * OW * (C / 8);
-    hipLaunchKernelGGL(k_maxpool_x3, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
-                       (long)B * IH * IW * ldx, B, IH, IW, ldx, cx0, C, (bf16_t*)y, (long)B * OH * OW * ldy, OH, OW,
-                       ldy, cy0);
+    if (dtype == ZP_F32X3)
+      hipLaunchKernelGGL(k_maxpool_split<3>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream,
+                         (const unsigned short*)x, (long)B * IH * IW * ldx, B, IH, IW, ldx, cx0, C, (unsigned short*)y,
+                         (long)B * OH * OW * ldy, OH, OW, ldy, cy0);
+    else
+      hipLaunchKernelGGL(k_maxpool_split<2>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream,
+                         (const unsigned short*)x, (long)B * IH * IW * ldx, B, IH, IW, ldx, cx0, C, (unsigned short*)y,
+                         (long)B * OH * OW * ldy, OH, OW, ldy, cy0);
     ZP_LAUNCH_CHECK("zp_maxpool3s2");
     return ZP_OK;
   }
@@ -1415,10 +1439,16 @@ extern "C" int zp_maxpool3s2_bwd(const void* x, int ldx, int cx0, const void* dy
 
 extern "C" int zp_global_avgpool(const void* x, int B, int H, int W, int ldx, int cx0, int C, int dtype, void* y,
                                  void* stream) {
-  if (dtype == ZP_F32X3) {  // y: [3][B][C]
+  if (dtype == ZP_F32X3 || dtype == ZP_F32H2) {  // y: [NPL][B][C]
     ZP_CHECK_ARG(x && y && B > 0 && H > 0 && W > 0 && C > 0, "zp_global_avgpool: bad args");
-    hipLaunchKernelGGL(k_avgpool_x3, dim3((C + 63) / 64, B), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
-                       (long)B * H * W * ldx, H, W, ldx, cx0, C, (bf16_t*)y, (long)B * C);
+    if (dtype == ZP_F32X3)
+      hipLaunchKernelGGL(k_avgpool_split<3>, dim3((C + 63) / 64, B), dim3(256), 0, (hipStream_t)stream,
+                         (const unsigned short*)x, (long)B * H * W * ldx, H, W, ldx, cx0, C, (unsigned short*)y,
+                         (long)B * C);
+    else
+      hipLaunchKernelGGL(k_avgpool_split<2>, dim3((C + 63) / 64, B), dim3(256), 0, (hipStream_t)stream,
+                         (const unsigned short*)x, (long)B * H * W * ldx, H, W, ldx, cx0, C, (unsigned short*)y,
+                         (long)B * C);
     ZP_LAUNCH_CHECK("zp_global_avgpool");
     return ZP_OK;
   }
@@ -1444,11 +1474,12 @@ extern "C" int zp_global_avgpool(const void* x, int B, int H, int W, int ldx, in
 
 extern "C" int zp_broadcast_hw(const void* src, int B, int C, int dtype, void* y, int H, int W, int ldy, int cy0,
                                void* stream) {
-  if (dtype == ZP_F32X3) {  // src [3][B][C] -> the three planes of y [3][B, H, W, ldy]
+  if (dtype == ZP_F32X3 || dtype == ZP_F32H2) {  // src [NPL][B][C] -> the planes of y [NPL][B, H, W, ldy]
     ZP_CHECK_ARG(src && y && B > 0 && C > 0 && C % 8 == 0 && ldy % 8 == 0 && cy0 % 8 == 0,
                  "zp_broadcast_hw: bad args / alignment");
     const long total = (long)B * H * W * C;
-    for (int p = 0; p < 3; ++p)
+    const int npl = dtype == ZP_F32X3 ? 3 : 2;
+    for (int p = 0; p < npl; ++p)
       hipLaunchKernelGGL(k_broadcast_vec<bf16_t>, dim3(grid_for(total / 8)), dim3(256), 0, (hipStream_t)stream,
                          (const bf16_t*)src + (long)p * B * C, B, C, (bf16_t*)y + (long)p * B * H * W * ldy, H, W,
                          ldy, cy0);

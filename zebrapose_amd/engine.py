@@ -32,10 +32,14 @@ from . import _lib as L
 from . import geometry as G
 from .model.resnet import TVBottleneck
 
-_KE = {L.ZP_F32: 32, L.ZP_BF16: 64, L.ZP_F16: 64, L.ZP_F32X3: 32}
-_E = {L.ZP_F32: 4, L.ZP_BF16: 8, L.ZP_F16: 8, L.ZP_F32X3: 8}
-_ES = {L.ZP_F32: 4, L.ZP_BF16: 2, L.ZP_F16: 2, L.ZP_F32X3: 6}  # bytes per element (x3: three bf16 planes)
-_TN = {L.ZP_F32: "f32", L.ZP_BF16: "bf16", L.ZP_F16: "f16", L.ZP_F32X3: "x3"}
+_KE = {L.ZP_F32: 32, L.ZP_BF16: 64, L.ZP_F16: 64, L.ZP_F32X3: 32, L.ZP_F32H2: 32}
+_E = {L.ZP_F32: 4, L.ZP_BF16: 8, L.ZP_F16: 8, L.ZP_F32X3: 8, L.ZP_F32H2: 8}
+# bytes per element (x3: three bf16 planes, h2: two fp16 planes)
+_ES = {L.ZP_F32: 4, L.ZP_BF16: 2, L.ZP_F16: 2, L.ZP_F32X3: 6, L.ZP_F32H2: 4}
+_TN = {L.ZP_F32: "f32", L.ZP_BF16: "bf16", L.ZP_F16: "f16", L.ZP_F32X3: "x3", L.ZP_F32H2: "h2"}
+# the split-fp32 storage forms (include/zp.h): dtype code -> (planes, plane element type, the f32
+# call's out_mode that writes it)
+SPLIT = {L.ZP_F32X3: (3, torch.bfloat16, L.ZP_OUT_NHWC_X3), L.ZP_F32H2: (2, torch.float16, L.ZP_OUT_NHWC_H2)}
 
 
 class Act:
@@ -55,12 +59,15 @@ class Act:
 
 
 def joined(buf):
-    """The f32 values of an activation buffer: itself, or -- for an x3 engine's plane-0 view of a
-    [3, ...] bf16 tensor -- (hi + mid) + lo, which is exact (include/zp.h ZP_F32X3)."""
+    """The f32 values of an activation buffer: itself, or -- for a split engine's plane-0 view --
+    (hi + mid) + lo of a [3, ...] bf16 tensor (exact, include/zp.h ZP_F32X3), or hi + lo * 2^-11 of a
+    [2, ...] fp16 tensor (ZP_F32H2)."""
     base = buf._base
-    if buf.dtype == torch.bfloat16 and base is not None and base.dim() == buf.dim() + 1 and base.shape[0] == 3 \
-            and base.data_ptr() == buf.data_ptr():
-        return (base[0].float() + base[1].float()) + base[2].float()
+    if base is not None and base.dim() == buf.dim() + 1 and base.data_ptr() == buf.data_ptr():
+        if buf.dtype == torch.bfloat16 and base.shape[0] == 3:
+            return (base[0].float() + base[1].float()) + base[2].float()
+        if buf.dtype == torch.float16 and base.shape[0] == 2:
+            return base[0].float() + base[1].float() * (1.0 / 2048.0)
     return buf.float()
 
 
@@ -107,15 +114,20 @@ class Tape:
 class Engine:
     """Executes a BinaryCodeNet_Deeplab module tree (zebrapose_amd.model) with libzp."""
 
-    def __init__(self, net, dtype=torch.bfloat16, x3=False):
-        """x3: fp32 in split form (include/zp.h ZP_F32X3): every activation / packed weight is three
-        bf16 planes (hi, mid, lo) summing exactly to the f32 value, and every conv product is formed
-        from its six leading terms on bf16 MFMAs (f32-accurate).  Eval-mode forward only; the
-        fp32 network's training path keeps the exact-f32 MFMA engine."""
+    def __init__(self, net, dtype=torch.bfloat16, x3=False, split=None):
+        """split: fp32 in a split form (include/zp.h), eval-mode forward only -- the fp32 network's
+        training path keeps the exact-f32 MFMA engine:
+          "x3" (x3=True): three bf16 planes (hi, mid, lo) summing exactly to the f32 value, every
+                conv product from its six leading terms on bf16 MFMAs (ZP_F32X3);
+          "h2": two fp16 planes, v = hi + lo * 2^-11 (22 bits), three fp16 MFMA terms (ZP_F32H2)."""
         self._net = weakref.ref(net)
-        self.x3 = x3
-        self.dtype = torch.bfloat16 if x3 else dtype
-        self.dt = L.ZP_F32X3 if x3 else L.dtype_code(dtype)
+        if x3:
+            split = "x3"
+        assert split in (None, "x3", "h2"), split
+        self.split = split
+        self.x3 = split is not None  # any split-fp32 form
+        self.dt = {"x3": L.ZP_F32X3, "h2": L.ZP_F32H2}[split] if split else L.dtype_code(dtype)
+        self.npl, self.dtype, self.split_out = SPLIT[self.dt] if split else (1, dtype, None)
         self._packed = {}
         self._jobs = []  # (cache key, weight, PackJob) of every cached packing, for _prepack
         self._job_table = None
@@ -156,9 +168,9 @@ class Engine:
 
     def _empty(self, shape, dev):
         """An activation buffer of this engine's storage: plane 0 (a [B, H, W, C] view) of a
-        [3, B, H, W, C] bf16 tensor in x3 mode."""
+        [NPL, B, H, W, C] tensor in a split mode."""
         if self.x3:
-            return torch.empty((3,) + tuple(shape), dtype=torch.bfloat16, device=dev)[0]
+            return torch.empty((self.npl,) + tuple(shape), dtype=self.dtype, device=dev)[0]
         return torch.empty(shape, dtype=self.dtype, device=dev)
 
     def _pack(self, unit, sub, transposed, cstride, k_pad, rows, tag, cache=True, dt=None):
@@ -173,12 +185,12 @@ class Engine:
         if hit is not None and hit[0] == ver:
             return hit[1]
         d0, d1 = w.shape[0], w.shape[1]
-        shape = (3, rows, k_pad) if dt == L.ZP_F32X3 else (rows, k_pad)
+        shape = (SPLIT[dt][0], rows, k_pad) if dt in SPLIT else (rows, k_pad)
         if hit is not None and tuple(hit[1].shape) == shape:
             out = hit[1]
         else:
-            tdt = torch.bfloat16 if dt == L.ZP_F32X3 else {L.ZP_F32: torch.float32, L.ZP_BF16: torch.bfloat16,
-                                                             L.ZP_F16: torch.float16}[dt]
+            tdt = SPLIT[dt][1] if dt in SPLIT else {L.ZP_F32: torch.float32, L.ZP_BF16: torch.bfloat16,
+                                                      L.ZP_F16: torch.float16}[dt]
             out = torch.empty(shape, dtype=tdt, device=w.device)
             self._cache_gen += 1
         ky = [t[0] for t in sub.taps]
@@ -297,7 +309,8 @@ class Engine:
             # algorithmic HBM bytes: the input slice and every output read / written once, the
             # packed weights of each sub-problem once (the residual, when fused, read once)
             es = _ES[dt]
-            osz = 4 if out_mode == L.ZP_OUT_HEAD_NCHW else (6 if out_mode == L.ZP_OUT_NHWC_X3 else es)
+            osz = 4 if out_mode == L.ZP_OUT_HEAD_NCHW else (6 if out_mode == L.ZP_OUT_NHWC_X3 else
+                                                            (4 if out_mode == L.ZP_OUT_NHWC_H2 else es))
             mgrid = x.B * plan.GH * plan.GW
             nbytes = (x.P * x.C * es + len(plan.subs) * mgrid * cout * osz
                       + sum(w.numel() * w.element_size() for w in weights) + (0 if res is None else mgrid * cout * es))
@@ -316,10 +329,10 @@ class Engine:
         tc, tp, stages, var = C.c_int(), C.c_int(), C.c_int(), C.c_int()
         L.call("zp_conv2d_config", C.byref(a), C.byref(tc), C.byref(tp), C.byref(stages), C.byref(var))
         tn = _TN[dt]
-        if var.value == 5:  # rocprofv3 name: k_conv3s<WC>
-            return f"k_conv3s<WC={tc.value // 32}>"
-        if var.value == 4:  # rocprofv3 name: k_conv3<WC, WP, NWP, ST, PIPE>
-            return f"k_conv3<WC={tc.value // 32},NWP={tp.value // 64}>"
+        if var.value == 5:  # rocprofv3 name: k_conv3s<NPL, WC>
+            return f"k_conv3s<{tn},WC={tc.value // 32}>"
+        if var.value == 4:  # rocprofv3 name: k_conv3<NPL, WC, WP, NWP, ST, PIPE>
+            return f"k_conv3<{tn},WC={tc.value // 32},NWP={tp.value // 64}>"
         if var.value == 1:  # rocprofv3 name: k_conv_strip<T, WC, STAGES, SPW = 5>
             return f"k_conv_strip<{tn},WC={tc.value // 32},ST=3>"
         if var.value == 3:  # rocprofv3 name: k_conv_quad<T, W>
@@ -358,7 +371,7 @@ class Engine:
             ws, kp, rows = self._fwd_weights(unit, plan, cache=True, dt=L.ZP_F32)
             scale, shift = self._fold(unit)
             outs = [(out.ptr, out.ld, out.c0, OH, OW, scale, shift, None)] * len(plan.subs)
-            self._conv(x, plan, unit.cout, ws, kp, rows, outs, res, unit.relu, out_mode=L.ZP_OUT_NHWC_X3,
+            self._conv(x, plan, unit.cout, ws, kp, rows, outs, res, unit.relu, out_mode=self.split_out,
                        small=(unit.k, unit.d, unit.p), label=label, dt=L.ZP_F32)
             if self.trace is not None:
                 self.trace.append(("conv", unit, x, out, res))

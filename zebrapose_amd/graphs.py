@@ -21,10 +21,10 @@ import torch
 def _engines(net):
     out = []
     for m in net.modules():
-        for name in ("_engine", "_engine_x3"):
-            e = getattr(m, name, None)
-            if e is not None:
-                out.append(e)
+        e = getattr(m, "_engine", None)
+        if e is not None:
+            out.append(e)
+        out.extend(getattr(m, "_engines_split", {}).values())
     return out
 
 

@@ -31,6 +31,9 @@ from ..parallel import finish_grads, grads_sink
 from .aspp import ASPP, ASPP_50
 from .resnet import ResNet34_OS8, ResNet50_OS8
 
+SPLIT_FORMS = ("x3", "h2")  # include/zp.h ZP_F32X3 / ZP_F32H2
+DEFAULT_SPLIT = "h2"  # the fp32 eval forward's split form when f32_split is True
+
 model_urls = {
     "resnet18": "https://download.pytorch.org/models/resnet18-5c106cde.pth",
     "resnet34": "https://download.pytorch.org/models/resnet34-333f7ec4.pth",
@@ -212,20 +215,25 @@ class DeepLabV3(nn.Module):
             raise NotImplementedError("num_resnet_layers must be 34 or 50")
         prec = precision or os.environ.get("ZP_PRECISION", "fp32")
         object.__setattr__(self, "_engine", Engine(self, _PREC[prec]))
-        object.__setattr__(self, "_engine_x3", None)
-        self.f32_split = os.environ.get("ZP_F32_SPLIT", "1") != "0"
+        object.__setattr__(self, "_engines_split", {})
+        env = os.environ.get("ZP_F32_SPLIT", "1")
+        self.f32_split = False if env == "0" else (env if env in SPLIT_FORMS else True)
 
     def set_precision(self, precision):
         object.__setattr__(self, "_engine", Engine(self, _PREC[precision]))
-        object.__setattr__(self, "_engine_x3", None)
+        object.__setattr__(self, "_engines_split", {})
 
     def eval_engine(self):
-        """The engine that runs this network's eval (inference) forward: the split-fp32 engine for
-        precision 'fp32' (unless f32_split is off), else the precision's own engine."""
-        if self._engine.dtype == torch.float32 and self.f32_split:
-            if self._engine_x3 is None:
-                object.__setattr__(self, "_engine_x3", Engine(self, torch.float32, x3=True))
-            return self._engine_x3
+        """The engine that runs this network's eval (inference) forward: for precision 'fp32' the
+        split-fp32 engine of form ``f32_split`` ("x3" / "h2"; True = DEFAULT_SPLIT; False / "off":
+        the exact-f32 MFMA engine), else the precision's own engine."""
+        sp = self.f32_split
+        if self._engine.dtype == torch.float32 and sp and sp != "off":
+            kind = sp if sp in SPLIT_FORMS else DEFAULT_SPLIT
+            eng = self._engines_split.get(kind)
+            if eng is None:
+                eng = self._engines_split[kind] = Engine(self, torch.float32, split=kind)
+            return eng
         return self._engine
 
     @property
