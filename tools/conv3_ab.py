@@ -30,7 +30,7 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--strip", type=int, default=-1, help="zp_conv_tuning key 7 (k_conv3s: 0 off, 1, 2)")
+    ap.add_argument("--strip", default="-1", help="zp_conv_tuning key 7 values to A/B (k_conv3s: 0 off, 1, 2)")
     ap.add_argument("--form", default="x3", choices=["x3", "h2"])
     ap.add_argument("--minblocks", default="256", help="zp_conv_tuning key 8 values to A/B (comma list)")
     a = ap.parse_args()
@@ -39,7 +39,6 @@ def main():
     from zebrapose_amd.model import layers as LY
     dev = torch.device("cuda", 0)
     flags = [int(f) for f in a.flags.split(",")]
-    L.lib.zp_conv_tuning(7, a.strip)
     res = {}
     setups = []
     for name in a.layers.split(","):
@@ -59,12 +58,15 @@ def main():
         fl = 2.0 * a.batch * hw * hw * (9 if kind == "conv" else 9) * cin * cout
         setups.append((name, eng, unit, Act(xs), y, fl))
     mbs = [int(m) for m in a.minblocks.split(",")]
+    strips = [int(m) for m in a.strip.split(",")]
     for r in range(a.rounds):
         for f0 in flags:
           for mb in mbs:
+           for sm in strips:
             L.lib.zp_conv_tuning(1, f0)
             L.lib.zp_conv_tuning(8, mb)
-            f = (f0, mb)
+            L.lib.zp_conv_tuning(7, sm)
+            f = (f0, mb, sm)
             for name, eng, unit, x, y, fl in setups:
                 for _ in range(2):
                     eng.unit_fwd(unit, x, y, None)
@@ -79,10 +81,11 @@ def main():
                 res.setdefault((name, f), []).append(us)
     L.lib.zp_conv_tuning(1, -1)
     L.lib.zp_conv_tuning(8, 256)
+    L.lib.zp_conv_tuning(7, -1)
     for (name, f), v in sorted(res.items()):
         fl = [s[5] for s in setups if s[0] == name][0]
         us = min(v)
-        print(f"{name:8s} flags {f[0]:6d} minblocks {f[1]:4d}: {us:9.1f} us  {fl / us * 1e-6:7.1f} TFLOP/s  ({fl / us * 1e-6 / (2516.6 / (6 if a.form == 'x3' else 3)):.3f} of the {a.form} ceiling)")
+        print(f"{name:8s} flags {f[0]:6d} minblocks {f[1]:4d} strip {f[2]:2d}: {us:9.1f} us  {fl / us * 1e-6:7.1f} TFLOP/s  ({fl / us * 1e-6 / (2516.6 / (6 if a.form == 'x3' else 3)):.3f} of the {a.form} ceiling)")
 
 
 if __name__ == "__main__":

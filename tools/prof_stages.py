@@ -38,7 +38,7 @@ from prof_summary import bench_label  # noqa: E402
 PEAK = {"bf16": 2516.6, "fp32": 157.3}
 # the fp32 eval forward runs the split-fp32 engine (six bf16 MFMA products per f32 MAC): its
 # ceiling is the bf16 peak / 6; frac_of_peak for fp32 stays against the f32 MFMA peak (157.3)
-PEAK_SPLIT = 2516.6 / 6
+PEAK_SPLIT = {"x3": 2516.6 / 6, "h2": 2516.6 / 3}  # three bf16 planes / two fp16 planes
 STAGES = ["stem", "layer1", "layer2", "layer4", "layer5", "aspp", "up1", "up2", "head", "decode"]
 
 
@@ -154,6 +154,9 @@ def stage_table(src, prec):
         k["mfma_busy"] += m[2].get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0)
         k["grbm"] += m[2].get("GRBM_GUI_ACTIVE", 0.0)
     rows = []
+    labels = " ".join(per_kernel)
+    form = "h2" if "k_conv3<h2" in labels or "k_conv3s<h2" in labels else (
+        "x3" if "k_conv3<x3" in labels or "k_conv3s<x3" in labels else None)
     tot = defaultdict(float)
     for s in STAGES + ["other"]:
         d = st[s]
@@ -161,8 +164,8 @@ def stage_table(src, prec):
             continue
         for k, v in d.items():
             tot[k] += v
-        rows.append(summarise(s, d, prec))
-    rows.append(summarise("total", tot, prec))
+        rows.append(summarise(s, d, prec, form))
+    rows.append(summarise("total", tot, prec, form))
     kern = {k: {"launches": int(v["n"]), "us_per_launch": round(v["ns"] / v["n"] / 1e3, 2),
                 "hbm_bytes_per_launch": round((v["read"] + v["write"]) / v["n"]),
                 "read_bytes_per_launch": round(v["read"] / v["n"]), "write_bytes_per_launch": round(v["write"] / v["n"]),
@@ -170,18 +173,18 @@ def stage_table(src, prec):
                 "mfma_busy_pct": round(100.0 * v["mfma_busy"] / (v["grbm"] / 8.0 * 1024.0), 1) if v["grbm"] else None}
             for k, v in per_kernel.items()}
     return {"precision": prec, "batch": log["batch"], "lib_sha16": log["lib_sha16"], "stages": rows,
-            "kernels": kern}
+            "split_form": form, "kernels": kern}
 
 
-def summarise(name, d, prec):
+def summarise(name, d, prec, form=None):
     t = d["ns"] * 1e-9
     busy = 100.0 * d["mfma_busy"] / (d["grbm"] / 8.0 * 1024.0) if d["grbm"] else None
     return {"stage": name, "dispatches": int(d["dispatches"]), "us": round(d["ns"] / 1e3, 1),
             "gflop": round(d["flops"] / 1e9, 2),
             "tflops": round(d["flops"] / t / 1e12, 1) if t and d["flops"] else None,
             "frac_of_peak": round(d["flops"] / t / 1e12 / PEAK[prec], 3) if t and d["flops"] else None,
-            "frac_of_split_ceiling": (round(d["flops"] / t / 1e12 / PEAK_SPLIT, 3) if prec == "fp32" and t and d["flops"]
-                                      else None),
+            "frac_of_split_ceiling": (round(d["flops"] / t / 1e12 / PEAK_SPLIT[form], 3)
+                                      if form and t and d["flops"] else None),
             "mfma_busy_pct": None if busy is None else round(busy, 1),
             "hbm_mb": round((d["read"] + d["write"]) / 1e6, 1),
             "algo_mb": round(d["algo_bytes"] / 1e6, 1),
@@ -191,9 +194,12 @@ def summarise(name, d, prec):
 
 def md(tab):
     p = tab["precision"]
-    x3 = p == "fp32"
-    peak = ("frac of f32 MFMA peak 157.3 | frac of split ceiling 419.4" if x3 else "frac of bf16 peak 2516.6")
-    out = [f"### R34 inference bs={tab['batch']}, {p}{' (split-fp32 engine)' if x3 else ''} (libzp {tab['lib_sha16']})",
+    form = tab.get("split_form")
+    x3 = bool(form)
+    peak = (f"frac of f32 MFMA peak 157.3 | frac of split ceiling {PEAK_SPLIT[form]:.1f}" if x3
+            else "frac of bf16 peak 2516.6")
+    eng = {"x3": " (split-fp32 engine, three bf16 planes)", "h2": " (split-fp32 engine, two fp16 planes)"}.get(form, "")
+    out = [f"### R34 inference bs={tab['batch']}, {p}{eng} (libzp {tab['lib_sha16']})",
            "",
            f"| stage | dispatches | us | GFLOP | TFLOP/s | {peak} | MFMA busy % | HBM MB (algorithmic) | HBM GB/s |",
            "|---|---|---|---|---|---|---|---|---|" + ("---|" if x3 else "")]

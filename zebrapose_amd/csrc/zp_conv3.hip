@@ -916,8 +916,11 @@ static void conv3_dispatch(const zp_conv_args& a, const conv_taps& tg, int tc, h
   // 128-channel layers: 8 waves, 128 x 256, 2-deep ring (two planes: 3-deep, the same LDS);
   // smaller tiles: register-pipelined one wave per SIMD over 128 pixels (ZP_CONV3_SCHED=1: the
   // 128-channel tile that way too)
+  // (flags & 32768: the two-plane tile with the 2-deep ring, A/B)
   constexpr int ST8 = NPL == 2 ? 3 : 2;
-  if (tc == 128 && tp == 256) hipLaunchKernelGGL((k_conv3<NPL, 4, 4, 4, ST8, false>), grid, dim3(512), 0, st, a, tg, fl);
+  if (tc == 128 && tp == 256 && NPL == 2 && (fl & 32768))
+    hipLaunchKernelGGL((k_conv3<NPL, 4, 4, 4, 2, false>), grid, dim3(512), 0, st, a, tg, fl);
+  else if (tc == 128 && tp == 256) hipLaunchKernelGGL((k_conv3<NPL, 4, 4, 4, ST8, false>), grid, dim3(512), 0, st, a, tg, fl);
   else if (tc == 128) hipLaunchKernelGGL((k_conv3<NPL, 4, 4, 2, 2, true>), grid, dim3(256), 0, st, a, tg, fl);
   else if (tc == 64) hipLaunchKernelGGL((k_conv3<NPL, 2, 4, 2, 2, true>), grid, dim3(256), 0, st, a, tg, fl);
   else hipLaunchKernelGGL((k_conv3<NPL, 1, 4, 2, 2, true>), grid, dim3(256), 0, st, a, tg, fl);
