@@ -626,7 +626,41 @@ def run(args):
     torch.cuda.synchronize()
     pnp_ms = e0.elapsed_time(e1) / 5
     pnp_res = {"ms_per_batch": round(pnp_ms, 3), "crops_per_s": round(B / (pnp_ms * 1e-3), 1), "iterations": 150,
-               "correspondences_per_crop": round(n_corr / B)}
+               "correspondences_per_crop": round(n_corr / B),
+               "what": "the random network's decoded correspondences: no RANSAC early termination (worst case)"}
+    # the same on realistic scenes: 32 crops of 7000 correspondences from a known pose (0.5 px
+    # noise, 30% outliers) -- OpenCV's adaptive bound stops RANSAC after ~25 iterations
+    g = torch.Generator().manual_seed(7)
+    ns, HWs = 7000, 7000
+    Kc = torch.tensor([[572.4114, 0.0, 325.2611], [0.0, 573.57043, 242.04899], [0.0, 0.0, 1.0]], dtype=torch.float64)
+    sc_xy = torch.zeros(B, HWs, 2, dtype=torch.int32)
+    sc_xyz = torch.zeros(B, HWs, 3, dtype=torch.float32)
+    for b in range(B):
+        ang = torch.randn(3, generator=g, dtype=torch.float64) * 0.6
+        th = float(ang.norm())
+        kx = torch.tensor([[0, -ang[2], ang[1]], [ang[2], 0, -ang[0]], [-ang[1], ang[0], 0]], dtype=torch.float64) / th
+        Rm = torch.eye(3, dtype=torch.float64) + np.sin(th) * kx + (1 - np.cos(th)) * kx @ kx
+        tv = torch.tensor([0.0, 0.0, 800.0], dtype=torch.float64) + torch.rand(3, generator=g, dtype=torch.float64) * 100 - 50
+        pw = torch.rand(ns, 3, generator=g, dtype=torch.float64) * 120 - 60
+        Xc = pw @ Rm.T + tv
+        uv = torch.stack([Kc[0, 0] * Xc[:, 0] / Xc[:, 2] + Kc[0, 2], Kc[1, 1] * Xc[:, 1] / Xc[:, 2] + Kc[1, 2]], 1)
+        uv = uv + torch.randn(uv.shape, generator=g, dtype=torch.float64) * 0.5
+        outl = torch.rand(ns, generator=g) < 0.3
+        uv[outl] += torch.rand(int(outl.sum()), 2, generator=g, dtype=torch.float64) * 240 - 120
+        sc_xy[b] = uv.round().int()
+        sc_xyz[b] = pw.float()
+    sc = (torch.full((B,), ns, dtype=torch.int32, device=dev), sc_xy.to(dev), sc_xyz.to(dev))
+    pnp(*sc, Kc.numpy())
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(5):
+        r_sc = pnp(*sc, Kc.numpy())
+    e1.record()
+    torch.cuda.synchronize()
+    sc_ms = e0.elapsed_time(e1) / 5
+    pnp_res["scenes"] = {"ms_per_batch": round(sc_ms, 3), "crops_per_s": round(B / (sc_ms * 1e-3), 1),
+                         "correspondences_per_crop": ns, "outliers": 0.3, "success": int(r_sc[2].sum().item()),
+                         "what": "synthetic scenes from a known pose (0.5 px noise, 30% outliers): RANSAC stops early"}
 
     # ------------------------------------------------------------------ device crop pipeline (extra, §8f rank 2)
     from zebrapose_amd.crop import CropPipeline

@@ -118,3 +118,22 @@ def test_pnp_on_decoded_correspondences(gpu):
                                                   bbox, 128, 2, lut_dict, K)
     assert success and tv.shape == (3, 1)
     np.testing.assert_allclose(rot, Rg[0].cpu().numpy(), atol=1e-12)
+
+
+def test_pnp_chunked_scan_is_the_one_pass_scan(gpu, monkeypatch):
+    """The two-chunk schedule (first 32 iterations, then the rest, skipped by crops whose adaptive
+    bound already stopped them: OpenCV's early termination) gives the one-pass scan's result bit for
+    bit -- on realistic scenes (early stop) and random correspondences (no stop)."""
+    from zebrapose_amd.pnp import PnP
+    rng = np.random.default_rng(11)
+    scenes = [_scene(rng, n, f) for n, f in [(3000, 0.3), (7000, 0.3), (800, 0.5), (40, 0.1), (6, 0.0), (0, 0.0)]]
+    pw = rng.uniform(-60, 60, (2000, 3)).astype(np.float32)
+    scenes.append((pw, rng.integers(0, 480, (2000, 2)).astype(np.int32), None, None))  # random: no stop
+    counts, xy, xyz = _batch(scenes, 7000)
+    res = {}
+    for first in ("0", "32", "7"):
+        monkeypatch.setenv("ZP_PNP_FIRST", first)
+        res[first] = [v.cpu() for v in PnP()(counts, xy, xyz, K)]
+    for first in ("32", "7"):
+        for a, b in zip(res["0"], res[first]):
+            assert torch.equal(a, b), first

@@ -19,6 +19,7 @@
 //   k_pnp_select   thread per crop: the sequential RANSAC scan (adaptive iteration count)
 //   k_pnp_refine   block per crop: EPnP over the best model's inliers (block reductions)
 #include <math.h>
+#include <stdlib.h>
 #include "zp_common.h"
 
 // the linear algebra and EPnP pieces are host + device code (tools/pnp_host_check.hip runs them
@@ -417,6 +418,9 @@ struct PnpArgs {
   int* mvalid;         // [B][iters]
   int* good;           // [B][iters]
   int* best;           // [B] best iteration (-1 none)
+  int* maxgood;        // [B] the running RANSAC scan: inliers of the best model so far
+  int* niters;         // [B] its current iteration bound (RANSACUpdateNumIters)
+  int it0, it1;        // the chunk of iterations a hyp / score / select launch covers
   double* R;           // [B][9]
   double* T;           // [B][3]
   int* success;        // [B]
@@ -591,7 +595,10 @@ __device__ void null4(const double* A, const double* V, double* v4) {
 // per sweep) with the matrix in LDS, lane 0 finishes EPnP from the 4-vector null space.  (A
 // thread-per-hypothesis version spent ~8 ms of serial scratch traffic in the 12x12 Jacobi.)
 __global__ void __launch_bounds__(64) k_pnp_hyp(const PnpArgs a) {
-  const int b = blockIdx.y, it = blockIdx.x, lane = threadIdx.x;
+  const int b = blockIdx.y, it = a.it0 + blockIdx.x, lane = threadIdx.x;
+  // early termination: the scan of the chunks before this one already bounds the crop's RANSAC
+  // loop below this iteration (the bound only shrinks), so it is never evaluated
+  if (it >= a.niters[b]) return;
   __shared__ double A[144], V[144], cs[6][2];
   __shared__ double pw[5][3], uu[5], vv[5], cws[12], al[5][4], Aw[12], sa[4], mean[3];
   __shared__ int skip, rotated;
@@ -668,7 +675,8 @@ __global__ void __launch_bounds__(64) k_pnp_hyp(const PnpArgs a) {
 }
 
 __global__ void __launch_bounds__(256) k_pnp_score(const PnpArgs a) {
-  const int b = blockIdx.y, it = blockIdx.x;
+  const int b = blockIdx.y, it = a.it0 + blockIdx.x;
+  if (it >= a.niters[b]) return;
   __shared__ int red[256];
   const size_t mi = (size_t)b * a.iters + it;
   const int n = a.counts[b];
@@ -708,14 +716,17 @@ __device__ int update_num_iters(double p, double ep, int model_points, int max_i
   return (denom >= 0 || -num >= max_iters * (-denom)) ? max_iters : (int)rint(num / denom);
 }
 
+// the sequential RANSAC scan (ptsetreg.cpp RANSACPointSetRegistrator::run), continued over
+// iterations [it0, it1) from the state the previous chunks left (it0 == 0: fresh state)
 __global__ void k_pnp_select(const PnpArgs a) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= a.B) return;
   const int n = a.counts[b];
-  int best = -1;
+  int best = a.it0 == 0 ? -1 : a.best[b];
+  int niters = a.it0 == 0 ? a.iters : a.niters[b];
+  int maxgood = a.it0 == 0 ? 0 : a.maxgood[b];
   if (a.nsub[b] != 0) {
-    int niters = a.iters, maxgood = 0;
-    for (int it = 0; it < niters && it < a.iters; ++it) {
+    for (int it = a.it0; it < niters && it < a.it1; ++it) {
       const size_t mi = (size_t)b * a.iters + it;
       if (!a.mvalid[mi]) continue;
       const int g = a.good[mi];
@@ -725,8 +736,18 @@ __global__ void k_pnp_select(const PnpArgs a) {
         niters = update_num_iters(a.confidence, (double)(n - g) / n, a.model_points, niters);
       }
     }
+  } else {
+    niters = 0;
   }
   a.best[b] = best;
+  a.maxgood[b] = maxgood;
+  a.niters[b] = niters;
+}
+
+__global__ void k_pnp_scan_init(const PnpArgs a) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= a.B) return;
+  a.niters[b] = a.nsub[b] != 0 ? a.iters : 0;
 }
 
 // final EPnP over the best model's inliers; block per crop (4 waves), f64 block reductions:
@@ -869,7 +890,7 @@ using namespace zp;
 extern "C" long long zp_pnp_ws_bytes(int B, int iters) {
   if (B <= 0 || iters <= 0) return -1;
   const long long bi = (long long)B * iters;
-  return bi * 5 * 4 + (long long)B * 4 + bi * 12 * 8 + bi * 4 + bi * 4 + (long long)B * 4 + 256;
+  return bi * 5 * 4 + (long long)B * 4 + bi * 12 * 8 + bi * 4 + bi * 4 + (long long)B * 4 * 3 + 256;
 }
 
 extern "C" int zp_pnp_ransac(int B, int HW, const int* counts, const int* xy, const float* xyz, const double* K,
@@ -897,7 +918,9 @@ extern "C" int zp_pnp_ransac(int B, int HW, const int* counts, const int* xy, co
   a.mvalid = (int*)p;        p += bi * 4;
   a.good = (int*)p;          p += bi * 4;
   a.nsub = (int*)p;          p += (size_t)B * 4;
-  a.best = (int*)p;
+  a.best = (int*)p;          p += (size_t)B * 4;
+  a.maxgood = (int*)p;       p += (size_t)B * 4;
+  a.niters = (int*)p;
   a.R = R;
   a.T = T;
   a.success = success;
@@ -905,12 +928,26 @@ extern "C" int zp_pnp_ransac(int B, int HW, const int* counts, const int* xy, co
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(k_pnp_subsets, dim3((B + 63) / 64), dim3(64), 0, st, a);
   ZP_LAUNCH_CHECK("zp_pnp_ransac subsets");
-  hipLaunchKernelGGL(k_pnp_hyp, dim3(iters, B), dim3(64), 0, st, a);
-  ZP_LAUNCH_CHECK("zp_pnp_ransac hypotheses");
-  hipLaunchKernelGGL(k_pnp_score, dim3(iters, B), dim3(256), 0, st, a);
-  ZP_LAUNCH_CHECK("zp_pnp_ransac score");
-  hipLaunchKernelGGL(k_pnp_select, dim3((B + 63) / 64), dim3(64), 0, st, a);
-  ZP_LAUNCH_CHECK("zp_pnp_ransac select");
+  hipLaunchKernelGGL(k_pnp_scan_init, dim3((B + 63) / 64), dim3(64), 0, st, a);
+  // hypotheses in two chunks, each followed by the scan over it: the first FIRST iterations, then
+  // the rest.  A crop whose adaptive bound (RANSACUpdateNumIters) fell to <= FIRST skips the second
+  // chunk (its workgroups return at once), so the device work follows OpenCV's early termination
+  // (a 70%-inlier scene stops after ~25 iterations); the result is the one-pass scan's, bit for bit.
+  // Worst case (random correspondences, no termination): one extra round of launches.
+  // ZP_PNP_FIRST overrides FIRST (0: one chunk).
+  const char* ev = getenv("ZP_PNP_FIRST");
+  const int first = ev ? atoi(ev) : 32;
+  for (int c0 = 0; c0 < iters;) {
+    a.it0 = c0;
+    a.it1 = (c0 == 0 && first > 0) ? min(iters, first) : iters;
+    c0 = a.it1;
+    hipLaunchKernelGGL(k_pnp_hyp, dim3(a.it1 - a.it0, B), dim3(64), 0, st, a);
+    ZP_LAUNCH_CHECK("zp_pnp_ransac hypotheses");
+    hipLaunchKernelGGL(k_pnp_score, dim3(a.it1 - a.it0, B), dim3(256), 0, st, a);
+    ZP_LAUNCH_CHECK("zp_pnp_ransac score");
+    hipLaunchKernelGGL(k_pnp_select, dim3((B + 63) / 64), dim3(64), 0, st, a);
+    ZP_LAUNCH_CHECK("zp_pnp_ransac select");
+  }
   hipLaunchKernelGGL(k_pnp_refine, dim3(B), dim3(256), 0, st, a);
   ZP_LAUNCH_CHECK("zp_pnp_ransac refine");
   return ZP_OK;
