@@ -231,6 +231,13 @@ int zp_bn_bwd_apply(const void* dy, int lddy, int cdy0, const void* y, int ldy, 
 /* x f32 NCHW [B][C][H][W] -> y NHWC [B][H][W][cpad] (dtype), channels C..cpad-1 zero */
 int zp_nchw_to_nhwc(const float* x, int B, int C, int H, int W, int cpad, int dtype, void* y,
                     void* stream);
+/* Split-fp32 stem input (ZP_F32X3 / ZP_F32H2): the im2col of an f32 NHWC image x [B][H][W][ldx]
+ * (C real channels) for a k x k / stride s / padding p conv -- y [NPL][B][OH][OW][kpad] with
+ * element kk = (ky * k + kx) * C + c (kk >= k*k*C and out-of-image taps zero), stored split.  The
+ * stem conv (torchvision ResNet conv1 7x7/s2/p3, reference model/resnet.py:195) then runs as a 1x1
+ * split-fp32 conv over kpad channels, weights packed with zp_pack_weight(..., cstride = C, ...). */
+int zp_im2col_split(const float* x, int B, int H, int W, int ldx, int C, int k, int s, int p, int OH, int OW,
+                    int kpad, int dtype, void* y, void* stream);
 /* 3x3 / stride 2 / pad 1 max pool, NHWC slices; C multiple of 8 */
 int zp_maxpool3s2(const void* x, int B, int IH, int IW, int ldx, int cx0, int C, int dtype,
                   void* y, int OH, int OW, int ldy, int cy0, void* stream);

@@ -82,6 +82,7 @@ _SIGS = {
                               vp]),
     "zp_nchw_to_nhwc": (i32, [vp, i32, i32, i32, i32, i32, i32, vp, vp]),
     "zp_maxpool3s2": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, vp, i32, i32, i32, i32, vp]),
+    "zp_im2col_split": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp]),
     "zp_maxpool3s2_bwd": (i32, [vp, i32, i32, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, i32, i32, i32,
                                 vp]),
     "zp_global_avgpool": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, vp, vp]),

@@ -742,6 +742,46 @@ __global__ void k_maxpool(const T* __restrict__ x, int B, int IH, int IW, int ld
   }
 }
 
+// Split-fp32 stem im2col (zp_im2col_split): thread per (output pixel, 8-element chunk of the
+// kpad-long patch row); taps gathered from the f32 NHWC image (L2-resident: each input pixel is
+// read by <= 16 overlapping 7x7 / s2 windows), each element split into the NPL planes
+template <int NPL>
+__global__ void k_im2col_split(const float* __restrict__ x, int B, int H, int W, int ldx, int C, int k, int s, int p,
+                               int OH, int OW, int kpad, unsigned short* __restrict__ y) {
+  const int KC = kpad / 8, KK = k * k * C;
+  const long total = (long)B * OH * OW * KC;
+  const long plane = (long)B * OH * OW * kpad;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const long pix = e / KC;
+    const int kc = (int)(e - pix * KC);
+    const int ox = (int)(pix % OW);
+    const long t = pix / OW;
+    const int oy = (int)(t % OH), b = (int)(t / OH);
+    uint32_t w[NPL][4];
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) {
+      unsigned short q[2][NPL];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int kk = kc * 8 + i + h;
+        float v = 0.f;
+        if (kk < KK) {
+          const int tap = kk / C, c = kk - tap * C;
+          const int ky = tap / k, kx = tap - ky * k;
+          const int iy = oy * s - p + ky, ix = ox * s - p + kx;
+          if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) v = x[(((long)b * H + iy) * W + ix) * ldx + c];
+        }
+        SplitF32<NPL>::split(v, q[h]);
+      }
+#pragma unroll
+      for (int pl = 0; pl < NPL; ++pl) w[pl][i >> 1] = (uint32_t)q[0][pl] | ((uint32_t)q[1][pl] << 16);
+    }
+    unsigned short* yo = y + pix * kpad + kc * 8;
+#pragma unroll
+    for (int pl = 0; pl < NPL; ++pl) *(uint4*)(yo + pl * plane) = make_uint4(w[pl][0], w[pl][1], w[pl][2], w[pl][3]);
+  }
+}
+
 // Split-fp32 max pool (NPL planes, SplitF32<NPL>): the 3x3 window max of the joined f32 values
 // (PyTorch CPU rule), stored split again (joining is exact, so the winner's value is reproduced
 // exactly).  Planes: x + p * psx, y + p * psy.
@@ -1383,6 +1423,23 @@ extern "C" int zp_bn_bwd_apply(const void* dy, int lddy, int cdy0, const void* y
       hipLaunchKernelGGL(KERNEL<T>, grid, dim3(256), 0, st, __VA_ARGS__);                   \
     }                                                                                       \
   } while (0)
+
+extern "C" int zp_im2col_split(const float* x, int B, int H, int W, int ldx, int C, int k, int s, int p, int OH,
+                               int OW, int kpad, int dtype, void* y, void* stream) {
+  ZP_CHECK_ARG(dtype == ZP_F32X3 || dtype == ZP_F32H2, "zp_im2col_split: dtype %d is not a split-fp32 form", dtype);
+  ZP_CHECK_ARG(x && y && B > 0 && H > 0 && W > 0 && C > 0 && ldx >= C && k > 0 && s > 0 && p >= 0 && OH > 0 &&
+                   OW > 0 && kpad % 8 == 0 && kpad >= k * k * C,
+               "zp_im2col_split: bad args");
+  const long total = (long)B * OH * OW * (kpad / 8);
+  if (dtype == ZP_F32X3)
+    hipLaunchKernelGGL(k_im2col_split<3>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, x, B, H, W, ldx,
+                       C, k, s, p, OH, OW, kpad, (unsigned short*)y);
+  else
+    hipLaunchKernelGGL(k_im2col_split<2>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, x, B, H, W, ldx,
+                       C, k, s, p, OH, OW, kpad, (unsigned short*)y);
+  ZP_LAUNCH_CHECK("zp_im2col_split");
+  return ZP_OK;
+}
 
 extern "C" int zp_nchw_to_nhwc(const float* x, int B, int C, int H, int W, int cpad, int dtype, void* y, void* stream) {
   ZP_DTYPE_CHECK("zp_nchw_to_nhwc", dtype);

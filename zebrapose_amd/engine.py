@@ -128,6 +128,9 @@ class Engine:
         self.x3 = split is not None  # any split-fp32 form
         self.dt = {"x3": L.ZP_F32X3, "h2": L.ZP_F32H2}[split] if split else L.dtype_code(dtype)
         self.npl, self.dtype, self.split_out = SPLIT[self.dt] if split else (1, dtype, None)
+        # split forms: the stem as im2col + split GEMM (ZP_SPLIT_STEM=0: the exact-f32 small-Cin
+        # kernel writing split output)
+        self.split_stem = os.environ.get("ZP_SPLIT_STEM", "1") != "0"
         self._packed = {}
         self._jobs = []  # (cache key, weight, PackJob) of every cached packing, for _prepack
         self._job_table = None
@@ -364,6 +367,26 @@ class Engine:
         OH, OW = unit.out_hw(x.H, x.W)
         assert (out.H, out.W, out.C) == (OH, OW, unit.cout), ((out.H, out.W, out.C), (OH, OW, unit.cout))
         train = tape is not None
+        if self.x3 and unit.cin < _KE[self.dt] and unit.s == 2 and unit.d == 1 and self.split_stem:
+            # the split-mode stem as a GEMM: the f32 image's 7x7 / s2 patches (k*k*3 = 147 -> 160
+            # channels, zp_im2col_split) in split form, then a 1x1 split-fp32 conv over them with the
+            # 7x7 weights packed tap-major (k = tap * 3 + c, the im2col order)
+            assert not train, "the split engine runs eval forwards only"
+            cr = unit.conv.weight.shape[1]
+            kp = G.ceil_to(unit.k * unit.k * cr, 32)
+            col = Act(self._empty((x.B, OH, OW, kp), x.buf.device))
+            L.call("zp_im2col_split", x.ptr, x.B, x.H, x.W, x.ld, cr, unit.k, unit.s, unit.p, OH, OW, kp, self.dt,
+                   col.ptr, L.stream_ptr())
+            taps = [(ky, kx) for ky in range(unit.k) for kx in range(unit.k)]
+            rows = G.ceil_to(unit.cout, 128)
+            w = self._pack(unit, G.Sub(taps, [(0, 0)] * len(taps)), 0, cr, kp, rows, "stem_im2col")
+            scale, shift = self._fold(unit)
+            plan = G.conv_fwd(OH, OW, 1, 1, 0)
+            outs = [(out.ptr, out.ld, out.c0, OH, OW, scale, shift, None)]
+            self._conv(col, plan, unit.cout, [w], kp, rows, outs, res, unit.relu, label=label)
+            if self.trace is not None:
+                self.trace.append(("conv", unit, x, out, res))
+            return
         if self.x3 and unit.cin < _KE[self.dt]:
             # the split-mode stem: its 3 (-> 8) input channels are below k_conv3's 32-channel K step;
             # it runs the exact-f32 small-Cin kernel on the f32 NHWC input and writes split output
