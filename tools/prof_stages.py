@@ -9,7 +9,7 @@ sequence is identical from step 2 on.  The last step is the window from its k_nc
 input conversion, first kernel of a step) to the end of the run (the decode kernels end it).  Its
 conv dispatches are matched one by one, in order, to the driver's stage log (engine.stage_log:
 stage, kernel label, FLOPs); the label of every pair is checked.  Non-conv kernels are attributed
-by name (nchw_to_nhwc -> stem, maxpool -> layer1, global avgpool / broadcast -> aspp, decode).
+by name (nchw_to_nhwc, im2col -> stem, maxpool -> layer1, global avgpool / broadcast -> aspp, decode).
 
 Per stage:
   time      sum of the dispatch durations (kernel-trace pass, End - Start timestamps)
@@ -48,7 +48,7 @@ def one(pattern):
 
 
 def nonconv_stage(name):
-    if "nchw_to_nhwc" in name:
+    if "nchw_to_nhwc" in name or "im2col" in name:
         return "stem"
     if "maxpool" in name:
         return "layer1"
