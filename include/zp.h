@@ -132,6 +132,12 @@ int zp_conv2d_stat_parts(const zp_conv_args* a);
  * structure in one tile, 4 = k_conv3: the split-fp32 (ZP_F32X3) kernel, 5 = k_conv3s: its 3x3
  * stride-1 form with activation-strip reuse) */
 int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* stages, int* variant);
+/* Split-fp32 forms (ZP_F32X3 / ZP_F32H2) only: a launch whose grid would leave most CUs idle (a
+ * one-sub NHWC conv with under 256 workgroups, e.g. bs = 1) is cut along K into slices whose f32
+ * sums are finished (summed in slice order, then BN / residual / ReLU / split store) by a second
+ * kernel, when zp_conv_args.stats points to an f32 workspace of this many bytes (0: not split;
+ * stats NULL: not split).  Deterministic. */
+long long zp_conv2d_split_ws(const zp_conv_args* a);
 /* runtime tuning knobs (tests / sweeps): key 0 = minimum workgroup count for the 256-channel
  * tile (default 1024); key 1 = conv schedule flags (-1 = ZP_CONV_FLAGS or the default); key 2 =
  * 64-channel layers on the strip kernel (default 1); key 3 = the lean weight-gradient kernel
@@ -140,8 +146,8 @@ int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* stages, int* 
  * fewest workgroups the four-phase kernel (k_conv_quad) runs with (default 256); key 7 = the
  * split-fp32 strip kernel k_conv3s (0 off, 1 64-channel tiles, 2 also 128-channel tiles; -1 =
  * ZP_CONV3_STRIP or the default 1); key 8 = the fewest workgroups a split-fp32 launch runs
- * 128-channel tiles with (fewer: 64-channel tiles).  Returns the previous value, -1 for an
- * unknown key. */
+ * 128-channel tiles with (fewer: 64-channel tiles); key 9 = split-K of small split-fp32 launches
+ * (default 1, 0 off).  Returns the previous value, -1 for an unknown key. */
 int zp_conv_tuning(int key, int value);
 
 /* Pack an f32 weight tensor src[d0][d1][kh][kw] into dst[rows_pad][k_pad] (dtype), taps

@@ -135,18 +135,22 @@ def test_h2_weight_pack(gpu):
     assert ((joined - ref).abs() <= 2.0 ** -22 * ref.abs() + 2.0 ** -36).all()
 
 
+@pytest.mark.parametrize("splitk", [1, 0], ids=["splitk", "no_splitk"])
 @pytest.mark.parametrize("form", FORMS)
 @pytest.mark.parametrize("min_blocks", [0, 256], ids=["tile_by_cout", "small_grid_64"])
 @pytest.mark.parametrize("geom", GEOMS, ids=[_gid(g) for g in GEOMS])
-def test_split_conv_is_f32_accurate(gpu, geom, min_blocks, form):
+def test_split_conv_is_f32_accurate(gpu, geom, min_blocks, form, splitk):
     """min_blocks = zp_conv_tuning key 8: 0 keeps the 128-channel tiles at these small batches,
-    256 (the default) moves launches of < 256 workgroups to 64-channel tiles."""
+    256 (the default) moves launches of < 256 workgroups to 64-channel tiles; splitk = key 9 (these
+    B = 2 grids are small: with it on, the one-sub launches run split along K)."""
     from zebrapose_amd import _lib as L
     old = L.lib.zp_conv_tuning(8, min_blocks)
+    old_sk = L.lib.zp_conv_tuning(9, splitk)
     try:
         _check_geom(gpu, geom, form)
     finally:
         L.lib.zp_conv_tuning(8, old)
+        L.lib.zp_conv_tuning(9, old_sk)
 
 
 @pytest.mark.parametrize("form", FORMS)
@@ -156,11 +160,13 @@ def test_split_strip_kernel(gpu, geom, mode, form):
     from zebrapose_amd import _lib as L
     old = L.lib.zp_conv_tuning(7, mode)
     old_mb = L.lib.zp_conv_tuning(8, 0)  # the cout tile by Cout alone
+    old_sk = L.lib.zp_conv_tuning(9, 0)  # no split-K (it takes these small grids before the strip kernel)
     try:
         variant = _check_geom(gpu, geom, form)
     finally:
         L.lib.zp_conv_tuning(7, old)
         L.lib.zp_conv_tuning(8, old_mb)
+        L.lib.zp_conv_tuning(9, old_sk)
     cout, H = geom[2], geom[8]
     tc = 128 if cout > 64 else 64
     strip = (mode == 2 or (mode == 1 and tc == 64)) and H * H >= 256
@@ -315,3 +321,47 @@ def test_split_accumulation_numerics(gpu, cin):
         res[mode] = (d.abs().max().item(), d.pow(2).mean().sqrt().item(), d.mean().item())
     print(f"K={cin}: bf16-MFMA acc max/rms/mean {res['x3']}, f32-MFMA {res['f32']} (scale {ref.abs().max().item():.3g})")
     assert res["x3"][0] <= 2.0 * res["f32"][0] + 1e-30
+
+
+@pytest.mark.parametrize("form", FORMS)
+@pytest.mark.parametrize("geom", [("conv", 512, 512, 3, 1, 4, 4, False, 32), ("conv", 256, 256, 3, 1, 2, 2, False, 32),
+                                  ("conv", 1280, 256, 1, 1, 0, 1, True, 8)],
+                         ids=["l5_d4", "l4_d2", "aspp_proj"])
+def test_split_k_small_batch(gpu, geom, form):
+    """bs = 1: the small-grid launches are cut along K (zp_conv2d_split_ws > 0, zp_conv_tuning key 9)
+    and finished by k_splitk_epi; the result is as accurate as the unsplit kernel's (both against
+    float64) and differs from it (the split path ran)."""
+    from zebrapose_amd import _lib as L
+    from zebrapose_amd.engine import Engine, Unit, Act, joined
+    from zebrapose_amd.model import layers as LY
+    kind, cin, cout, k, s, p, d, bias, H = geom
+    torch.manual_seed(6)
+    conv = LY.Conv2d(cin, cout, k, s, p, d, bias=bias)
+    bn = LY.BatchNorm2d(cout)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.normal_(0, 0.1)
+        bn.running_mean.normal_(0, 0.1)
+        bn.running_var.uniform_(0.5, 1.5)
+    conv, bn = conv.to(gpu).eval(), bn.to(gpu).eval()
+    unit = Unit(conv, bn, relu=True)
+    x = torch.randn(1, cin, H, H)
+    res = torch.randn(1, cout, H, H)
+    ref = _ref64(kind, conv, bn, x, res, True, s, p, d)
+    xh, rh = x.permute(0, 2, 3, 1).contiguous(), res.permute(0, 2, 3, 1).contiguous()
+    eng = Engine(torch.nn.Module(), torch.float32, split=form)
+    xa, ra = Act(_split_act(xh, gpu, form)), Act(_split_act(rh, gpu, form))
+    out = {}
+    for mode in (1, 0):
+        old = L.lib.zp_conv_tuning(9, mode)
+        try:
+            oa = Act(eng._empty((1, H, H, cout), gpu))
+            eng.unit_fwd(unit, xa, oa, None, res=ra)
+            torch.cuda.synchronize()
+        finally:
+            L.lib.zp_conv_tuning(9, old)
+        out[mode] = joined(oa.buf).permute(0, 3, 1, 2).double().cpu()
+    e1, e0 = (out[1] - ref).abs().max().item(), (out[0] - ref).abs().max().item()
+    print(f"{geom} {form} bs=1: split-K max|d| {e1:.3g}, unsplit {e0:.3g}")
+    assert not torch.equal(out[1], out[0])
+    assert e1 <= 2.0 * e0 + 2.0 ** -22 * ref.abs().max().item(), (e1, e0)

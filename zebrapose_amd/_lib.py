@@ -69,6 +69,7 @@ _SIGS = {
     "zp_conv_rows_pad": (i32, [i32]),
     "zp_conv2d_grid": (i32, [C.POINTER(ConvArgs)]),
     "zp_conv2d_stat_parts": (i32, [C.POINTER(ConvArgs)]),
+    "zp_conv2d_split_ws": (C.c_longlong, [C.POINTER(ConvArgs)]),
     "zp_pack_weight": (i32, [vp, i32, i32, i32, i32, i32, i32, C.POINTER(i32), C.POINTER(i32), i32, i32, vp, i32,
                              i32, vp]),
     "zp_conv2d_wgrad_ws_bytes": (i64, [C.POINTER(WgradArgs)]),

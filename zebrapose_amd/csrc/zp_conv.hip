@@ -2769,7 +2769,7 @@ extern "C" int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* st
   *tc = conv_tc(*a);
   *tp = conv_tp(*a);
   *stages = *tc == 256 ? 2 : conv_stages(*a, *tc);
-  *variant = (a->dtype == ZP_F32X3 || a->dtype == ZP_F32H2) ? (conv3_strip_ok(*a, *tc) ? 5 : 4) : quad_plan(*a, nullptr) ? 3 : *tc <= 128 && strip_eligible(*a, nullptr) ? ((conv_flags() & 64) ? 2 : 1) : 0;
+  *variant = (a->dtype == ZP_F32X3 || a->dtype == ZP_F32H2) ? (conv3_nsplit(*a) == 1 && conv3_strip_ok(*a, *tc) ? 5 : 4) : quad_plan(*a, nullptr) ? 3 : *tc <= 128 && strip_eligible(*a, nullptr) ? ((conv_flags() & 64) ? 2 : 1) : 0;
   return ZP_OK;
 }
 
@@ -2782,6 +2782,14 @@ extern "C" int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* st
  * 64-channel tiles, 2 also the 128-channel tiles; -1 = ZP_CONV3_STRIP / default 1); key 8: the
  * fewest workgroups a split-fp32 launch runs 128-channel tiles with (fewer: 64-channel tiles).
  * Returns the previous value. */
+/* split-fp32 split-K workspace: bytes of f32 slices zp_conv2d uses for these args when a.stats
+ * points to that many (0: the launch is not split) */
+extern "C" long long zp_conv2d_split_ws(const zp_conv_args* a) {
+  if (!a || (a->dtype != ZP_F32X3 && a->dtype != ZP_F32H2)) return 0;
+  const int ns = conv3_nsplit(*a);
+  return ns > 1 ? (long long)ns * a->N * a->GH * a->GW * a->Cout * 4 : 0;
+}
+
 extern "C" int zp_conv_tuning(int key, int value) {
   if (key == 0) {
     const int old = g_tc256_min_blocks;
@@ -2815,6 +2823,7 @@ extern "C" int zp_conv_tuning(int key, int value) {
   }
   if (key == 7) return conv3_strip_mode(value);
   if (key == 8) return conv3_min_blocks(value);
+  if (key == 9) return conv3_splitk_mode(value);
   if (key == 4) {
     const int old = g_wgrad2_rounds;
     g_wgrad2_rounds = value > 0 ? value : 1;

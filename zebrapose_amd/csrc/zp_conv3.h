@@ -8,5 +8,7 @@ int conv3_tp(const zp_conv_args& a, int tc);     // pixel tile of the generic ke
 bool conv3_strip_ok(const zp_conv_args& a, int tc);  // k_conv3s eligible
 int conv3_strip_mode(int v);
 int conv3_min_blocks(int v);                      // zp_conv_tuning key 8; returns the previous value                      // zp_conv_tuning key 7; returns the previous value
+int conv3_splitk_mode(int v);                     // zp_conv_tuning key 9; returns the previous value
+int conv3_nsplit(const zp_conv_args& a);          // split-K slices (1: none)
 int conv3_launch(const zp_conv_args& a, hipStream_t st, int flags);
 }  // namespace zp

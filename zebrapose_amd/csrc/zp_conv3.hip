@@ -126,6 +126,75 @@ __device__ __forceinline__ void conv3_epilogue(const zp_conv_args& A, const zp_c
   }
 }
 
+// split-K slice: the raw f32 sums of this tile into ws [M][Cout] (acc[i][j] = 4 consecutive output
+// channels x one grid point)
+template <int WC, int WP>
+__device__ __forceinline__ void splitk_store(float* __restrict__ ws, const int Cout, const f32x4 (&acc)[WC][WP],
+                                             const int p0, const int c0, const int wc, const int wp, const int lane,
+                                             const int M) {
+  const int lr = lane & 15;
+  const int cbase = c0 + wc * 16 * WC + (lane >> 4) * 4;
+#pragma unroll
+  for (int j = 0; j < WP; ++j) {
+    const int p = p0 + wp * 16 * WP + j * 16 + lr;
+    if (p >= M) continue;
+#pragma unroll
+    for (int i = 0; i < WC; ++i) {
+      const int cf = cbase + i * 16;
+      if (cf + 3 < Cout) {
+        *(float4*)(ws + (size_t)p * Cout + cf) = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (cf + r < Cout) ws[(size_t)p * Cout + cf + r] = acc[i][j][r];
+      }
+    }
+  }
+}
+
+// split-K epilogue: thread per (grid point, 4 output channels); the slices summed in slice order
+// (deterministic), then conv3_epilogue's BN / bias, split residual, ReLU and split store (one
+// sub-problem, NHWC output)
+template <int NPL>
+__global__ void k_splitk_epi(const zp_conv_args A, const float* __restrict__ ws, const int nsplit) {
+  using SP = SplitF32<NPL>;
+  const zp_conv_sub& S = A.sub[0];
+  const int GHW = A.GH * A.GW, M = A.N * GHW, C4 = (A.Cout + 3) / 4;
+  const long psy = (long)A.N * S.OH * S.OW * S.ldy;
+  const long psr = (long)A.N * S.OH * S.OW * A.ldr;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < (long)M * C4; e += (long)gridDim.x * blockDim.x) {
+    const int p = (int)(e / C4), cf = (int)(e - (long)p * C4) * 4;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int z = 0; z < nsplit; ++z) {
+      const float* w = ws + ((size_t)z * M + p) * A.Cout + cf;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (cf + r < A.Cout) v[r] += w[r];
+    }
+    const int n = p / GHW, rr = p - n * GHW;
+    const int gy = rr / A.GW, gx = rr - gy * A.GW;
+    const size_t pix = ((size_t)n * S.OH + gy * S.oys + S.oyo) * S.OW + gx * S.oxs + S.oxo;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (cf + r >= A.Cout) continue;
+      float o = v[r] * (S.scale ? S.scale[cf + r] : 1.f) + (S.shift ? S.shift[cf + r] : 0.f);
+      if (A.res) {
+        const unsigned short* R = (const unsigned short*)A.res + pix * A.ldr + A.cr0 + cf + r;
+        unsigned short q[NPL];
+#pragma unroll
+        for (int pl = 0; pl < NPL; ++pl) q[pl] = R[pl * psr];
+        o += SP::join(q);
+      }
+      if (A.relu) o = fmaxf(o, 0.f);
+      unsigned short q[NPL];
+      SP::split(o, q);
+      unsigned short* Y = (unsigned short*)S.y + pix * S.ldy + S.cy0 + cf + r;
+#pragma unroll
+      for (int pl = 0; pl < NPL; ++pl) Y[pl * psy] = q[pl];
+    }
+  }
+}
+
 // The correction terms of a split product (besides hi*hi, plane 0 x plane 0, into the main
 // accumulator): plane pairs (A[t], B[t]) of (weight, activation)
 template <int NPL> struct Terms;
@@ -181,7 +250,8 @@ __device__ __forceinline__ void flush_corr(f32x4& acc, const f32x4& c2) {
 //     ahead; per step one counted vmcnt wait + one barrier, no LDS read on the MFMA critical path.
 // ------------------------------------------------------------------------------------
 template <int NPL, int WC, int WP, int NWP, int ST, bool PIPE>
-__global__ void __launch_bounds__(128 * NWP) k_conv3(const zp_conv_args A, const conv_taps TG, const int flags) {
+__global__ void __launch_bounds__(128 * NWP) k_conv3(const zp_conv_args A, const conv_taps TG, const int flags,
+                                                     float* __restrict__ ws, const int nsplit) {
   constexpr int TC = 32 * WC, TP = 16 * WP * NWP, NW = 2 * NWP;
   constexpr int NTW = TC / 16, NT = (TC + TP) / 16;  // weight tiles / all tiles (16 rows) per plane
   constexpr int UNITS = NPL * NT;                    // (plane, tile) DMA units per stage
@@ -196,7 +266,10 @@ __global__ void __launch_bounds__(128 * NWP) k_conv3(const zp_conv_args A, const
   __shared__ uint4 lds[ST * UNITS * 64];
   static_assert(ST * UNITS * 1024 <= 160 * 1024, "LDS");
   static_assert(((NPL - 1) * NT + WC + 3) * 1024 < 65536, "ds_read immediate range");
-  const zp_conv_sub& S = A.sub[blockIdx.z];
+  // split-K (nsplit > 1, one sub-problem): blockIdx.z is the K slice; its raw f32 sums go to ws
+  // [nsplit][M][Cout] and k_splitk_epi finishes them
+  const int tb = nsplit > 1 ? 0 : blockIdx.z, kz = nsplit > 1 ? blockIdx.z : 0;
+  const zp_conv_sub& S = A.sub[tb];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wc = wid / NWP, wp = wid % NWP;
@@ -211,10 +284,11 @@ __global__ void __launch_bounds__(128 * NWP) k_conv3(const zp_conv_args A, const
     by = lin - bx * gridDim.y;
   }
   const int p0 = bx * TP, c0 = by * TC;
-  const int tb = blockIdx.z;
   const int CB = A.Cin / 32;
   const int ny = TG.ny[tb], nx = TG.nx[tb], dty = TG.dty[tb], dtx = TG.dtx[tb];
-  const int nK = S.ntaps * CB;
+  const int nK_all = S.ntaps * CB;
+  const int ks0 = (int)((long)kz * nK_all / nsplit);
+  const int nK = (int)((long)(kz + 1) * nK_all / nsplit) - ks0;  // this slice's K steps
   const int lr = lane & 15, lk = (lane >> 4) * 8;
   // plane strides in bytes (scalar offsets of the DMA: the three planes of a tile share the lane's
   // offset register)
@@ -257,10 +331,12 @@ __global__ void __launch_bounds__(128 * NWP) k_conv3(const zp_conv_args A, const
   // a tile evicted the rows before the next tap came back to them, and the staging ran at the
   // Infinity-Cache / HBM rate.  act_off = ((ty * IW + tx) * ldx + cb * 32) * 2; the weight offset
   // of (tap t, chunk cb) in the packed row (k = t * Cin + c) is w_koff = (t * Cin + cb * 32) * 2.
-  int w_tyi = 0, w_txi = 0, w_cb = 0, w_t = 0;
-  int act_off = ((TG.ty0[tb] * A.IW + TG.tx0[tb]) * A.ldx) * 2;
-  int w_koff = 0;
+  // the walk starts at step ks0 = (chunk cb, tap t = tyi * nx + txi)
+  int w_cb = ks0 / S.ntaps, w_t = ks0 - (ks0 / S.ntaps) * S.ntaps;
+  int w_tyi = w_t / nx, w_txi = w_t - (w_t / nx) * nx;
   const int step_x = dtx * A.ldx * 2, step_y = dty * A.IW * A.ldx * 2;
+  int act_off = ((TG.ty0[tb] * A.IW + TG.tx0[tb]) * A.ldx) * 2 + w_tyi * step_y + w_txi * step_x + w_cb * 64;
+  int w_koff = (w_t * A.Cin + w_cb * 32) * 2;
   const int cin2 = A.Cin * 2;
   // diagnostic ablation flags (timing only, wrong results): 4096 no DMA after the prologue, 8192 no
   // MFMA, 16384 no epilogue stores
@@ -553,7 +629,8 @@ __global__ void __launch_bounds__(128 * NWP) k_conv3(const zp_conv_args A, const
 #pragma unroll
       for (int j = 0; j < WP; ++j) flush_corr<NPL>(acc[i][j], acc2[PIPE ? i : 0][PIPE ? j : 0]);
   }
-  conv3_epilogue<NPL, WC, WP>(A, S, acc, p0, c0, wc, wp, lane, M, GHW, flags);
+  if (nsplit > 1) splitk_store<WC, WP>(ws + (size_t)kz * M * A.Cout, A.Cout, acc, p0, c0, wc, wp, lane, M);
+  else conv3_epilogue<NPL, WC, WP>(A, S, acc, p0, c0, wc, wp, lane, M, GHW, flags);
 }
 
 // ------------------------------------------------------------------------------------
@@ -898,11 +975,35 @@ static bool conv3_strip(const zp_conv_args& a, int tc, strip3_geo* sg) {
   return true;
 }
 
+static int g_splitk = 1;  // zp_conv_tuning key 9: split-K of small split-fp32 launches (0 off)
+
+int conv3_splitk_mode(int v) {
+  const int old = g_splitk;
+  g_splitk = v;
+  return old;
+}
+
+// split-K slices of a split-fp32 launch: a one-sub NHWC conv whose grid leaves most CUs idle (under
+// 256 workgroups -- bs = 1: layer5's 512 -> 512 runs as 64 workgroups over 144 K steps) is cut
+// along K into up to 16 slices of >= 8 steps, for about 512 workgroups
+int conv3_nsplit(const zp_conv_args& a) {
+  if (!g_splitk || a.nsub != 1 || a.out_mode != ZP_OUT_NHWC) return 1;
+  const int tc = conv3_tc(a);
+  const long blocks = (long)ceil_div((long)a.N * a.GH * a.GW, conv3_tp(a, tc)) * ceil_div(a.Cout, tc);
+  const int nK = a.sub[0].ntaps * (a.Cin / 32);
+  if (blocks >= 256) return 1;
+  int ns = 1;
+  while (ns < 16 && blocks * ns * 2 <= 512 && nK / (ns * 2) >= 8) ns *= 2;
+  return ns;
+}
+
 // kernel launches for one split form (NPL planes: 3 = ZP_F32X3, 2 = ZP_F32H2)
 template <int NPL>
 static void conv3_dispatch(const zp_conv_args& a, const conv_taps& tg, int tc, hipStream_t st, int fl) {
+  const int ns = a.stats ? conv3_nsplit(a) : 1;
+  float* ws = (float*)a.stats;
   strip3_geo s3{};
-  if (conv3_strip(a, tc, &s3)) {
+  if (ns == 1 && conv3_strip(a, tc, &s3)) {
     s3.x_bytes = tg.x_bytes;
     s3.w_bytes = tg.w_bytes[0];
     const dim3 sgrid((unsigned)(((long)a.N * a.GH * a.GW) / 256), (unsigned)(a.Cout / tc), 1);
@@ -912,18 +1013,24 @@ static void conv3_dispatch(const zp_conv_args& a, const conv_taps& tg, int tc, h
   }
   const int tp = conv3_tp(a, tc);
   const int gx = ceil_div((long)a.N * a.GH * a.GW, tp), gy = ceil_div(a.Cout, tc);
-  const dim3 grid(gx, gy, a.nsub);
+  const dim3 grid(gx, gy, ns > 1 ? ns : a.nsub);
   // 128-channel layers: 8 waves, 128 x 256, 2-deep ring (two planes: 3-deep, the same LDS);
   // smaller tiles: register-pipelined one wave per SIMD over 128 pixels (ZP_CONV3_SCHED=1: the
   // 128-channel tile that way too)
   // (flags & 32768: the two-plane tile with the 2-deep ring, A/B)
   constexpr int ST8 = NPL == 2 ? 3 : 2;
   if (tc == 128 && tp == 256 && NPL == 2 && (fl & 32768))
-    hipLaunchKernelGGL((k_conv3<NPL, 4, 4, 4, 2, false>), grid, dim3(512), 0, st, a, tg, fl);
-  else if (tc == 128 && tp == 256) hipLaunchKernelGGL((k_conv3<NPL, 4, 4, 4, ST8, false>), grid, dim3(512), 0, st, a, tg, fl);
-  else if (tc == 128) hipLaunchKernelGGL((k_conv3<NPL, 4, 4, 2, 2, true>), grid, dim3(256), 0, st, a, tg, fl);
-  else if (tc == 64) hipLaunchKernelGGL((k_conv3<NPL, 2, 4, 2, 2, true>), grid, dim3(256), 0, st, a, tg, fl);
-  else hipLaunchKernelGGL((k_conv3<NPL, 1, 4, 2, 2, true>), grid, dim3(256), 0, st, a, tg, fl);
+    hipLaunchKernelGGL((k_conv3<NPL, 4, 4, 4, 2, false>), grid, dim3(512), 0, st, a, tg, fl, ws, ns);
+  else if (tc == 128 && tp == 256)
+    hipLaunchKernelGGL((k_conv3<NPL, 4, 4, 4, ST8, false>), grid, dim3(512), 0, st, a, tg, fl, ws, ns);
+  else if (tc == 128) hipLaunchKernelGGL((k_conv3<NPL, 4, 4, 2, 2, true>), grid, dim3(256), 0, st, a, tg, fl, ws, ns);
+  else if (tc == 64) hipLaunchKernelGGL((k_conv3<NPL, 2, 4, 2, 2, true>), grid, dim3(256), 0, st, a, tg, fl, ws, ns);
+  else hipLaunchKernelGGL((k_conv3<NPL, 1, 4, 2, 2, true>), grid, dim3(256), 0, st, a, tg, fl, ws, ns);
+  if (ns > 1) {
+    const long total = (long)a.N * a.GH * a.GW * ((a.Cout + 3) / 4);
+    const int blocks = (int)(total + 255) / 256 < 8192 ? (int)((total + 255) / 256) : 8192;
+    hipLaunchKernelGGL((k_splitk_epi<NPL>), dim3(blocks), dim3(256), 0, st, a, ws, ns);
+  }
 }
 
 int conv3_launch(const zp_conv_args& a, hipStream_t st, int fl) {
@@ -932,7 +1039,7 @@ int conv3_launch(const zp_conv_args& a, hipStream_t st, int fl) {
                "with out_mode ZP_OUT_NHWC_X3 / _H2)", a.Cin);
   ZP_CHECK_ARG(a.ldx >= a.cx0 + a.Cin && a.cx0 % 8 == 0 && a.ldx % 8 == 0, "zp_conv2d: bad ldx/cx0");
   ZP_CHECK_ARG(a.k_pad % 32 == 0, "zp_conv2d: k_pad %d not a multiple of 32", a.k_pad);
-  ZP_CHECK_ARG(!a.stats, "zp_conv2d: split fp32 is forward (eval) only: no train-mode statistics");
+  // a.stats: for the split forms an optional f32 split-K workspace (zp_conv2d_split_ws bytes)
   ZP_CHECK_ARG(a.out_mode == ZP_OUT_NHWC || a.out_mode == ZP_OUT_HEAD_NCHW,
                "zp_conv2d: split fp32 writes split NHWC (ZP_OUT_NHWC) or the f32 head (ZP_OUT_HEAD_NCHW)");
   const int tc = conv3_tc(a);

@@ -296,6 +296,11 @@ class Engine:
             stats = torch.empty(3 * parts * cout, dtype=torch.float32, device=x.buf.device)
         if stats is not None:
             a.stats = stats.data_ptr()
+        elif dt in SPLIT:  # split-K workspace of a small split-fp32 launch (zp_conv2d_split_ws)
+            nb = L.lib.zp_conv2d_split_ws(C.byref(a))
+            if nb > 0:
+                stats = torch.empty(nb // 4, dtype=torch.float32, device=x.buf.device)
+                a.stats = stats.data_ptr()
         st = L.stream_ptr()
         if self.timing is not None or self.stage_log is not None:
             if self.timing is not None:
