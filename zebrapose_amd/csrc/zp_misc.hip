@@ -399,6 +399,9 @@ static inline int bn_bwd_pix(int P, int C) {
   const int lanes = C / 8 < 256 ? (C / 8 > 0 ? C / 8 : 1) : 256;
   const int R = 256 / lanes > 0 ? 256 / lanes : 1;
   int rows = 16;
+  // large layers (up2 at bs 32: 4096 slots at 16 rows): up to 64 rows while >= 1024 slots remain --
+  // fewer partials for the totals pass to read
+  while (rows < 64 && (P + R * rows * 2 - 1) / (R * rows * 2) >= 1024) rows <<= 1;
   while (rows > 4 && (P + R * rows - 1) / (R * rows) < 512) rows >>= 1;
   return R * rows;
 }
@@ -495,27 +498,28 @@ __global__ void __launch_bounds__(256) k_bn_bwd_reduce(const T* __restrict__ dy,
 }
 
 // totals over parts -> part[0][parts][c], part[1][parts][c]; dgamma / dbeta
-// block = 32 channels x 32 part lanes (1024 threads)
+// block = 8 channels x 128 part lanes (1024 threads; C / 8 blocks: 8 for a 64-channel BN, where the
+// former 32 x 32 layout ran 2 blocks for the whole GPU); each lane sums its parts (4 loads per
+// stream in flight), then a fixed pairwise tree over the 128 lanes (deterministic)
 __global__ void __launch_bounds__(1024) k_bn_bwd_totals(float* __restrict__ part, int parts, int C, float* dgamma,
                                                         float* dbeta, int accumulate) {
-  __shared__ double sh[2][32][33];
-  const int cl = threadIdx.x & 31, pl = threadIdx.x >> 5;
-  const int c = blockIdx.x * 32 + cl;
+  __shared__ double sh[2][128][9];
+  const int cl = threadIdx.x & 7, pl = threadIdx.x >> 3;
+  const int c = blockIdx.x * 8 + cl;
   double s = 0, q = 0;
   if (c < C)
-    for (int k0 = pl; k0 < parts; k0 += 32 * 8) {
-      // eight parts' loads in flight, summed in part order
-      // (clamped, unconditional loads: no branch between them)
-      float a[8], b[8];
+    for (int k0 = pl; k0 < parts; k0 += 128 * 4) {
+      // clamped, unconditional loads: no branch between them
+      float a[4], b[4];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int k = min(k0 + 32 * u, parts - 1);
+      for (int u = 0; u < 4; ++u) {
+        const int k = min(k0 + 128 * u, parts - 1);
         a[u] = part[(size_t)k * C + c];
         b[u] = part[((size_t)parts + 1 + k) * C + c];
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const bool in = k0 + 32 * u < parts;
+      for (int u = 0; u < 4; ++u) {
+        const bool in = k0 + 128 * u < parts;
         s += in ? (double)a[u] : 0.0;
         q += in ? (double)b[u] : 0.0;
       }
@@ -523,11 +527,16 @@ __global__ void __launch_bounds__(1024) k_bn_bwd_totals(float* __restrict__ part
   sh[0][pl][cl] = s;
   sh[1][pl][cl] = q;
   __syncthreads();
-  if (pl != 0 || c >= C) return;
-  for (int k = 1; k < 32; ++k) {
-    s += sh[0][k][cl];
-    q += sh[1][k][cl];
+  for (int w = 64; w > 0; w >>= 1) {
+    if (pl < w) {
+      sh[0][pl][cl] += sh[0][pl + w][cl];
+      sh[1][pl][cl] += sh[1][pl + w][cl];
+    }
+    __syncthreads();
   }
+  if (pl != 0 || c >= C) return;
+  s = sh[0][0][cl];
+  q = sh[1][0][cl];
   part[(size_t)parts * C + c] = (float)s;
   part[((size_t)parts + 1 + parts) * C + c] = (float)q;
   if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)q : (float)q;
@@ -1368,7 +1377,7 @@ extern "C" int zp_bn_bwd_reduce(const void* dy, int lddy, int cdy0, const void* 
 #undef ZP_BNR_T
 #undef ZP_BNR
   ZP_LAUNCH_CHECK("zp_bn_bwd_reduce");
-  hipLaunchKernelGGL(k_bn_bwd_totals, dim3((C + 31) / 32), dim3(1024), 0, st, partials, parts, C, dgamma, dbeta,
+  hipLaunchKernelGGL(k_bn_bwd_totals, dim3((C + 7) / 8), dim3(1024), 0, st, partials, parts, C, dgamma, dbeta,
                      accumulate);
   ZP_LAUNCH_CHECK("zp_bn_bwd_reduce totals");
   return ZP_OK;
