@@ -16,6 +16,7 @@ LAYERS = {  # name: (kind, cin, cout, k, d, hw)
     "up2conv": ("conv", 256, 256, 3, 1, 128),
     "l5": ("conv", 512, 512, 3, 4, 32),
     "up2T": ("convT", 320, 256, 3, 1, 64),
+    "up1T": ("convT", 256, 256, 3, 1, 32),
     "up1conv": ("conv", 256, 256, 3, 1, 64),
     "l1": ("conv", 64, 64, 3, 1, 64),
     "l2": ("conv", 128, 128, 3, 1, 32),
