@@ -132,8 +132,9 @@ int zp_conv2d_stat_parts(const zp_conv_args* a);
  * structure in one tile, 4 = k_conv3: the split-fp32 (ZP_F32X3) kernel, 5 = k_conv3s: its 3x3
  * stride-1 form with activation-strip reuse) */
 int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* stages, int* variant);
-/* Split-fp32 forms (ZP_F32X3 / ZP_F32H2) only: a launch whose grid would leave most CUs idle (a
- * one-sub NHWC conv with under 256 workgroups, e.g. bs = 1) is cut along K into slices whose f32
+/* Split-fp32 forms (ZP_F32X3 / ZP_F32H2) only: a launch whose grid would leave most CUs idle (an
+ * NHWC conv -- one sub-problem or several: ConvT phases, merged ASPP branches -- with under 256
+ * workgroups, e.g. bs = 1) is cut along K into slices whose f32
  * sums are finished (summed in slice order, then BN / residual / ReLU / split store) by a second
  * kernel, when zp_conv_args.stats points to an f32 workspace of this many bytes (0: not split;
  * stats NULL: not split).  Deterministic. */

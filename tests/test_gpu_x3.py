@@ -325,8 +325,8 @@ def test_split_accumulation_numerics(gpu, cin):
 
 @pytest.mark.parametrize("form", FORMS)
 @pytest.mark.parametrize("geom", [("conv", 512, 512, 3, 1, 4, 4, False, 32), ("conv", 256, 256, 3, 1, 2, 2, False, 32),
-                                  ("conv", 1280, 256, 1, 1, 0, 1, True, 8)],
-                         ids=["l5_d4", "l4_d2", "aspp_proj"])
+                                  ("conv", 1280, 256, 1, 1, 0, 1, True, 8), ("convT", 320, 256, 3, 2, 1, 1, False, 16)],
+                         ids=["l5_d4", "l4_d2", "aspp_proj", "convT_4phases"])
 def test_split_k_small_batch(gpu, geom, form):
     """bs = 1: the small-grid launches are cut along K (zp_conv2d_split_ws > 0, zp_conv_tuning key 9)
     and finished by k_splitk_epi; the result is as accurate as the unsplit kernel's (both against
@@ -336,7 +336,10 @@ def test_split_k_small_batch(gpu, geom, form):
     from zebrapose_amd.model import layers as LY
     kind, cin, cout, k, s, p, d, bias, H = geom
     torch.manual_seed(6)
-    conv = LY.Conv2d(cin, cout, k, s, p, d, bias=bias)
+    if kind == "conv":
+        conv = LY.Conv2d(cin, cout, k, s, p, d, bias=bias)
+    else:  # the four sub-pixel phases: a multi-sub launch split along K per phase
+        conv = LY.ConvTranspose2d(cin, cout, k, s, p, output_padding=1, bias=False)
     bn = LY.BatchNorm2d(cout)
     with torch.no_grad():
         bn.weight.uniform_(0.5, 1.5)
@@ -345,17 +348,19 @@ def test_split_k_small_batch(gpu, geom, form):
         bn.running_var.uniform_(0.5, 1.5)
     conv, bn = conv.to(gpu).eval(), bn.to(gpu).eval()
     unit = Unit(conv, bn, relu=True)
+    OH, OW = unit.out_hw(H, H)
     x = torch.randn(1, cin, H, H)
-    res = torch.randn(1, cout, H, H)
+    res = torch.randn(1, cout, OH, OW) if kind == "conv" else None
     ref = _ref64(kind, conv, bn, x, res, True, s, p, d)
-    xh, rh = x.permute(0, 2, 3, 1).contiguous(), res.permute(0, 2, 3, 1).contiguous()
+    xh = x.permute(0, 2, 3, 1).contiguous()
     eng = Engine(torch.nn.Module(), torch.float32, split=form)
-    xa, ra = Act(_split_act(xh, gpu, form)), Act(_split_act(rh, gpu, form))
+    xa = Act(_split_act(xh, gpu, form))
+    ra = None if res is None else Act(_split_act(res.permute(0, 2, 3, 1).contiguous(), gpu, form))
     out = {}
     for mode in (1, 0):
         old = L.lib.zp_conv_tuning(9, mode)
         try:
-            oa = Act(eng._empty((1, H, H, cout), gpu))
+            oa = Act(eng._empty((1, OH, OW, cout), gpu))
             eng.unit_fwd(unit, xa, oa, None, res=ra)
             torch.cuda.synchronize()
         finally:

@@ -2787,7 +2787,7 @@ extern "C" int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* st
 extern "C" long long zp_conv2d_split_ws(const zp_conv_args* a) {
   if (!a || (a->dtype != ZP_F32X3 && a->dtype != ZP_F32H2)) return 0;
   const int ns = conv3_nsplit(*a);
-  return ns > 1 ? (long long)ns * a->N * a->GH * a->GW * a->Cout * 4 : 0;
+  return ns > 1 ? (long long)ns * a->nsub * a->N * a->GH * a->GW * a->Cout * 4 : 0;
 }
 
 extern "C" int zp_conv_tuning(int key, int value) {

@@ -152,13 +152,14 @@ __device__ __forceinline__ void splitk_store(float* __restrict__ ws, const int C
   }
 }
 
-// split-K epilogue: thread per (grid point, 4 output channels); the slices summed in slice order
-// (deterministic), then conv3_epilogue's BN / bias, split residual, ReLU and split store (one
-// sub-problem, NHWC output)
+// split-K epilogue: thread per (grid point, 4 output channels) of sub-problem blockIdx.y; the
+// slices summed in slice order (deterministic), then conv3_epilogue's BN / bias, split residual,
+// ReLU and split store (NHWC output)
 template <int NPL>
 __global__ void k_splitk_epi(const zp_conv_args A, const float* __restrict__ ws, const int nsplit) {
   using SP = SplitF32<NPL>;
-  const zp_conv_sub& S = A.sub[0];
+  const zp_conv_sub& S = A.sub[blockIdx.y];
+  ws += (size_t)blockIdx.y * nsplit * ((size_t)A.N * A.GH * A.GW) * A.Cout;
   const int GHW = A.GH * A.GW, M = A.N * GHW, C4 = (A.Cout + 3) / 4;
   const long psy = (long)A.N * S.OH * S.OW * S.ldy;
   const long psr = (long)A.N * S.OH * S.OW * A.ldr;
@@ -266,9 +267,9 @@ __global__ void __launch_bounds__(128 * NWP) k_conv3(const zp_conv_args A, const
   __shared__ uint4 lds[ST * UNITS * 64];
   static_assert(ST * UNITS * 1024 <= 160 * 1024, "LDS");
   static_assert(((NPL - 1) * NT + WC + 3) * 1024 < 65536, "ds_read immediate range");
-  // split-K (nsplit > 1, one sub-problem): blockIdx.z is the K slice; its raw f32 sums go to ws
-  // [nsplit][M][Cout] and k_splitk_epi finishes them
-  const int tb = nsplit > 1 ? 0 : blockIdx.z, kz = nsplit > 1 ? blockIdx.z : 0;
+  // split-K (nsplit > 1): blockIdx.z = sub * nsplit + K slice; the slice's raw f32 sums go to ws
+  // [nsub][nsplit][M][Cout] and k_splitk_epi finishes them
+  const int tb = (int)blockIdx.z / nsplit, kz = (int)blockIdx.z - tb * nsplit;
   const zp_conv_sub& S = A.sub[tb];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -629,7 +630,7 @@ __global__ void __launch_bounds__(128 * NWP) k_conv3(const zp_conv_args A, const
 #pragma unroll
       for (int j = 0; j < WP; ++j) flush_corr<NPL>(acc[i][j], acc2[PIPE ? i : 0][PIPE ? j : 0]);
   }
-  if (nsplit > 1) splitk_store<WC, WP>(ws + (size_t)kz * M * A.Cout, A.Cout, acc, p0, c0, wc, wp, lane, M);
+  if (nsplit > 1) splitk_store<WC, WP>(ws + ((size_t)tb * nsplit + kz) * M * A.Cout, A.Cout, acc, p0, c0, wc, wp, lane, M);
   else conv3_epilogue<NPL, WC, WP>(A, S, acc, p0, c0, wc, wp, lane, M, GHW, flags);
 }
 
@@ -987,13 +988,14 @@ int conv3_splitk_mode(int v) {
 // 256 workgroups -- bs = 1: layer5's 512 -> 512 runs as 64 workgroups over 144 K steps) is cut
 // along K into up to 16 slices of >= 8 steps, for about 512 workgroups
 int conv3_nsplit(const zp_conv_args& a) {
-  if (!g_splitk || a.nsub != 1 || a.out_mode != ZP_OUT_NHWC) return 1;
+  if (!g_splitk || a.out_mode != ZP_OUT_NHWC || a.nsub < 1) return 1;
   const int tc = conv3_tc(a);
-  const long blocks = (long)ceil_div((long)a.N * a.GH * a.GW, conv3_tp(a, tc)) * ceil_div(a.Cout, tc);
-  const int nK = a.sub[0].ntaps * (a.Cin / 32);
+  const long blocks = (long)ceil_div((long)a.N * a.GH * a.GW, conv3_tp(a, tc)) * ceil_div(a.Cout, tc) * a.nsub;
+  int nK = 1 << 30;  // the shortest sub-problem's K steps (ConvT phases: 1 .. 4 taps)
+  for (int s = 0; s < a.nsub; ++s) nK = min(nK, a.sub[s].ntaps * (a.Cin / 32));
   if (blocks >= 256) return 1;
   int ns = 1;
-  while (ns < 16 && blocks * ns * 2 <= 512 && nK / (ns * 2) >= 8) ns *= 2;
+  while (ns < 16 && blocks * ns * 2 <= 512 && nK / (ns * 2) >= (a.nsub > 1 ? 4 : 8)) ns *= 2;
   return ns;
 }
 
@@ -1013,7 +1015,7 @@ static void conv3_dispatch(const zp_conv_args& a, const conv_taps& tg, int tc, h
   }
   const int tp = conv3_tp(a, tc);
   const int gx = ceil_div((long)a.N * a.GH * a.GW, tp), gy = ceil_div(a.Cout, tc);
-  const dim3 grid(gx, gy, ns > 1 ? ns : a.nsub);
+  const dim3 grid(gx, gy, ns * a.nsub);
   // 128-channel layers: 8 waves, 128 x 256, 2-deep ring (two planes: 3-deep, the same LDS);
   // smaller tiles: register-pipelined one wave per SIMD over 128 pixels (ZP_CONV3_SCHED=1: the
   // 128-channel tile that way too)
@@ -1029,7 +1031,7 @@ static void conv3_dispatch(const zp_conv_args& a, const conv_taps& tg, int tc, h
   if (ns > 1) {
     const long total = (long)a.N * a.GH * a.GW * ((a.Cout + 3) / 4);
     const int blocks = (int)(total + 255) / 256 < 8192 ? (int)((total + 255) / 256) : 8192;
-    hipLaunchKernelGGL((k_splitk_epi<NPL>), dim3(blocks), dim3(256), 0, st, a, ws, ns);
+    hipLaunchKernelGGL((k_splitk_epi<NPL>), dim3(blocks, a.nsub), dim3(256), 0, st, a, ws, ns);
   }
 }
 
