@@ -67,6 +67,17 @@ extern "C" {
  * Forward (eval) kernels only. */
 #define ZP_F32H2 4
 
+/* Range guard of ZP_F32H2.  A finite value at or above 65520 in magnitude has no two-plane form
+ * (hi rounds to fp16 infinity).  Every ZP_F32H2 store -- the zp_conv2d epilogues (split-K's
+ * included), zp_im2col_split, the f32 stem writing ZP_OUT_NHWC_H2 and zp_pack_weight(_multi) --
+ * sets *flag = 1 (a device word) when it meets one; nothing clears it.  The flag is per device
+ * (the calling thread's current device at registration; launches read it at enqueue time, so a
+ * captured hipGraph keeps the word of its capture).  NULL unregisters.  The max / average pools and
+ * broadcasts of split tensors cannot leave the range of their inputs and do not check.  The Python
+ * engine registers one word, reads it once per fp32 eval forward and re-runs an overflowing forward
+ * on the full-range ZP_F32X3 form (reference forward: model/BinaryCodeNet.py:161-174, plain f32). */
+int zp_split_range_flag(unsigned int* flag);
+
 /* zp_conv_args.out_mode */
 #define ZP_OUT_NHWC 0       /* y[n, oy, ox, cy0 + c] (ldy elements per pixel), dtype of the call */
 #define ZP_OUT_HEAD_NCHW 1  /* c == 0 -> y (f32 [N,1,OH,OW]); c >= 1 -> y2 (f32 [N,Cout-1,OH,OW]) */

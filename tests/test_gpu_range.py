@@ -1,0 +1,144 @@
+"""Range guard of the two-plane split-fp32 engine (include/zp.h zp_split_range_flag).
+
+The default fp32 eval engine stores activations and weights as two fp16 planes, so a finite value
+at or above 65520 has no representation.  The reference computes in plain f32 over the whole range
+(model/BinaryCodeNet.py:161-174).  These tests push values past fp16's range three ways -- a BN
+gamma / beta scaled by 1e5 (activations), a conv weight scaled by 1e7 (the packer), an input scaled
+by 1e5 (the stem's im2col) -- and require:
+  * the device flag fires and the forward is re-run on the full-range x3 engine (sticky);
+  * the outputs are finite and within 1e-3 of the oracle (ref_cpu.forward, CPU f32) relative to the
+    logit scale: max |d| <= 1e-3 * max |ref|;
+  * the same through GraphedInference, where the overflow shows up only at replay time;
+  * with the guard off, the two-plane forward of the same state is wrong by more than 1% of the
+    logit scale -- silently, since a ReLU maps the NaN an infinity becomes to 0 (the guard is what
+    fixes it);
+  * values below fp16's normal range (activations ~1e-7) need no fallback and stay within 1e-3.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _net(golden, mutate=None):
+    from oracle import ref_cpu
+    from zebrapose_amd.model.BinaryCodeNet import BinaryCodeNet_Deeplab
+    sd = ref_cpu.synthetic_state(34, 16, 0, dict(golden("r34_bn_buffers.npz")))
+    if mutate is not None:
+        mutate(sd)
+    net = BinaryCodeNet_Deeplab(34, 16, 2, concat=True, output_kernel_size=1, precision="fp32")
+    net.load_state_dict(sd)
+    net.net.f32_split = "h2"
+    return net.cuda().eval(), sd
+
+
+def _oracle(sd, x):
+    from oracle import ref_cpu
+    with torch.no_grad():
+        m, c = ref_cpu.forward(sd, torch.from_numpy(x))
+    return m.numpy(), c.numpy()
+
+
+def _close(got, ref, what):
+    got = [g.cpu().numpy() if torch.is_tensor(g) else g for g in got]
+    scale = max(float(np.abs(r).max()) for r in ref)
+    for g, r in zip(got, ref):
+        assert np.isfinite(g).all(), f"{what}: non-finite output"
+        d = float(np.abs(g - r).max())
+        print(f"{what}: logit scale {scale:.3g}, max |d| {d:.3g} ({d / scale:.2e} of the scale)")
+        assert d <= 1e-3 * scale, (what, d, scale)
+
+
+def _err(m, c, ref):
+    """max |d| relative to the logit scale (inf when an output is not finite)"""
+    got = (m.cpu().numpy(), c.cpu().numpy())
+    if not all(np.isfinite(g).all() for g in got):
+        return float("inf")
+    scale = max(float(np.abs(r).max()) for r in ref)
+    d = max(float(np.abs(g - r).max()) for g, r in zip(got, ref))
+    print(f"unguarded h2: max |d| {d:.3g} = {d / scale:.2e} of the logit scale {scale:.3g}")
+    return d / scale
+
+
+def _scale_bn(key, s):
+    def f(sd):
+        sd[key + ".weight"].mul_(s)
+        sd[key + ".bias"].mul_(s)
+    return f
+
+
+@pytest.mark.parametrize("case", ["bn_gamma", "conv_weight"])
+def test_eager_overflow_falls_back_to_x3(golden, case):
+    if case == "bn_gamma":  # layer5's output (x_high) reaches ~1e5 and every later layer follows
+        mutate = _scale_bn("net.resnet.layer5.2.bn2", 1e5)
+    else:  # weights beyond fp16's range (He-normal ~0.04 -> ~4e5): the split packer raises the flag
+
+        def mutate(sd):
+            sd["net.aspp.conv_1x1_3.weight"].mul_(1e7)
+    net, sd = _net(golden, mutate)
+    x = golden("r34_fwd64.npz")["fwd64_x"]
+    ref = _oracle(sd, x)
+    # control: with the guard off the two-plane forward is wrong -- silently: an infinity becomes
+    # NaN in the next convolution's sums and the ReLU (fmaxf) turns NaN into 0, so the logits can
+    # come out finite
+    net.net.range_check = False
+    with torch.no_grad():
+        m, c = net(torch.from_numpy(x).cuda())
+    assert _err(m, c, ref) > 1e-2, "expected the unguarded h2 forward to be wrong"
+    net.net.range_check = True
+    with pytest.warns(RuntimeWarning, match="fp16's range"):
+        with torch.no_grad():
+            m, c = net(torch.from_numpy(x).cuda())
+    assert net.net.range_fallbacks == 1 and net.net.f32_split == "x3"
+    assert net.net.eval_engine().split == "x3"
+    _close((m, c), ref, f"eager {case}")
+    # sticky: the next forward runs x3 directly (no second fallback)
+    with torch.no_grad():
+        m2, c2 = net(torch.from_numpy(x).cuda())
+    assert net.net.range_fallbacks == 1
+    assert torch.equal(m, m2) and torch.equal(c, c2)
+
+
+def test_graph_replay_overflow_recaptures_on_x3(golden):
+    """Input-dependent overflow: the graph is captured on h2 (warm-up inputs are zeros), a replay
+    with crops scaled by 1e5 raises the flag in the stem's im2col, and the step is re-captured and
+    replayed on x3."""
+    from zebrapose_amd.graphs import GraphedInference
+    net, sd = _net(golden)
+    x = golden("r34_fwd64.npz")["fwd64_x"]
+    gi = GraphedInference(net, batch=x.shape[0], size=x.shape[2])
+    assert gi._flag is not None and net.net.eval_engine().split == "h2"
+    m, c = gi(torch.from_numpy(x).cuda())
+    assert gi.range_fallbacks == 0
+    _close((m, c), _oracle(sd, x), "graph h2, in range")
+    xs = (x * np.float32(1e5)).astype(np.float32)
+    with pytest.warns(RuntimeWarning, match="fp16's range"):
+        m, c = gi(torch.from_numpy(xs).cuda())
+    assert gi.range_fallbacks == 1 and net.net.f32_split == "x3" and gi._flag is None
+    _close((m, c), _oracle(sd, xs), "graph after fallback, scaled input")
+    m, c = gi(torch.from_numpy(x).cuda())  # the x3 graph keeps serving in-range crops
+    assert gi.range_fallbacks == 1
+    _close((m, c), _oracle(sd, x), "graph x3, in range")
+
+
+def test_eager_scaled_input_falls_back(golden):
+    net, sd = _net(golden)
+    x = golden("r34_fwd64.npz")["fwd64_x"]
+    xs = (x * np.float32(1e5)).astype(np.float32)
+    with pytest.warns(RuntimeWarning):
+        with torch.no_grad():
+            m, c = net(torch.from_numpy(xs).cuda())
+    assert net.net.range_fallbacks == 1
+    _close((m, c), _oracle(sd, xs), "eager scaled input")
+
+
+def test_tiny_activations_need_no_fallback(golden):
+    """Below fp16's normal range hi is subnormal and the absolute error is 2^-36: layer5's output
+    at ~1e-7 needs no fallback and the logits stay within the tolerance."""
+    net, sd = _net(golden, _scale_bn("net.resnet.layer5.2.bn2", 1e-7))
+    x = golden("r34_fwd64.npz")["fwd64_x"]
+    with torch.no_grad():
+        m, c = net(torch.from_numpy(x).cuda())
+    assert net.net.range_fallbacks == 0 and net.net.eval_engine().split == "h2"
+    _close((m, c), _oracle(sd, x), "eager tiny x_high")

@@ -116,6 +116,7 @@ _SIGS = {
     "zp_crop_gt": (i32, [vp, vp, vp, i32, i32, i32, vp, vp, i32, i32, i32, vp, vp, vp, vp]),
     "zp_adam_multi": (i32, [i32, vp, vp, vp, vp, vp, f64, f64, f64, f64, i64, vp]),
     "zp_adam_multi_dev": (i32, [i32, vp, vp, vp, vp, vp, f64, f64, f64, f64, vp, vp]),
+    "zp_split_range_flag": (i32, [vp]),
 }
 
 
@@ -158,6 +159,24 @@ def ptr(t) -> int | None:
     if t is None:
         return None
     return t.data_ptr()
+
+
+_RANGE_FLAGS = {}
+
+
+def range_flag(device) -> torch.Tensor:
+    """The device word registered with zp_split_range_flag (include/zp.h) for ``device``: int32 [1],
+    set to 1 by any ZP_F32H2 store that meets a finite value beyond fp16's range.  Created and
+    registered on first use (outside a graph capture: the engine's eager forward does it)."""
+    dev = torch.device(device)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    t = _RANGE_FLAGS.get(idx)
+    if t is None:
+        t = torch.zeros(1, dtype=torch.int32, device=f"cuda:{idx}")
+        with torch.cuda.device(idx):
+            check(lib.zp_split_range_flag(t.data_ptr()), "zp_split_range_flag")
+        _RANGE_FLAGS[idx] = t
+    return t
 
 
 def dtype_code(dt) -> int:

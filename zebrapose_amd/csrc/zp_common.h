@@ -58,8 +58,9 @@ __device__ __forceinline__ float join3(bf16_t h, bf16_t m, bf16_t l) { return (b
 //   SplitF32<3>: bf16 hi + mid + lo, exact (split3 / join3);
 //   SplitF32<2>: IEEE fp16 hi + lo' with v ~ hi + lo' * 2^-11: hi = RNE(v), lo' = RNE((v - hi) * 2^11)
 //     (the residual is scaled into fp16's normal range; 22 significant bits, |v - join| <= 2^-23 |v|
-//     for |v| in fp16's normal range).  Finite |v| > 65504 rounds hi to infinity (the network's
-//     activations and weights are far below); non-finite values keep lo' = 0.
+//     for |v| in fp16's normal range, 2^-36 absolute below it).  Finite |v| >= 65520 rounds hi to
+//     infinity: every store site raises the range flag for it (h2_overflow below) and the engine
+//     re-runs the forward on the full-range SplitF32<3>; non-finite values keep lo' = 0.
 // CS: the factor the lo-plane products carry (k_conv3 scales its correction accumulator by it).
 template <int NPL> struct SplitF32;
 template <> struct SplitF32<3> {
@@ -81,6 +82,20 @@ template <> struct SplitF32<2> {
     return __builtin_fmaf((float)__builtin_bit_cast(f16_t, p[1]), CS, (float)__builtin_bit_cast(f16_t, p[0]));
   }
 };
+
+// Range guard of the two-plane form (zp_split_range_flag): a finite value at or above 65520 in
+// magnitude rounds hi to fp16 infinity.  Every ZP_F32H2 store site ORs this per lane and, at the
+// end, raises the registered device word with a plain vector store (any lane, value 1).
+__device__ __forceinline__ bool h2_overflow(float v) {
+  const float a = __builtin_fabsf(v);
+  return a >= 65520.f && a < __builtin_inff();
+}
+__device__ __forceinline__ void raise_range_flag(unsigned* flag, bool bad) {
+  if (bad && flag) *flag = 1u;
+}
+// the word registered for the calling thread's current device (NULL: no guard); read by the host
+// launch code of every split store (a captured hipGraph keeps the pointer of its capture)
+unsigned* range_flag();
 
 template <typename T> struct Elem;
 template <> struct Elem<float> {

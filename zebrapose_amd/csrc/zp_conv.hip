@@ -37,7 +37,7 @@ template <typename T, int WC, int WP, int NWP>
 __device__ __forceinline__ void conv_epilogue(const zp_conv_args& A, const zp_conv_sub& S, f32x4 (&acc)[WC][WP],
                                               const int p0, const int c0, const int wc, const int wp, const int lane,
                                               const int M, const int GHW, const int bx, const int zi,
-                                              const int nz) {
+                                              const int nz, unsigned* rflag = nullptr) {
   // ---------------- epilogue ----------------
   // (zi, nz): this tile's sub-problem and the sub-problem count, for the statistics part index
   // (blockIdx.z / gridDim.z, except in k_conv_quad, whose tiles hold all four sub-pixel phases)
@@ -208,6 +208,7 @@ __device__ __forceinline__ void conv_epilogue(const zp_conv_args& A, const zp_co
               SplitF32<2>::split(v[r], q);
               Y[r] = q[0];
               Y[r + psy] = q[1];
+              raise_range_flag(rflag, h2_overflow(v[r]));
             }
           }
           continue;
@@ -618,7 +619,7 @@ __global__ void __launch_bounds__(128 * NWP) k_conv(const zp_conv_args A, const 
 
   if (pingpong && wid < 4) __builtin_amdgcn_s_barrier();  // same barrier count for both groups
 
-  conv_epilogue<T, WC, WP, NWP>(A, S, acc, p0, c0, wc, wp, lane, M, GHW, bx, blockIdx.z, gridDim.z);
+  conv_epilogue<T, WC, WP, NWP>(A, S, acc, p0, c0, wc, wp, lane, M, GHW, bx, blockIdx.z, gridDim.z, TG.rflag);
 }
 
 // ------------------------------------------------------------------------------------
@@ -2464,6 +2465,7 @@ extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
                  "zp_conv2d: input (%lld B) / weights (%lld B) must stay below 2 GiB per launch (split the batch)",
                  xb, wb);
     tg.x_bytes = (unsigned)xb;
+    tg.rflag = a.out_mode == ZP_OUT_NHWC_H2 ? range_flag() : nullptr;
     for (int s = 0; s < a.nsub; ++s) {
       const zp_conv_sub& S = a.sub[s];
       tg.w_bytes[s] = (unsigned)wb;

@@ -24,9 +24,11 @@ __device__ __forceinline__ void block_barrier() {
 template <int NPL, int WC, int WP>
 __device__ __forceinline__ void conv3_epilogue(const zp_conv_args& A, const zp_conv_sub& S, f32x4 (&acc)[WC][WP],
                                                const int p0, const int c0, const int wc, const int wp,
-                                               const int lane, const int M, const int GHW, const int flags) {
+                                               const int lane, const int M, const int GHW, const int flags,
+                                               unsigned* rflag) {
   using SP = SplitF32<NPL>;
   const int lr = lane & 15;
+  bool bad = false;  // NPL == 2: a finite value beyond fp16's range (zp_split_range_flag)
   int pn[WP], poy[WP], pox[WP];
   bool pok[WP];
 #pragma unroll
@@ -107,7 +109,10 @@ __device__ __forceinline__ void conv3_epilogue(const zp_conv_args& A, const zp_c
       }
       unsigned short q[4][NPL];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) SP::split(v[r], q[r]);
+      for (int r = 0; r < 4; ++r) {
+        SP::split(v[r], q[r]);
+        if constexpr (NPL == 2) bad |= h2_overflow(v[r]);
+      }
       if ((flags & 16384) && v[0] != 1.f) continue;  // diagnostic: no stores (unless a value is exactly 1)
       unsigned short* Y = (unsigned short*)S.y + pix * S.ldy + S.cy0 + cf;
       if (full) {
@@ -124,6 +129,7 @@ __device__ __forceinline__ void conv3_epilogue(const zp_conv_args& A, const zp_c
       }
     }
   }
+  if constexpr (NPL == 2) raise_range_flag(rflag, bad);
 }
 
 // split-K slice: the raw f32 sums of this tile into ws [M][Cout] (acc[i][j] = 4 consecutive output
@@ -156,8 +162,9 @@ __device__ __forceinline__ void splitk_store(float* __restrict__ ws, const int C
 // slices summed in slice order (deterministic), then conv3_epilogue's BN / bias, split residual,
 // ReLU and split store (NHWC output)
 template <int NPL>
-__global__ void k_splitk_epi(const zp_conv_args A, const float* __restrict__ ws, const int nsplit) {
+__global__ void k_splitk_epi(const zp_conv_args A, const float* __restrict__ ws, const int nsplit, unsigned* rflag) {
   using SP = SplitF32<NPL>;
+  bool bad = false;
   const zp_conv_sub& S = A.sub[blockIdx.y];
   ws += (size_t)blockIdx.y * nsplit * ((size_t)A.N * A.GH * A.GW) * A.Cout;
   const int GHW = A.GH * A.GW, M = A.N * GHW, C4 = (A.Cout + 3) / 4;
@@ -189,11 +196,13 @@ __global__ void k_splitk_epi(const zp_conv_args A, const float* __restrict__ ws,
       if (A.relu) o = fmaxf(o, 0.f);
       unsigned short q[NPL];
       SP::split(o, q);
+      if constexpr (NPL == 2) bad |= h2_overflow(o);
       unsigned short* Y = (unsigned short*)S.y + pix * S.ldy + S.cy0 + cf + r;
 #pragma unroll
       for (int pl = 0; pl < NPL; ++pl) Y[pl * psy] = q[pl];
     }
   }
+  if constexpr (NPL == 2) raise_range_flag(rflag, bad);
 }
 
 // The correction terms of a split product (besides hi*hi, plane 0 x plane 0, into the main
@@ -631,7 +640,7 @@ __global__ void __launch_bounds__(128 * NWP) k_conv3(const zp_conv_args A, const
       for (int j = 0; j < WP; ++j) flush_corr<NPL>(acc[i][j], acc2[PIPE ? i : 0][PIPE ? j : 0]);
   }
   if (nsplit > 1) splitk_store<WC, WP>(ws + ((size_t)tb * nsplit + kz) * M * A.Cout, A.Cout, acc, p0, c0, wc, wp, lane, M);
-  else conv3_epilogue<NPL, WC, WP>(A, S, acc, p0, c0, wc, wp, lane, M, GHW, flags);
+  else conv3_epilogue<NPL, WC, WP>(A, S, acc, p0, c0, wc, wp, lane, M, GHW, flags, TG.rflag);
 }
 
 // ------------------------------------------------------------------------------------
@@ -659,6 +668,7 @@ struct strip3_geo {
   int W, TR, SW, SR;            // width, rows per tile, strip width W + 2 pad, strip rows TR * SW
   int ty0, dty, tx0, dtx, pad;  // tap grid (3 x 3) and the halo width
   unsigned x_bytes, w_bytes;
+  unsigned* rflag;              // range flag of the two-plane stores (conv_taps::rflag)
 };
 
 template <int NPL, int WC>
@@ -889,7 +899,7 @@ __global__ void __launch_bounds__(512) k_conv3s(const zp_conv_args A, const stri
     group(O{}, O{}, g + 1);  // steps 6k+3..6k+5: weight slots 1, 0, 1
   }
   (void)nw_units;
-  conv3_epilogue<NPL, WC, WP>(A, S, acc, p0, c0, wc, wp, lane, M, GHW, flags);
+  conv3_epilogue<NPL, WC, WP>(A, S, acc, p0, c0, wc, wp, lane, M, GHW, flags, SG.rflag);
 }
 
 
@@ -1008,6 +1018,7 @@ static void conv3_dispatch(const zp_conv_args& a, const conv_taps& tg, int tc, h
   if (ns == 1 && conv3_strip(a, tc, &s3)) {
     s3.x_bytes = tg.x_bytes;
     s3.w_bytes = tg.w_bytes[0];
+    s3.rflag = tg.rflag;
     const dim3 sgrid((unsigned)(((long)a.N * a.GH * a.GW) / 256), (unsigned)(a.Cout / tc), 1);
     if (tc == 128) hipLaunchKernelGGL((k_conv3s<NPL, 4>), sgrid, dim3(512), 0, st, a, s3, fl);
     else hipLaunchKernelGGL((k_conv3s<NPL, 2>), sgrid, dim3(512), 0, st, a, s3, fl);
@@ -1031,7 +1042,7 @@ static void conv3_dispatch(const zp_conv_args& a, const conv_taps& tg, int tc, h
   if (ns > 1) {
     const long total = (long)a.N * a.GH * a.GW * ((a.Cout + 3) / 4);
     const int blocks = (int)(total + 255) / 256 < 8192 ? (int)((total + 255) / 256) : 8192;
-    hipLaunchKernelGGL((k_splitk_epi<NPL>), dim3(blocks, a.nsub), dim3(256), 0, st, a, ws, ns);
+    hipLaunchKernelGGL((k_splitk_epi<NPL>), dim3(blocks, a.nsub), dim3(256), 0, st, a, ws, ns, tg.rflag);
   }
 }
 
@@ -1066,6 +1077,7 @@ int conv3_launch(const zp_conv_args& a, hipStream_t st, int fl) {
                "zp_conv2d: split input (%lld B) / weights (%lld B) must stay below 2 GiB per launch (split the batch)",
                xb, wb);
   tg.x_bytes = (unsigned)xb;
+  tg.rflag = npl == 2 ? range_flag() : nullptr;
   for (int s = 0; s < a.nsub; ++s) {
     const zp_conv_sub& S = a.sub[s];
     tg.w_bytes[s] = (unsigned)wb;

@@ -51,6 +51,7 @@ __device__ __forceinline__ void vm_wait() {
 struct conv_taps {
   int ny[ZP_MAX_SUB], nx[ZP_MAX_SUB], ty0[ZP_MAX_SUB], dty[ZP_MAX_SUB], tx0[ZP_MAX_SUB], dtx[ZP_MAX_SUB];
   unsigned x_bytes, w_bytes[ZP_MAX_SUB];
+  unsigned* rflag;  // two-plane split stores: the range flag (range_flag()), or NULL
 };
 
 // LDS byte address of a __shared__ pointer

@@ -96,8 +96,9 @@ __global__ void k_pack(const PackArgs a) {
 // split-fp32 packing (ZP_F32X3 / ZP_F32H2): the same element map as k_pack, the f32 weight split
 // into NPL planes [NPL][rows_pad][k_pad] (SplitF32<NPL>)
 template <int NPL>
-__global__ void k_pack_split(const PackArgs a) {
+__global__ void k_pack_split(const PackArgs a, unsigned* rflag) {
   const long total = (long)a.rows_pad * a.k_pad;
+  bool bad = false;
   const int rows = a.transposed ? a.d1 : a.d0;
   const int chans = a.transposed ? a.d0 : a.d1;
   unsigned short* d = (unsigned short*)a.dst;
@@ -113,9 +114,11 @@ __global__ void k_pack_split(const PackArgs a) {
     }
     unsigned short q[NPL];
     SplitF32<NPL>::split(v, q);
+    if constexpr (NPL == 2) bad |= h2_overflow(v);
 #pragma unroll
     for (int p = 0; p < NPL; ++p) d[e + p * total] = q[p];
   }
+  if constexpr (NPL == 2) raise_range_flag(rflag, bad);
 }
 
 // one launch for many pack jobs: blockIdx.y = job (read once, uniform), threads over the job's
@@ -123,7 +126,7 @@ __global__ void k_pack_split(const PackArgs a) {
 // layout, so a wave reads one contiguous span) and writes them at k = t * cstride + c (adjacent
 // threads -> adjacent k: coalesced 2-byte stores), then the pair's share of the k_pad tail (zeros).
 // Same result as zp_pack_weight per job.
-__device__ __forceinline__ void pack_store(const zp_pack_job& a, int d, float v) {
+__device__ __forceinline__ void pack_store(const zp_pack_job& a, int d, float v, unsigned* rflag) {
   if (a.dtype == ZP_F32X3) {  // three planes of rows_pad * k_pad
     const size_t ps = (size_t)a.rows_pad * a.k_pad;
     unsigned short q[3];
@@ -134,6 +137,7 @@ __device__ __forceinline__ void pack_store(const zp_pack_job& a, int d, float v)
     unsigned short q[2];
     SplitF32<2>::split(v, q);
     for (int p = 0; p < 2; ++p) ((unsigned short*)a.dst)[d + p * ps] = q[p];
+    raise_range_flag(rflag, h2_overflow(v));
   } else if (a.dtype == ZP_BF16) ((bf16_t*)a.dst)[d] = f2bf(v);
   else if (a.dtype == ZP_F16) ((f16_t*)a.dst)[d] = (f16_t)v;
   else ((float*)a.dst)[d] = v;
@@ -146,7 +150,7 @@ __device__ __forceinline__ void pack_store(const zp_pack_job& a, int d, float v)
 // below it read the transposed layouts one scattered 36-byte run per lane (r02 PMC: 1.3 GB moved per
 // 116 MB of weights).
 constexpr int PK_R = 8, PK_C = 64, PK_ROW = PK_C * 9 + 1;  // +1: the transposed fill hits distinct banks
-__global__ void __launch_bounds__(256) k_pack_multi(const zp_pack_job* __restrict__ jobs) {
+__global__ void __launch_bounds__(256) k_pack_multi(const zp_pack_job* __restrict__ jobs, unsigned* rflag) {
   const zp_pack_job& a = jobs[blockIdx.y];
   // tap offsets in LDS (a private copy of the job's tap arrays would live in scratch)
   __shared__ int toff[ZP_MAX_TAPS];
@@ -181,12 +185,12 @@ __global__ void __launch_bounds__(256) k_pack_multi(const zp_pack_job* __restric
       for (int e = threadIdx.x; e < PK_R * a.ntaps * PK_C; e += blockDim.x) {
         const int cl = e % PK_C, q = e / PK_C, t = q % a.ntaps, rl = q / a.ntaps;
         const int r = r0 + rl;
-        if (cl < cw && r < a.rows_pad) pack_store(a, r * a.k_pad + t * a.cstride + c0 + cl, tile[rl * PK_ROW + cl * 9 + toff[t]]);
+        if (cl < cw && r < a.rows_pad) pack_store(a, r * a.k_pad + t * a.cstride + c0 + cl, tile[rl * PK_ROW + cl * 9 + toff[t]], rflag);
       }
       if (c0 == 0)  // the row's k_pad tail
         for (int e = threadIdx.x; e < PK_R * (a.k_pad - kt); e += blockDim.x) {
           const int rl = e / (a.k_pad - kt), kk = kt + e % (a.k_pad - kt);
-          if (r0 + rl < a.rows_pad) pack_store(a, (r0 + rl) * a.k_pad + kk, 0.f);
+          if (r0 + rl < a.rows_pad) pack_store(a, (r0 + rl) * a.k_pad + kk, 0.f, rflag);
         }
       __syncthreads();
     }
@@ -205,11 +209,11 @@ __global__ void __launch_bounds__(256) k_pack_multi(const zp_pack_job* __restric
       for (int t = 0; t < 9; ++t) v[t] = (live && t < a.ntaps) ? sp[toff[t]] : 0.f;
 #pragma unroll
       for (int t = 0; t < 9; ++t)
-        if (t < a.ntaps) pack_store(a, o + t * a.cstride, v[t]);
+        if (t < a.ntaps) pack_store(a, o + t * a.cstride, v[t], rflag);
     } else {
-      for (int t = 0; t < a.ntaps; ++t) pack_store(a, o + t * a.cstride, live ? sp[toff[t]] : 0.f);
+      for (int t = 0; t < a.ntaps; ++t) pack_store(a, o + t * a.cstride, live ? sp[toff[t]] : 0.f, rflag);
     }
-    for (int kk = kt + c; kk < a.k_pad; kk += a.cstride) pack_store(a, r * a.k_pad + kk, 0.f);
+    for (int kk = kt + c; kk < a.k_pad; kk += a.cstride) pack_store(a, r * a.k_pad + kk, 0.f, rflag);
   }
 }
 
@@ -756,8 +760,9 @@ __global__ void k_maxpool(const T* __restrict__ x, int B, int IH, int IW, int ld
 // read by <= 16 overlapping 7x7 / s2 windows), each element split into the NPL planes
 template <int NPL>
 __global__ void k_im2col_split(const float* __restrict__ x, int B, int H, int W, int ldx, int C, int k, int s, int p,
-                               int OH, int OW, int kpad, unsigned short* __restrict__ y) {
+                               int OH, int OW, int kpad, unsigned short* __restrict__ y, unsigned* rflag) {
   const int KC = kpad / 8, KK = k * k * C;
+  bool bad = false;
   const long total = (long)B * OH * OW * KC;
   const long plane = (long)B * OH * OW * kpad;
   for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
@@ -781,6 +786,7 @@ __global__ void k_im2col_split(const float* __restrict__ x, int B, int H, int W,
           if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) v = x[(((long)b * H + iy) * W + ix) * ldx + c];
         }
         SplitF32<NPL>::split(v, q[h]);
+        if constexpr (NPL == 2) bad |= h2_overflow(v);
       }
 #pragma unroll
       for (int pl = 0; pl < NPL; ++pl) w[pl][i >> 1] = (uint32_t)q[0][pl] | ((uint32_t)q[1][pl] << 16);
@@ -789,6 +795,7 @@ __global__ void k_im2col_split(const float* __restrict__ x, int B, int H, int W,
 #pragma unroll
     for (int pl = 0; pl < NPL; ++pl) *(uint4*)(yo + pl * plane) = make_uint4(w[pl][0], w[pl][1], w[pl][2], w[pl][3]);
   }
+  if constexpr (NPL == 2) raise_range_flag(rflag, bad);
 }
 
 // Split-fp32 max pool (NPL planes, SplitF32<NPL>): the 3x3 window max of the joined f32 values
@@ -1239,6 +1246,22 @@ using namespace zp;
     else hipLaunchKernelGGL(KERNEL<float>, grid, block, 0, st, __VA_ARGS__);            \
   } while (0)
 
+// zp_split_range_flag registry: one word per device, set by the caller
+static unsigned* g_range_flag[64];
+
+unsigned* zp::range_flag() {
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= 64) return nullptr;
+  return g_range_flag[d];
+}
+
+extern "C" int zp_split_range_flag(unsigned int* flag) {
+  int d = 0;
+  ZP_CHECK_ARG(hipGetDevice(&d) == hipSuccess && d >= 0 && d < 64, "zp_split_range_flag: no current device");
+  g_range_flag[d] = flag;
+  return ZP_OK;
+}
+
 extern "C" int zp_abi_version(void) { return ZP_ABI_VERSION; }
 extern "C" const char* zp_last_error(void) { return g_err; }
 extern "C" int zp_conv_rows_pad(int Cout) {
@@ -1263,9 +1286,11 @@ extern "C" int zp_pack_weight(const float* src, int d0, int d1, int kh, int kw, 
     a.kx[t] = (signed char)kx[t];
   }
   if (dtype == ZP_F32X3)
-    hipLaunchKernelGGL(k_pack_split<3>, dim3(grid_for((long)rows_pad * k_pad)), dim3(256), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(k_pack_split<3>, dim3(grid_for((long)rows_pad * k_pad)), dim3(256), 0, (hipStream_t)stream, a,
+                       nullptr);
   else if (dtype == ZP_F32H2)
-    hipLaunchKernelGGL(k_pack_split<2>, dim3(grid_for((long)rows_pad * k_pad)), dim3(256), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(k_pack_split<2>, dim3(grid_for((long)rows_pad * k_pad)), dim3(256), 0, (hipStream_t)stream, a,
+                       range_flag());
   else
     ZP_BY_DTYPE(dtype, k_pack, dim3(grid_for((long)rows_pad * k_pad)), dim3(256), (hipStream_t)stream, a);
   ZP_LAUNCH_CHECK("zp_pack_weight");
@@ -1277,7 +1302,7 @@ extern "C" int zp_pack_weight_multi(int n, const zp_pack_job* jobs, const long l
   ZP_CHECK_ARG(n >= 0 && n <= 65535 && total >= 0 && total < (1ll << 40) && (n == 0 || (jobs && prefix)),
                "zp_pack_weight_multi: bad args");
   if (n == 0 || total == 0) return ZP_OK;
-  hipLaunchKernelGGL(k_pack_multi, dim3(256, n), dim3(256), 0, (hipStream_t)stream, jobs);
+  hipLaunchKernelGGL(k_pack_multi, dim3(256, n), dim3(256), 0, (hipStream_t)stream, jobs, range_flag());
   ZP_LAUNCH_CHECK("zp_pack_weight_multi");
   return ZP_OK;
 }
@@ -1442,10 +1467,10 @@ extern "C" int zp_im2col_split(const float* x, int B, int H, int W, int ldx, int
   const long total = (long)B * OH * OW * (kpad / 8);
   if (dtype == ZP_F32X3)
     hipLaunchKernelGGL(k_im2col_split<3>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, x, B, H, W, ldx,
-                       C, k, s, p, OH, OW, kpad, (unsigned short*)y);
+                       C, k, s, p, OH, OW, kpad, (unsigned short*)y, nullptr);
   else
     hipLaunchKernelGGL(k_im2col_split<2>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, x, B, H, W, ldx,
-                       C, k, s, p, OH, OW, kpad, (unsigned short*)y);
+                       C, k, s, p, OH, OW, kpad, (unsigned short*)y, range_flag());
   ZP_LAUNCH_CHECK("zp_im2col_split");
   return ZP_OK;
 }

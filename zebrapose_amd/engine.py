@@ -708,6 +708,15 @@ class Engine:
 
         self._prepack(dev)
         st = L.stream_ptr()
+        if self.dt == L.ZP_F32H2:
+            # the range guard (include/zp.h zp_split_range_flag): registered before the first
+            # two-plane store; its reader (DeepLabV3.forward) clears it after an eager forward.  A
+            # captured forward clears it at its start, so that each replay starts clean
+            # (GraphedInference reads it after the replay; the weights were packed, and their
+            # range checked, by the eager warm-up)
+            flag = L.range_flag(dev)
+            if torch.cuda.is_current_stream_capturing():
+                flag.zero_()
         self.stage = "stem"
         if self.x3:  # the stem reads f32 (exact-f32 small-Cin kernel) and writes split output
             xin = Act(torch.empty((B, H, W, 8), dtype=torch.float32, device=dev))

@@ -17,6 +17,8 @@ from __future__ import annotations
 import numpy as np
 import torch
 
+from . import _lib as L
+
 
 def _engines(net):
     out = []
@@ -26,6 +28,11 @@ def _engines(net):
             out.append(e)
         out.extend(getattr(m, "_engines_split", {}).values())
     return out
+
+
+def _deeplabs(net):
+    """The modules of ``net`` that carry the fp32 eval engines' range guard (model.BinaryCodeNet.DeepLabV3)."""
+    return [m for m in net.modules() if hasattr(m, "h2_active")]
 
 
 def _state_tensors(net):
@@ -49,21 +56,45 @@ class GraphedInference:
         if dev.type != "cuda":
             raise ValueError("GraphedInference needs the network on a HIP device")
         self.net, self.decoder, self.bbox_size = net, decoder, int(bbox_size)
+        self.warmup, self.dev = warmup, dev
         self.x = torch.zeros((batch, 3, size, size), dtype=torch.float32, device=dev)
         self.bb = torch.zeros((batch, 4), dtype=torch.int32, device=dev)
         self.bb[:, 2:] = size  # any valid box for the warm-up; callers pass their own
+        self.range_fallbacks = 0
+        self._capture()
+
+    def _capture(self):
+        net, dev, warmup = self.net, self.dev, self.warmup
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.no_grad(), torch.cuda.stream(side):
             for _ in range(max(1, warmup)):  # fills the weight-pack / BN-fold caches outside the capture
                 self._step()
         torch.cuda.current_stream(dev).wait_stream(side)
+        # the two-plane split engine's range guard (after the eager warm-up, which checks itself and
+        # may already have switched a network to x3): the captured forward clears the device flag at
+        # its start (Engine._forward_main), _replay reads it after each replay
+        self._guarded = [m for m in _deeplabs(net) if m.h2_active() and m.range_check]
+        self._flag = L.range_flag(dev) if self._guarded else None
         self.graph = torch.cuda.CUDAGraph()
         # thread_local: under torch.distributed the RCCL watchdog thread may query events meanwhile
         with torch.no_grad(), torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
             self.out = self._step()
         self._tensors, self._engs = _state_tensors(net), _engines(net)
         self._stamp = _state_stamp(self._tensors, self._engs)
+
+    def _replay(self):
+        self.graph.replay()
+        if self._flag is not None and int(self._flag.item()):
+            # a value beyond fp16's range: the networks switch to the full-range x3 engine, and the
+            # step is captured again (the warm-up and capture leave the static inputs alone) and
+            # replayed
+            self._flag.zero_()
+            for m in self._guarded:
+                m.range_fallback()
+            self.range_fallbacks += 1
+            self._capture()
+            self.graph.replay()
 
     def _step(self):
         mask, code = self.net(self.x)
@@ -84,7 +115,7 @@ class GraphedInference:
         if bboxes is not None:
             self.bb.copy_(torch.as_tensor(np.asarray(bboxes), dtype=torch.int32).reshape(self.bb.shape),
                           non_blocking=False)
-        self.graph.replay()
+        self._replay()
         return self.out
 
 

@@ -23,6 +23,7 @@ inference only (configs[4]: R50 multi-object inference).  Set per instance (``ne
 from __future__ import annotations
 
 import os
+import warnings
 
 import torch
 import torch.nn as nn
@@ -221,6 +222,12 @@ class DeepLabV3(nn.Module):
         object.__setattr__(self, "_engines_split", {})
         env = os.environ.get("ZP_F32_SPLIT", "1")
         self.f32_split = False if env == "0" else (env if env in SPLIT_FORMS else True)
+        # range guard of the two-plane form (include/zp.h zp_split_range_flag): every "h2" eval
+        # forward reads the device flag once when it is done (one 4-byte readback); a forward that
+        # met a value beyond fp16's range is re-run on the full-range "x3" form, which this network
+        # then keeps (range_fallbacks counts the switches).  ZP_RANGE_CHECK=0 turns the readback off.
+        self.range_check = os.environ.get("ZP_RANGE_CHECK", "1") != "0"
+        self.range_fallbacks = 0
 
     def set_precision(self, precision):
         object.__setattr__(self, "_engine", Engine(self, _PREC[precision]))
@@ -239,6 +246,24 @@ class DeepLabV3(nn.Module):
             return eng
         return self._engine
 
+    def h2_active(self):
+        """True when the eval forward runs the two-plane split form (and so needs the range guard)."""
+        if self.training or self._engine.dtype != torch.float32:
+            return False
+        eng = self.eval_engine()
+        return eng.split == "h2"
+
+    def range_fallback(self):
+        """Switch the eval forward to the full-range three-plane form after a range-guard hit."""
+        warnings.warn("zebrapose_amd: an activation or weight of the fp32 eval forward exceeds fp16's range "
+                      "(|v| >= 65520); the two-plane split engine is replaced by the full-range x3 engine for "
+                      "this network", RuntimeWarning, stacklevel=3)
+        self.f32_split = "x3"
+        self.range_fallbacks += 1
+        # the two-plane packings may hold infinities: a later switch back to "h2" repacks (and
+        # re-checks) them
+        self._engines_split.pop("h2", None)
+
     @property
     def precision(self):
         return {torch.bfloat16: "bf16", torch.float16: "fp16"}.get(self._engine.dtype, "fp32")
@@ -254,6 +279,13 @@ class DeepLabV3(nn.Module):
             return _DeepLabFn.apply(self, x, *params)
         eng = self._engine if self.training else self.eval_engine()
         mask, code, _ = eng.forward(x, train=self.training)
+        if eng.split == "h2" and self.range_check and not torch.cuda.is_current_stream_capturing():
+            # (a captured forward is checked by its GraphedInference after each replay)
+            flag = L.range_flag(x.device)
+            if int(flag.item()):
+                flag.zero_()
+                self.range_fallback()
+                mask, code, _ = self.eval_engine().forward(x, train=False)
         return mask, code
 
 
