@@ -128,11 +128,26 @@ def _gpu_worker(rank, world, port, q, mode="buckets"):
             assert ts.buckets is None and isinstance(ts.net, torch.nn.parallel.DistributedDataParallel)
         else:
             assert ts.buckets is not None and ts.net is net
+        # when each parameter's gradient reached autograd (its AccumulateGrad / DDP hook): the share
+        # of the engine's reverse pass enqueued by then.  At world size 2 under torch's DDP the
+        # stage-by-stage chain (zebrapose_amd.staged) is taken automatically -- the path an unchanged
+        # train_v6.py:259 takes at world 8
+        eng = net.net._engine
+        seen = {}
+
+        def hook_for(n):
+            def hook(t):
+                seen.setdefault(n, getattr(eng, "bwd_progress", (0, 1)))
+            return hook
+        hooks = [p.register_post_accumulate_grad_hook(hook_for(n)) for n, p in net.named_parameters()]
         ts(x, gt, gm)
         torch.cuda.synchronize()
+        for h in hooks:
+            h.remove()
         avg = {n: params[n].grad.detach().double().cpu() for n in names}
         nb = len(ts.buckets.buckets) if ts.buckets is not None else None
-        q.put((rank, nb, {n: local[n].tolist() for n in names}, {n: avg[n].tolist() for n in names}, norm_local))
+        q.put((rank, nb, {n: local[n].tolist() for n in names}, {n: avg[n].tolist() for n in names}, norm_local,
+               {n: list(v) for n, v in seen.items()}))
     finally:
         if dist.is_initialized():
             dist.destroy_process_group()
@@ -142,7 +157,10 @@ def _gpu_worker(rank, world, port, q, mode="buckets"):
 @pytest.mark.parametrize("mode", ["buckets", "torch_ddp"])
 def test_grad_buckets_engine_two_ranks(gpu, mode):
     """Both data-parallel paths over the libzp network: GradBuckets (default) and torch's own
-    DistributedDataParallel(net) (ZP_TORCH_DDP=1, the wrapper train_v6.py:259 uses)."""
+    DistributedDataParallel(net) (ZP_TORCH_DDP=1, the wrapper train_v6.py:259 uses).  Under torch's
+    DDP the staged chain is automatic at world size 2 (no ZP_STAGED_BACKWARD): its hooks must fire
+    stage by stage -- the head's with under a quarter of the reverse pass enqueued, the stem's at the
+    end."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -166,3 +184,13 @@ def test_grad_buckets_engine_two_ranks(gpu, mode):
             got = torch.tensor(res[r][3][n])
             assert (got - want).abs().max().item() <= 1e-5 * scale, n
     assert res[0][4] > 0 and res[1][4] > 0
+    if mode == "torch_ddp":  # the automatic staged chain: head hooks early, the stem's at the end
+        for r in range(world):
+            hp = res[r][5]
+            assert len(hp) == 152
+            done, total = hp["net.aspp.conv_1x1_4.weight"]
+            assert done < total / 4, (r, done, total)
+            done, total = hp["net.resnet.layer5.2.conv2.weight"]
+            assert done < total / 2, (r, done, total)
+            done, total = hp["net.resnet.resnet.0.weight"]
+            assert done == total, (r, done, total)

@@ -27,6 +27,8 @@ def _free_port():
 def _worker(port, mode, q):
     os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
                       ZP_QUIET="1")
+    v3 = mode.endswith("_v3")
+    mode = mode[:-3] if v3 else mode
     if mode in ("torch_ddp", "torch_ddp_staged"):
         os.environ["ZP_TORCH_DDP"] = "1"
     if mode == "torch_ddp_staged":  # zebrapose_amd.staged (automatic at world size > 1)
@@ -39,15 +41,23 @@ def _worker(port, mode, q):
         from zebrapose_amd.model.BinaryCodeNet import BinaryCodeNet_Deeplab
         from zebrapose_amd.train import TrainStep
         torch.manual_seed(0)
-        net = BinaryCodeNet_Deeplab(34, 16, 2, concat=True, output_kernel_size=1, precision="bf16").to(dev)
+        if v3:  # the 3-head network (train_v5.py) through the same exchange paths; it runs 256 x 256 only
+            from zebrapose_amd.model.BinaryCodeNet_v3 import BinaryCodeNet_Deeplab_v3
+            net = BinaryCodeNet_Deeplab_v3(34, 16, 2, concat=True, output_kernel_size=1, precision="bf16").to(dev)
+            hw = 256
+        else:
+            net = BinaryCodeNet_Deeplab(34, 16, 2, concat=True, output_kernel_size=1, precision="bf16").to(dev)
+            hw = 64
         net.train()
         g = torch.Generator().manual_seed(5)
-        x = torch.randn(2, 3, 64, 64, generator=g).to(dev)
-        gt = (torch.rand(2, 16, 32, 32, generator=g) < 0.5).to(torch.uint8).to(dev)
-        gm = (torch.rand(2, 32, 32, generator=g) < 0.7).float().to(dev)
+        x = torch.randn(2, 3, hw, hw, generator=g).to(dev)
+        gt = (torch.rand(2, 16, hw // 2, hw // 2, generator=g) < 0.5).to(torch.uint8).to(dev)
+        gm = (torch.rand(2, hw // 2, hw // 2, generator=g) < 0.7).float().to(dev)
+        ge = (torch.rand(2, hw // 2, hw // 2, generator=g) < 0.8).float().to(dev) if v3 else None
+        extra = (ge,) if v3 else ()
         ts0 = TrainStep(net, ddp=False, learning_rate=0.0)
         ts0.optimizer.step = lambda: None
-        ts0(x, gt, gm)
+        ts0(x, gt, gm, *extra)
         local = {n: p.grad.detach().clone() for n, p in net.named_parameters()}
         # count the BN-buffer broadcasts (DDP broadcast_buffers=True: one per forward)
         calls = {"bcast": 0}
@@ -82,7 +92,7 @@ def _worker(port, mode, q):
             return hook
         hooks = [p.register_post_accumulate_grad_hook(hook_for(n)) for n, p in net.named_parameters()]
         bc0 = calls["bcast"]
-        ts(x, gt, gm)
+        ts(x, gt, gm, *extra)
         torch.cuda.synchronize()
         for h in hooks:
             h.remove()
@@ -110,7 +120,7 @@ def _worker(port, mode, q):
             dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["buckets", "torch_ddp", "torch_ddp_staged"])
+@pytest.mark.parametrize("mode", ["buckets", "torch_ddp", "torch_ddp_staged", "torch_ddp_staged_v3"])
 def test_rccl_world1_grad_exchange(gpu, mode):
     """torch_ddp_staged: torch's DistributedDataParallel(net) -- the unchanged train_v6.py:259 line --
     over the stage-by-stage autograd chain (zebrapose_amd.staged): the head's gradients must reach
@@ -127,10 +137,17 @@ def test_rccl_world1_grad_exchange(gpu, mode):
     assert p.exitcode == 0
     bad = {n: d for n, d in res["diffs"].items() if d}
     assert not bad, f"averaged gradients differ from the local ones: {bad}"
-    assert res["nparams"] == 152
+    v3 = mode.endswith("_v3")
+    nparams = res["nparams"]
+    assert nparams == (192 if v3 else 152), nparams
     hp = res["hook_progress"]
-    assert len(hp) == 152
-    if mode == "torch_ddp_staged":
+    assert len(hp) == nparams
+    if v3:  # ASPP_v3's head runs last in the forward, first in the reverse pass
+        done, total = hp["net.aspp_v3.conv_1x1_4.weight"]
+        assert done < total / 4, (done, total)
+        done, total = hp["net.resnet.resnet.0.weight"]
+        assert done == total
+    elif mode == "torch_ddp_staged":
         done, total = hp["net.aspp.conv_1x1_4.weight"]
         assert done < total / 4, (done, total)  # head gradients handed over early
         done, total = hp["net.resnet.layer5.2.conv2.weight"]

@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--strip", default="-1", help="zp_conv_tuning key 7 values to A/B (k_conv3s: 0 off, 1, 2)")
     ap.add_argument("--form", default="x3", choices=["x3", "h2"])
     ap.add_argument("--minblocks", default="256", help="zp_conv_tuning key 8 values to A/B (comma list)")
+    ap.add_argument("--wide", default="-1", help="zp_conv_tuning key 10 values to A/B (k_conv3w: 0 off, 1 on)")
     a = ap.parse_args()
     from zebrapose_amd import _lib as L
     from zebrapose_amd.engine import Engine, Unit, Act
@@ -60,18 +61,27 @@ def main():
         setups.append((name, eng, unit, Act(xs), y, fl))
     mbs = [int(m) for m in a.minblocks.split(",")]
     strips = [int(m) for m in a.strip.split(",")]
+    wides = [int(m) for m in a.wide.split(",")]
+    first = {}
     for r in range(a.rounds):
         for f0 in flags:
           for mb in mbs:
            for sm in strips:
-            L.lib.zp_conv_tuning(1, f0)
-            L.lib.zp_conv_tuning(8, mb)
-            L.lib.zp_conv_tuning(7, sm)
-            f = (f0, mb, sm)
-            for name, eng, unit, x, y, fl in setups:
+            for wd in wides:
+             L.lib.zp_conv_tuning(1, f0)
+             L.lib.zp_conv_tuning(8, mb)
+             L.lib.zp_conv_tuning(7, sm)
+             L.lib.zp_conv_tuning(10, wd)
+             f = (f0, mb, sm, wd)
+             for name, eng, unit, x, y, fl in setups:
                 for _ in range(2):
                     eng.unit_fwd(unit, x, y, None)
                 torch.cuda.synchronize()
+                if r == 0:  # outputs of every setting against the first one (bit-identical expected)
+                    ref = first.setdefault(name, y.buf._base.clone())
+                    nd = int((ref != y.buf._base).sum())
+                    if nd:
+                        print(f"{name} {f}: {nd} of {ref.numel()} stored halves differ from the first setting")
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(a.iters):
@@ -83,10 +93,11 @@ def main():
     L.lib.zp_conv_tuning(1, -1)
     L.lib.zp_conv_tuning(8, 256)
     L.lib.zp_conv_tuning(7, -1)
+    L.lib.zp_conv_tuning(10, -1)
     for (name, f), v in sorted(res.items()):
         fl = [s[5] for s in setups if s[0] == name][0]
         us = min(v)
-        print(f"{name:8s} flags {f[0]:6d} minblocks {f[1]:4d} strip {f[2]:2d}: {us:9.1f} us  {fl / us * 1e-6:7.1f} TFLOP/s  ({fl / us * 1e-6 / (2516.6 / (6 if a.form == 'x3' else 3)):.3f} of the {a.form} ceiling)")
+        print(f"{name:8s} flags {f[0]:6d} minblocks {f[1]:4d} strip {f[2]:2d} wide {f[3]:2d}: {us:9.1f} us  {fl / us * 1e-6:7.1f} TFLOP/s  ({fl / us * 1e-6 / (2516.6 / (6 if a.form == 'x3' else 3)):.3f} of the {a.form} ceiling)")
 
 
 if __name__ == "__main__":

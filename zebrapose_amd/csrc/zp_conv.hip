@@ -2771,7 +2771,7 @@ extern "C" int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* st
   *tc = conv_tc(*a);
   *tp = conv_tp(*a);
   *stages = *tc == 256 ? 2 : conv_stages(*a, *tc);
-  *variant = (a->dtype == ZP_F32X3 || a->dtype == ZP_F32H2) ? (conv3_nsplit(*a) == 1 && conv3_strip_ok(*a, *tc) ? 5 : 4) : quad_plan(*a, nullptr) ? 3 : *tc <= 128 && strip_eligible(*a, nullptr) ? ((conv_flags() & 64) ? 2 : 1) : 0;
+  *variant = (a->dtype == ZP_F32X3 || a->dtype == ZP_F32H2) ? (*tc == 256 ? 6 : conv3_nsplit(*a) == 1 && conv3_strip_ok(*a, *tc) ? 5 : 4) : quad_plan(*a, nullptr) ? 3 : *tc <= 128 && strip_eligible(*a, nullptr) ? ((conv_flags() & 64) ? 2 : 1) : 0;
   return ZP_OK;
 }
 
@@ -2826,6 +2826,8 @@ extern "C" int zp_conv_tuning(int key, int value) {
   if (key == 7) return conv3_strip_mode(value);
   if (key == 8) return conv3_min_blocks(value);
   if (key == 9) return conv3_splitk_mode(value);
+  if (key == 10) return conv3w_mode(value);
+  if (key == 11) return conv3w_min_blocks(value);
   if (key == 4) {
     const int old = g_wgrad2_rounds;
     g_wgrad2_rounds = value > 0 ? value : 1;

@@ -922,6 +922,7 @@ int conv3_min_blocks(int v) {
 // cout tile: 128 / 64 / 32 by Cout; a launch whose 128 x 256 grid would leave CUs idle (fewer
 // workgroups than zp_conv_tuning key 8) takes 64-channel tiles instead (twice the workgroups)
 int conv3_tc(const zp_conv_args& a) {
+  if (conv3w_ok(a)) return 256;  // k_conv3w
   const int tc = a.Cout > 64 ? 128 : (a.Cout > 32 ? 64 : 32);
   if (tc == 128 && g_conv3_min_blocks > 0) {
     const long blocks = (((long)a.N * a.GH * a.GW + 255) / 256) * ((a.Cout + 127) / 128) * a.nsub;
@@ -934,6 +935,7 @@ int conv3_tc(const zp_conv_args& a) {
 // (register-pipelined, 3-deep ring) for 64-channel tiles, 32 x 128 for the head.
 int conv3_tp(const zp_conv_args& a, int tc) {
   static const int sched = env_int("ZP_CONV3_SCHED");
+  if (tc == 256) return 256;  // k_conv3w
   if (tc == 128) return sched == 1 ? 128 : 256;  // 8-wave ping-pong 128 x 256, or the pipelined 128 x 128
   return 128;
 }
@@ -1012,6 +1014,10 @@ int conv3_nsplit(const zp_conv_args& a) {
 // kernel launches for one split form (NPL planes: 3 = ZP_F32X3, 2 = ZP_F32H2)
 template <int NPL>
 static void conv3_dispatch(const zp_conv_args& a, const conv_taps& tg, int tc, hipStream_t st, int fl) {
+  if (tc == 256) {  // 256 x 256 two-plane tile (zp_conv3w.hip)
+    conv3w_launch(a, tg, st, fl);
+    return;
+  }
   const int ns = a.stats ? conv3_nsplit(a) : 1;
   float* ws = (float*)a.stats;
   strip3_geo s3{};

@@ -1,0 +1,398 @@
+// k_conv3w: the wide-tile two-plane split-fp32 (ZP_F32H2) convolution for gfx950 -- 256 output
+// channels x 256 pixels per workgroup (k_conv3's tile is 128 x 256).
+//
+// Why: k_conv3<h2, 128 x 256> is bound by its staging, not by its MFMAs.
+// A K step (one tap x 32 channels) stages 48 KB (two planes of 128 weight rows + 256 pixel rows)
+// for 1536 MFMA cycles per SIMD, and the ablations (profiles/r03_conv3_ablation.txt) show the
+// kernel running as long without its MFMAs as with them.  Staged bytes per FLOP scale as
+// 1/TC + 1/TP: the 256 x 256 tile stages 64 KB per K step for 3072 MFMA cycles per SIMD, two
+// thirds of the bytes per FLOP, and halves the per-step fixed costs (barrier, first-read latency,
+// DMA issue) per FLOP.
+//
+// Numerics are k_conv3's (SplitF32<2>): every product a*b from hi*hi + (hi*lo' + lo'*hi) * 2^-11
+// on v_mfma_f32_16x16x32_f16; the two correction products of a 16 x 16 block go into a fresh
+// accumulator c2 (per block and K step), flushed into the block's accumulator by one f32 FMA
+// (acc = fma(c2, 2^-11, acc), exact scaling, round to nearest) -- the same per-step flush the
+// 8-wave k_conv3 does per half tile.  Results equal k_conv3's up to the f32 accumulation order of
+// the flushes (both flush per K step: they are bit-identical).
+//
+// Tile: 8 waves = 2 (cout halves of 128) x 4 (pixel quarters of 64); a wave owns 8 x 4 blocks of
+// 16 x 16 (128 accumulator registers).  Its 8 weight fragments are streamed through a 3-deep
+// register ring, the 4 pixel fragments of both planes are held for the step: ~210 VGPRs, no spill
+// at two waves per SIMD.
+// Staging: per plane, a 16-row x 32-element tile (1 KB) is ONE buffer_load ... lds of 64 lanes
+// (lane l: row l & 15, elements (l >> 4) * 8 ..), so the LDS image is in MFMA fragment order and
+// every fragment read is a lane-linear conflict-free ds_read_b128.  2-stage ring of 64 KB: the DMA
+// of step k + 1 is issued at the top of step k into the buffer step k - 1 read (every wave passed
+// the barrier that ended step k - 1) and has the whole step to land.
+// Epilogue: v_permlane16_swap pairs the lane groups of cout blocks (i, i + 1) so that a lane holds
+// 8 consecutive output channels of one pixel: 16 B stores per lane and plane (k_conv3 stores 8 B),
+// 16 B residual loads.
+#include "zp_conv_kern.h"
+#include "zp_conv3.h"
+
+namespace zp {
+
+__device__ __forceinline__ void wbarrier() {
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// ABL: diagnostic ablations (timing only, wrong results): 1 no DMA after the prologue, 2 no MFMA, 3 no
+// barrier in the main loop
+template <int ABL>
+__global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv_taps TG, const int flags) {
+  constexpr int NPL = 2;
+  constexpr int TC = 256, TP = 256;
+  constexpr int NTW = TC / 16, NT = (TC + TP) / 16;  // weight tiles / all tiles per plane (16 rows each)
+  constexpr int UNITS = NPL * NT;                    // 1 KB DMA units per stage
+  constexpr int WC = 8, WP = 4;                      // per wave: 8 cout blocks x 4 pixel blocks
+  constexpr int TPW = NT / 8;                        // tiles per wave: 2 weight + 2 activation
+  static_assert(2 * TPW == WC, "one DMA piece per cout block");
+  using MT = MfmaTraits<f16_t>;
+  __shared__ uint4 lds[2 * UNITS * 64];
+  static_assert(2 * UNITS * 1024 <= 160 * 1024, "LDS");
+  static_assert(((NPL - 1) * NT + NT - 1) * 1024 < 65536, "ds_read immediate range");
+  const int tb = (int)blockIdx.z;
+  const zp_conv_sub& S = A.sub[tb];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wid >> 2, wp = wid & 3;
+  const int GHW = A.GH * A.GW;
+  const int M = A.N * GHW;
+  int bx = blockIdx.x, by = blockIdx.y;
+  if (flags & 2) {  // XCD-aware order (k_conv): consecutive pixel tiles (shared halo rows) on one XCD
+    const int total = gridDim.x * gridDim.y;
+    const int bid = blockIdx.x + gridDim.x * blockIdx.y;
+    const int lin = (total & 7) ? bid : (bid & 7) * (total >> 3) + (bid >> 3);
+    bx = lin / gridDim.y;
+    by = lin - bx * gridDim.y;
+  }
+  const int p0 = bx * TP, c0 = by * TC;
+  const int CB = A.Cin / 32;
+  const int ny = TG.ny[tb], nx = TG.nx[tb], dty = TG.dty[tb], dtx = TG.dtx[tb];
+  const int nK = S.ntaps * CB;
+  const int lr = lane & 15, lk = (lane >> 4) * 8;
+  const unsigned psx_b = (unsigned)((long)A.N * A.IH * A.IW * A.ldx * 2);
+  const unsigned psw_b = (unsigned)((long)A.w_rows * A.k_pad * 2);
+
+  // DMA tiles of this wave: t = wid + 8 k (k 0, 1: weight tiles; 2, 3: activation tiles), both
+  // planes each; per-lane plane-0 byte offsets and the activation tiles' tap validity masks
+  unsigned ubase[TPW], uym[TPW], uxm[TPW];
+#pragma unroll
+  for (int k = 0; k < TPW; ++k) {
+    const int t = wid + 8 * k;
+    uym[k] = uxm[k] = 0u;
+    if (t < NTW) {
+      ubase[k] = (unsigned)(((long)(c0 + t * 16 + lr) * A.k_pad + lk) * 2);
+    } else {
+      const int m = p0 + (t - NTW) * 16 + lr;
+      const bool ok = m < M;
+      const int mm = ok ? m : 0;
+      const int n = mm / GHW, rr = mm - n * GHW;
+      const int gy = rr / A.GW, gx = rr - gy * A.GW;
+      const int y0 = gy * A.sy, x0 = gx * A.sx;
+      ubase[k] = (unsigned)(((((long)n * A.IH + y0) * A.IW + x0) * A.ldx + A.cx0 + lk) * 2);
+      unsigned ym = 0, xm = 0;
+      for (int q = 0; q < ny; ++q) ym |= (unsigned)((unsigned)(y0 + TG.ty0[tb] + q * dty) < (unsigned)A.IH) << q;
+      for (int q = 0; q < nx; ++q) xm |= (unsigned)((unsigned)(x0 + TG.tx0[tb] + q * dtx) < (unsigned)A.IW) << q;
+      uym[k] = ok ? ym : 0u;
+      uxm[k] = xm;
+    }
+  }
+#if defined(__HIP_DEVICE_COMPILE__)
+  const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)A.x, (short)0, (int)TG.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)S.w, (short)0, (int)TG.w_bytes[tb], 0x00020000);
+#endif
+  // scalar walk of the next step to issue: 32-channel chunk outer, taps inner (k_conv3's order: the
+  // taps of one chunk re-read nearly the same input rows from L2)
+  int w_cb = 0, w_tyi = 0, w_txi = 0;
+  const int step_x = dtx * A.ldx * 2, step_y = dty * A.IW * A.ldx * 2;
+  int act_off = ((TG.ty0[tb] * A.IW + TG.tx0[tb]) * A.ldx) * 2;
+  int w_koff = 0;
+  const int cin2 = A.Cin * 2;
+  // the DMA of one K step as 8 pieces (tile k = q / 2 of this wave, plane q % 2): prep() forms the
+  // per-lane offsets of the next step to issue and advances the walk; piece<q>() issues one piece
+  struct DmaStep {
+    unsigned voff[TPW];
+    int koff;
+  };
+  auto prep = [&](DmaStep& d) {
+#pragma unroll
+    for (int k = 0; k < TPW; ++k) {
+      const bool ok = (uym[k] >> w_tyi) & (uxm[k] >> w_txi) & 1u;
+      d.voff[k] = k < 2 ? ubase[k] : (ok ? ubase[k] + (unsigned)act_off : 0x80000000u);
+    }
+    d.koff = w_koff;
+    w_koff += cin2;
+    act_off += step_x;
+    if (++w_txi == nx) {
+      w_txi = 0;
+      act_off += step_y - nx * step_x;
+      if (++w_tyi == ny) {
+        w_tyi = 0;
+        ++w_cb;
+        act_off += 64 - ny * step_y;
+        w_koff = w_cb * 64;
+      }
+    }
+  };
+  auto piece = [&](auto q_c, int stage, const DmaStep& d) {
+    constexpr int q = decltype(q_c)::value, k = q / 2, pl = q % 2;
+    const int t = wid + 8 * k;
+#if defined(__HIP_DEVICE_COMPILE__)
+    auto* dst = (__attribute__((address_space(3))) void*)&lds[(stage * UNITS + pl * NT + t) * 64];
+    if constexpr (k < 2) __builtin_amdgcn_raw_ptr_buffer_load_lds(wrsrc, dst, 16, d.voff[k], pl * psw_b + d.koff, 0, 0);
+    else __builtin_amdgcn_raw_ptr_buffer_load_lds(xrsrc, dst, 16, d.voff[k], pl * psx_b, 0, 0);
+#else
+    (void)t; (void)stage; (void)d;
+#endif
+  };
+  auto issue = [&](int stage) {
+    DmaStep d;
+    prep(d);
+    static_for<2 * TPW>([&](auto q_c) { piece(q_c, stage, d); });
+  };
+
+  f32x4 acc[WC][WP];
+#pragma unroll
+  for (int i = 0; i < WC; ++i)
+#pragma unroll
+    for (int j = 0; j < WP; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // fragment reads: inline-asm ds_read_b128 with explicit lgkmcnt waits.  Plain LDS loads would
+  // make the compiler put an s_waitcnt vmcnt(0) in front of every fragment read issued after the
+  // LDS-DMA of the next step (it cannot tell the DMA's LDS destination from the buffer being read),
+  // i.e. wait for the next step's staging before computing this one.
+  const unsigned l0 = lds_addr(lds) + (unsigned)lane * 16u;
+  const unsigned abase0 = l0 + (unsigned)(wc * WC) * 1024u, bbase0 = l0 + (unsigned)(NTW + wp * WP) * 1024u;
+  const unsigned abase1 = abase0 + UNITS * 1024u, bbase1 = bbase0 + UNITS * 1024u;
+  // one K step on stage buffer s: the 4 pixel fragments of both planes held for the step, the 8
+  // weight fragments streamed 2 ahead; per block: c2 = hi*lo' + lo'*hi, acc += hi*hi, and the flush
+  // acc = fma(c2, 2^-11, acc) one cout block later (its MFMAs have finished by then)
+  constexpr bool abl_dma = ABL == 1, abl_mfma = ABL == 2, abl_bar = ABL == 3;
+  auto step = [&](auto s_c, const bool more) {
+    constexpr int s = decltype(s_c)::value;
+    // the next step's DMA (into the other buffer: every wave has passed the barrier that ended the
+    // step which read it): one piece per cout block, after that block's correction MFMAs, so that
+    // the issue cost (~60 cycles per piece beside MFMAs) is spread over the step
+    DmaStep dn;
+    if (more) prep(dn);
+    const unsigned ab = s ? abase1 : abase0, bb = s ? bbase1 : bbase0;
+    uint4 bf[NPL][WP];
+    uint4 af[3][NPL];  // weight fragments: a 3-slot ring
+    static_for<NPL>([&](auto p_c) {
+      constexpr int p = decltype(p_c)::value;
+      static_for<WP>([&](auto j_c) {
+        constexpr int j = decltype(j_c)::value;
+        bf[p][j] = ds_read16<(p * NT + j) * 1024>(bb);
+      });
+    });
+    static_for<2>([&](auto q_c) {
+      constexpr int q = decltype(q_c)::value;
+      static_for<NPL>([&](auto p_c) {
+        constexpr int p = decltype(p_c)::value;
+        af[q][p] = ds_read16<(p * NT + q) * 1024>(ab);
+      });
+    });
+    f32x4 c2p[WP];  // the previous cout block's correction sums (flushed one block later)
+    static_for<WC>([&](auto i_c) {
+      constexpr int i = decltype(i_c)::value;
+      if constexpr (i + 2 < WC) {
+        static_for<NPL>([&](auto p_c) {
+          constexpr int p = decltype(p_c)::value;
+          af[(i + 2) % 3][p] = ds_read16<(p * NT + i + 2) * 1024>(ab);
+        });
+      }
+      // reads issued after cout block i's: blocks i + 1 and i + 2 (two planes each)
+      constexpr int after = (i + 1 < WC ? NPL : 0) + (i + 2 < WC ? NPL : 0);
+      asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(after) : "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      f32x4 c2[WP];
+#pragma unroll
+      for (int j = 0; j < WP; ++j) {
+        c2[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        if constexpr (abl_mfma) {
+          // (the fragment reads are asm volatile: they still issue)
+        } else {
+          MT::mma(c2[j], af[i % 3][0], bf[1][j]);  // k_conv3's term order (Terms<2>): hi*lo', then lo'*hi
+          MT::mma(c2[j], af[i % 3][1], bf[0][j]);
+        }
+      }
+      if (more && !abl_dma) piece(std::integral_constant<int, i>{}, s ^ 1, dn);
+#pragma unroll
+      for (int j = 0; j < WP; ++j) {
+        if constexpr (!abl_mfma) MT::mma(acc[i][j], af[i % 3][0], bf[0][j]);
+      }
+      if constexpr (i > 0) {
+#pragma unroll
+        for (int j = 0; j < WP; ++j) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i - 1][j][r] = __builtin_fmaf(c2p[j][r], SplitF32<2>::CS, acc[i - 1][j][r]);
+          asm volatile("" : "+v"(acc[i - 1][j]));  // pinned here: sunk into the next step, every
+        }                                            // block's c2 would stay live (333 spilled VGPRs)
+      }
+#pragma unroll
+      for (int j = 0; j < WP; ++j) c2p[j] = c2[j];
+      __builtin_amdgcn_sched_barrier(0);
+    });
+#pragma unroll
+    for (int j = 0; j < WP; ++j) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[WC - 1][j][r] = __builtin_fmaf(c2p[j][r], SplitF32<2>::CS, acc[WC - 1][j][r]);
+    }
+  };
+
+  // prologue: step 0's DMA into buffer 0
+  issue(0);
+  vm_wait<0>();
+  wbarrier();
+  __builtin_amdgcn_sched_barrier(0);
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  if (flags & 65536) {  // static priority for the second-dispatched half (MI355X_MICROARCH.md item 4)
+    if (wid >= 4) __builtin_amdgcn_s_setprio(1);
+  }
+  for (int ks = 0; ks < nK; ks += 2) {
+    // step ks on buffer 0, issuing the DMA of step ks + 1 into buffer 1
+    step(I0{}, ks + 1 < nK);
+    vm_wait<0>();
+    if constexpr (!abl_bar) wbarrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (ks + 1 >= nK) break;
+    step(I1{}, ks + 2 < nK);
+    vm_wait<0>();
+    if constexpr (!abl_bar) wbarrier();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+
+  // ---------------- epilogue: paired lane groups, 16 B per lane and plane ----------------
+  using SP = SplitF32<NPL>;
+  bool bad = false;
+  const int g = lane >> 4;
+  const long psy = (long)A.N * S.OH * S.OW * S.ldy;
+  const long psr = (long)A.N * S.OH * S.OW * A.ldr;
+  int pn[WP], poy[WP], pox[WP];
+  bool pok[WP];
+#pragma unroll
+  for (int j = 0; j < WP; ++j) {
+    const int p = p0 + wp * 16 * WP + j * 16 + lr;
+    pok[j] = p < M;
+    const int pp = pok[j] ? p : 0;
+    const int n = pp / GHW, rr = pp - n * GHW;
+    const int gy = rr / A.GW, gx = rr - gy * A.GW;
+    pn[j] = n;
+    poy[j] = gy * S.oys + S.oyo;
+    pox[j] = gx * S.oxs + S.oxo;
+  }
+#pragma unroll
+  for (int i = 0; i < WC; i += 2) {
+    const int cs = c0 + wc * 16 * WC + (i + (g & 1)) * 16 + (g >> 1) * 8;  // this lane's 8 channels
+    const bool cok = cs < A.Cout;
+    float sc[8], sh[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      sc[r] = 1.f;
+      sh[r] = 0.f;
+    }
+    if (cok && S.scale) {
+      const float4 s0 = *(const float4*)(S.scale + cs), s1 = *(const float4*)(S.scale + cs + 4);
+      sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w;
+      sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
+    }
+    if (cok && S.shift) {
+      const float4 s0 = *(const float4*)(S.shift + cs), s1 = *(const float4*)(S.shift + cs + 4);
+      sh[0] = s0.x; sh[1] = s0.y; sh[2] = s0.z; sh[3] = s0.w;
+      sh[4] = s1.x; sh[5] = s1.y; sh[6] = s1.z; sh[7] = s1.w;
+    }
+#pragma unroll
+    for (int j = 0; j < WP; ++j) {
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {  // all lanes active here (cross-lane op)
+        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][j][r]), __float_as_uint(acc[i + 1][j][r]),
+                                                         false, false);
+        v[r] = __uint_as_float(sw[0]);
+        v[r + 4] = __uint_as_float(sw[1]);
+      }
+      if (!pok[j] || !cok) continue;
+      const size_t pix = ((size_t)pn[j] * S.OH + poy[j]) * S.OW + pox[j];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) v[r] = v[r] * sc[r] + sh[r];
+      if (A.res) {
+        const unsigned short* R = (const unsigned short*)A.res + pix * A.ldr + A.cr0 + cs;
+        uint4 rq[NPL];
+#pragma unroll
+        for (int p = 0; p < NPL; ++p) rq[p] = *(const uint4*)(R + p * psr);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          unsigned short q[NPL];
+#pragma unroll
+          for (int p = 0; p < NPL; ++p) {
+            const uint32_t w4[4] = {rq[p].x, rq[p].y, rq[p].z, rq[p].w};
+            q[p] = (unsigned short)(w4[r >> 1] >> ((r & 1) * 16));
+          }
+          v[r] += SP::join(q);
+        }
+      }
+      if (A.relu) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) v[r] = fmaxf(v[r], 0.f);
+      }
+      uint32_t o[NPL][4];
+#pragma unroll
+      for (int r = 0; r < 8; r += 2) {
+        unsigned short q0[NPL], q1[NPL];
+        SP::split(v[r], q0);
+        SP::split(v[r + 1], q1);
+        bad |= h2_overflow(v[r]) || h2_overflow(v[r + 1]);
+#pragma unroll
+        for (int p = 0; p < NPL; ++p) o[p][r >> 1] = (uint32_t)q0[p] | ((uint32_t)q1[p] << 16);
+      }
+      if ((flags & 16384) && v[0] != 1.f) continue;  // diagnostic: no stores (unless a value is exactly 1)
+      unsigned short* Y = (unsigned short*)S.y + pix * S.ldy + S.cy0 + cs;
+#pragma unroll
+      for (int p = 0; p < NPL; ++p) *(uint4*)(Y + p * psy) = make_uint4(o[p][0], o[p][1], o[p][2], o[p][3]);
+    }
+  }
+  raise_range_flag(TG.rflag, bad);
+}
+
+// eligibility of the wide tile: two planes, NHWC output with 16-byte-aligned channel slices, Cout a
+// multiple of 256 and a grid of at least g_conv3w_min workgroups (fewer: k_conv3's 128 x 256 tile
+// keeps more CUs busy)
+static int g_conv3w = -1;       // zp_conv_tuning key 10 (-1: ZP_CONV3W or the default 1)
+static int g_conv3w_min = 256;  // zp_conv_tuning key 11
+
+int conv3w_mode(int v) {
+  const int old = g_conv3w;
+  g_conv3w = v;
+  return old;
+}
+int conv3w_min_blocks(int v) {
+  const int old = g_conv3w_min;
+  g_conv3w_min = v;
+  return old;
+}
+
+bool conv3w_ok(const zp_conv_args& a) {
+  static const int env = getenv("ZP_CONV3W") ? atoi(getenv("ZP_CONV3W")) : 1;
+  const int en = g_conv3w >= 0 ? g_conv3w : env;
+  if (!en || a.dtype != ZP_F32H2 || a.out_mode != ZP_OUT_NHWC || a.Cout % 256 != 0 || a.Cin % 32 != 0) return false;
+  if (a.w_rows % 256 != 0) return false;
+  for (int s = 0; s < a.nsub; ++s)
+    if (a.sub[s].ldy % 8 != 0 || a.sub[s].cy0 % 8 != 0) return false;
+  if (a.res && (a.ldr % 8 != 0 || a.cr0 % 8 != 0)) return false;
+  const long blocks = (((long)a.N * a.GH * a.GW + 255) / 256) * (a.Cout / 256) * a.nsub;
+  return blocks >= g_conv3w_min;
+}
+
+void conv3w_launch(const zp_conv_args& a, const conv_taps& tg, hipStream_t st, int fl) {
+  const dim3 grid((unsigned)(((long)a.N * a.GH * a.GW + 255) / 256), (unsigned)(a.Cout / 256), (unsigned)a.nsub);
+  if (fl & 4096) hipLaunchKernelGGL(k_conv3w<1>, grid, dim3(512), 0, st, a, tg, fl);  // diagnostic: no DMA
+  else if (fl & 8192) hipLaunchKernelGGL(k_conv3w<2>, grid, dim3(512), 0, st, a, tg, fl);  // diagnostic: no MFMA
+  else if (fl & 131072) hipLaunchKernelGGL(k_conv3w<3>, grid, dim3(512), 0, st, a, tg, fl);  // diagnostic: no barrier
+  else hipLaunchKernelGGL(k_conv3w<0>, grid, dim3(512), 0, st, a, tg, fl);
+}
+
+}  // namespace zp

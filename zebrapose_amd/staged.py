@@ -61,11 +61,15 @@ def stage_params(module):
 
 
 def enabled(module):
+    """Staged backward: under torch DDP (a process group of world size > 1) or ZP_STAGED_BACKWARD=1 --
+    never with a GradBuckets attached, whose reducer is fed by the single-node path (grads_sink /
+    finish_grads); ZP_STAGED_BACKWARD=0 turns it off."""
+    if getattr(module, "_grad_buckets", None) is not None:
+        return False
     env = os.environ.get("ZP_STAGED_BACKWARD")
     if env is not None:
         return env == "1"
-    return (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
-            and getattr(module, "_grad_buckets", None) is None)
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
 
 
 class _State:
@@ -79,17 +83,20 @@ class _State:
         if self.gen is None:
             self.gen = self.engine.backward_iter(self.tape, *head_grads, grads=self.grads)
         need = [p for p in params]
-        while any(p not in self.grads for p in need):
-            next(self.gen)
+        while self.gen is not None and any(p not in self.grads for p in need):
+            try:
+                next(self.gen)
+            except StopIteration:  # the reverse pass is done: a parameter it never reached gets None
+                self.gen = None   # (as the single node's by_ptr.get does)
         self.left -= 1
         if self.left == 0:  # the last stage: finish the pass (joins the side stream)
-            for _ in self.gen:
+            for _ in self.gen or ():
                 pass
             self.gen = None
             self.tape = None
         else:
             self.engine.side_join_current()
-        return [self.grads[p] for p in need]
+        return [self.grads.get(p) for p in need]
 
 
 class _StageFn(torch.autograd.Function):
