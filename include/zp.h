@@ -162,6 +162,28 @@ long long zp_conv2d_split_ws(const zp_conv_args* a);
  * (default 1, 0 off).  Returns the previous value, -1 for an unknown key. */
 int zp_conv_tuning(int key, int value);
 
+/* Fused 1x1 head (ZP_F32H2 only; the reference's conv_1x1_4 over torch.cat([x, x_128]) and the
+ * mask / code split, model/aspp.py:112 + model/BinaryCodeNet.py:172).  The conv of *a (one sub, NHWC,
+ * BN scale / shift, bias, residual and ReLU applied as by zp_conv2d) is NOT stored: each output
+ * pixel's Cout channels, followed by the C2 channels of x2 at the same pixel (ZP_F32H2 NHWC,
+ * [N][OH][OW][ldx2], channels cx20..), feed a 1x1 conv with hcout <= 32 outputs: weights w packed
+ * by zp_pack_weight(dtype ZP_F32H2, rows_pad 32, k = channel, k_pad >= Cout + C2), bias (f32 [hcout]
+ * or NULL).  Output f32 NCHW: channel 0 -> mask [N][1][OH][OW], channels 1.. -> code
+ * [N][hcout-1][OH][OW].  zp_conv2d_head_ok: 1 if *a has a geometry the fused kernel takes (the
+ * 256 x 256 split tile with Cout == 256; e.g. not at bs = 1, where the unfused path runs). */
+typedef struct zp_head_args {
+  const void* w;
+  int k_pad;
+  const float* bias;
+  int cout;
+  const void* x2;
+  int ldx2, cx20, C2;
+  float* mask;
+  float* code;
+} zp_head_args;
+int zp_conv2d_head_ok(const zp_conv_args* a);
+int zp_conv2d_head(const zp_conv_args* a, const zp_head_args* h, void* stream);
+
 /* Pack an f32 weight tensor src[d0][d1][kh][kw] into dst[rows_pad][k_pad] (dtype), taps
  * (ky[t], kx[t]), t < ntaps:
  *   transposed == 0: dst[r][t*cstride + c] = src[r][c][ky[t]][kx[t]]   (conv forward: OIHW)

@@ -1,6 +1,7 @@
 """Parity at the configuration the bench reports (BASELINE.json configs[1]: ResNet34 + DeepLabv3,
-bs=32, 256x256 crops), in bf16 (the benched precision) and fp32, through the drop-in module and
-libzp.so.  Reference anchor: model/BinaryCodeNet.py:161-174, aspp.py:83-114, test.py:248.
+bs=32, 256x256 crops), in fp32 (the benched headline: the two-plane split engine, with up2's last
+conv and the head fused into one launch) and bf16 (the labelled throughput leg), through the
+drop-in module and libzp.so.  Reference anchor: model/BinaryCodeNet.py:161-174, aspp.py:83-114, test.py:248.
 
 Weights: the synthetic checkpoint with BN calibrated on 256x256 crops by the real reference
 (tests/golden/r34_bn_buffers256.npz, oracle/capture_fixtures.py capture_fwd256): |logit| <= 6 on the
@@ -226,10 +227,11 @@ def test_bf16_bench_geometry_end_to_end(setup):
 
 @pytest.mark.parametrize("split", ["x3", "h2", False], ids=["split_x3", "split_h2", "f32_mfma"])
 def test_fp32_bench_geometry(setup, split):
-    """fp32 mode at bs=32 -- the benched headline: the split-fp32 eval engine (ZP_F32X3, the
-    default), and the exact-f32-MFMA engine: logits of crops 0, 13, 31 within the north-star 1e-3 of
-    the fp32 oracle, mask / code bits identical outside the band; every op replayed teacher-forced
-    to 1e-5 rel from the device's own stored (joined) inputs."""
+    """fp32 mode at bs=32: the split-fp32 eval engines (two fp16 planes, ZP_F32H2, the default; three
+    bf16 planes, ZP_F32X3) and the exact-f32-MFMA engine: logits of crops 0, 13, 31 within the
+    north-star 1e-3 of the fp32 oracle, mask / code bits identical outside the band; every op replayed
+    teacher-forced to 1e-5 rel from the device's own stored (joined) inputs (the trace keeps the head
+    a separate op: test_fp32_bench_geometry_fused_head covers the fused launch)."""
     from oracle import ref_cpu
     net, sd, x = setup
     net.set_precision("fp32")
@@ -281,6 +283,74 @@ def test_fp32_matches_reference_fixture_256(golden, split):
         m, c = net(torch.from_numpy(f["x"]).cuda())
     for got, ref in ((m.cpu().numpy(), f["mask"]), (c.cpu().numpy(), f["code"])):
         print(f"fwd256 fixture fp32 max |d| {np.abs(got - ref).max():.3g}")
+        np.testing.assert_allclose(got, ref, atol=1e-3, rtol=0)
+        amb = np.abs(ref) <= 1e-3
+        assert int((((got > THR) != (ref > THR)) & ~amb).sum()) == 0
+
+
+def test_fp32_bench_geometry_fused_head(setup):
+    """The benched fp32 forward as benched: two planes, up2's last 3x3 conv and the 1x1 head in one
+    launch (zp_conv2d_head: the conv's output is never stored; the head reads x_128 itself).  Logits of
+    the sampled crops within the north-star 1e-3 of the fp32 oracle, and within 2e-4 of the unfused
+    two-plane forward (the fused head multiplies the f32 conv output, the unfused one its stored
+    22-bit form: both are f32-accurate)."""
+    from oracle import ref_cpu
+    net, sd, x = setup
+    net.set_precision("fp32")
+    net.net.f32_split = "h2"
+    net.cuda().eval()
+    eng = net.net.eval_engine()
+    assert eng.head_fusable(x.shape[0], x.shape[2] // 2, x.shape[3] // 2)
+    eng.stage_log = []
+    with torch.no_grad():
+        m, c = net(x.cuda())
+    log, eng.stage_log = eng.stage_log, None
+    assert any(k.startswith("k_conv3w_head") for _, k, *_ in log), [k for _, k, *_ in log]
+    assert not any(st == "head" for st, *_ in log)  # no separate head launch
+    eng.fuse_head = False
+    with torch.no_grad():
+        mu, cu = net(x.cuda())
+    eng.fuse_head = True
+    for a, b in ((m, mu), (c, cu)):
+        d = float((a - b).abs().max())
+        print(f"fused vs unfused head: max |d| {d:.3g} (|logit| max {float(b.abs().max()):.3g})")
+        assert d <= 2e-4
+    xs = x[list(SAMPLE)]
+    with torch.no_grad():
+        fm, fc = ref_cpu.forward(sd, xs, 34)
+    for got, ref in ((m.cpu()[list(SAMPLE)].numpy(), fm.numpy()), (c.cpu()[list(SAMPLE)].numpy(), fc.numpy())):
+        print(f"fused head bs=32 fp32 max |d| vs CPU f32 oracle {float(np.abs(got - ref).max()):.3g}")
+        np.testing.assert_allclose(got, ref, atol=1e-3, rtol=0)
+        amb = np.abs(ref) <= 1e-3
+        assert int((((got > THR) != (ref > THR)) & ~amb).sum()) == 0
+    net.net.f32_split = True
+    net.set_precision("bf16")
+
+
+def test_fused_head_matches_reference_fixture_256(golden):
+    """The fused up2-conv + head launch at the reference's own 256x256 fixture (B=2: 128 workgroups,
+    below the wide tile's default minimum -- zp_conv_tuning key 11 lowered for the test)."""
+    from oracle import ref_cpu
+    from zebrapose_amd import _lib as L
+    from zebrapose_amd.model.BinaryCodeNet import BinaryCodeNet_Deeplab
+    f = golden("r34_fwd256.npz")
+    net = BinaryCodeNet_Deeplab(34, 16, 2, concat=True, output_kernel_size=1, precision="fp32")
+    net.net.f32_split = "h2"
+    net.load_state_dict(ref_cpu.synthetic_state(34, 16, 0, dict(golden("r34_bn_buffers256.npz"))))
+    net = net.cuda().eval()
+    old = L.lib.zp_conv_tuning(11, 1)
+    try:
+        eng = net.net.eval_engine()
+        assert eng.head_fusable(2, 128, 128)
+        eng.stage_log = []
+        with torch.no_grad():
+            m, c = net(torch.from_numpy(f["x"]).cuda())
+        assert any(k.startswith("k_conv3w_head") for _, k, *_ in eng.stage_log)
+        eng.stage_log = None
+    finally:
+        L.lib.zp_conv_tuning(11, old)
+    for got, ref in ((m.cpu().numpy(), f["mask"]), (c.cpu().numpy(), f["code"])):
+        print(f"fwd256 fixture, fused head: max |d| {np.abs(got - ref).max():.3g}")
         np.testing.assert_allclose(got, ref, atol=1e-3, rtol=0)
         amb = np.abs(ref) <= 1e-3
         assert int((((got > THR) != (ref > THR)) & ~amb).sum()) == 0

@@ -6,7 +6,7 @@ Tolerances:
              |ref logit| > 1e-3 (the ambiguous band is counted, must be tiny).
   bf16 mode  the synthetic random-weight model is ill-conditioned (oracle: rounding only the INPUT
              to bf16 moves the logits by 4% rel-L2), so bf16 is checked in norm against the fp32
-             reference: rel-L2 <= 0.25 (observed 0.16) and >= 90% of the bits outside |ref| < 0.25
+             reference: rel-L2 <= 0.20 (observed 0.16) and >= 99% of the bits outside |ref| < 0.25
              identical.  Per-kernel bf16 accuracy is checked tightly in test_gpu_units.py.
 """
 import numpy as np

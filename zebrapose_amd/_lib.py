@@ -55,6 +55,11 @@ class WgradArgs(C.Structure):
                 ("nsub", i32), ("sub", WgradSub * MAX_SUB), ("dw", vp), ("accumulate", i32)]
 
 
+class HeadArgs(C.Structure):
+    _fields_ = [("w", vp), ("k_pad", i32), ("bias", vp), ("cout", i32), ("x2", vp), ("ldx2", i32), ("cx20", i32),
+                ("C2", i32), ("mask", vp), ("code", vp)]
+
+
 class PackJob(C.Structure):
     _fields_ = [("src", vp), ("dst", vp), ("d0", i32), ("d1", i32), ("kh", i32), ("kw", i32),
                 ("transposed", i32), ("ntaps", i32), ("cstride", i32), ("rows_pad", i32), ("k_pad", i32),
@@ -117,6 +122,8 @@ _SIGS = {
     "zp_adam_multi": (i32, [i32, vp, vp, vp, vp, vp, f64, f64, f64, f64, i64, vp]),
     "zp_adam_multi_dev": (i32, [i32, vp, vp, vp, vp, vp, f64, f64, f64, f64, vp, vp]),
     "zp_split_range_flag": (i32, [vp]),
+    "zp_conv2d_head_ok": (i32, [C.POINTER(ConvArgs)]),
+    "zp_conv2d_head": (i32, [C.POINTER(ConvArgs), C.POINTER(HeadArgs), vp]),
 }
 
 

@@ -2765,6 +2765,17 @@ extern "C" int zp_conv2d_stat_parts(const zp_conv_args* a) {
   return (conv_tp(*a) / 64) * zp_conv2d_grid(a) * a->nsub;
 }
 
+extern "C" int zp_conv2d_head_ok(const zp_conv_args* a) {
+  return a && a->dtype == ZP_F32H2 && a->nsub == 1 && a->Cout == 256 && a->out_mode == ZP_OUT_NHWC &&
+         conv3_tc(*a) == 256;
+}
+
+extern "C" int zp_conv2d_head(const zp_conv_args* a, const zp_head_args* h, void* stream) {
+  ZP_CHECK_ARG(a && h, "zp_conv2d_head: null args");
+  ZP_CHECK_ARG(zp_conv2d_head_ok(a), "zp_conv2d_head: not a fused-head geometry (zp_conv2d_head_ok)");
+  return conv3_launch(*a, (hipStream_t)stream, conv_flags(), h);
+}
+
 /* launch configuration zp_conv2d picks for these args (for kernel labels in reports) */
 extern "C" int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* stages, int* variant) {
   ZP_CHECK_ARG(a && tc && tp && stages && variant, "zp_conv2d_config: null args");

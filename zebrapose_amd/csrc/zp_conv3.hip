@@ -1052,7 +1052,7 @@ static void conv3_dispatch(const zp_conv_args& a, const conv_taps& tg, int tc, h
   }
 }
 
-int conv3_launch(const zp_conv_args& a, hipStream_t st, int fl) {
+int conv3_launch(const zp_conv_args& a, hipStream_t st, int fl, const zp_head_args* head) {
   const int npl = a.dtype == ZP_F32H2 ? 2 : 3;
   ZP_CHECK_ARG(a.Cin > 0 && a.Cin % 32 == 0, "zp_conv2d: split fp32 needs Cin %% 32 == 0 (got %d; the stem runs in f32 "
                "with out_mode ZP_OUT_NHWC_X3 / _H2)", a.Cin);
@@ -1100,6 +1100,19 @@ int conv3_launch(const zp_conv_args& a, hipStream_t st, int fl) {
     for (int t = 0; grid && t < S.ntaps; ++t)
       grid = S.ty[t] == tg.ty0[s] + (t / nx) * tg.dty[s] && S.tx[t] == tg.tx0[s] + (t % nx) * tg.dtx[s];
     ZP_CHECK_ARG(grid, "zp_conv2d: sub %d taps must form a (row x column) grid of at most 32 x 32, rows outer", s);
+  }
+  if (head) {
+    const zp_head_args& h = *head;
+    ZP_CHECK_ARG(tc == 256 && a.Cout == 256 && a.nsub == 1 && npl == 2,
+                 "zp_conv2d_head: not a fused-head geometry (zp_conv2d_head_ok)");
+    ZP_CHECK_ARG(h.w && h.mask && (h.code || h.cout == 1) && h.cout >= 1 && h.cout <= 32, "zp_conv2d_head: bad head");
+    ZP_CHECK_ARG(h.C2 >= 0 && h.C2 % 32 == 0 && h.k_pad % 8 == 0 && h.k_pad >= a.Cout + h.C2,
+                 "zp_conv2d_head: C2 %d / k_pad %d", h.C2, h.k_pad);
+    ZP_CHECK_ARG(h.C2 == 0 || (h.x2 && h.ldx2 % 8 == 0 && h.cx20 % 8 == 0 && h.ldx2 >= h.cx20 + h.C2),
+                 "zp_conv2d_head: x2 layout");
+    conv3w_head_launch(a, tg, h, st, fl);
+    ZP_LAUNCH_CHECK("zp_conv2d_head");
+    return ZP_OK;
   }
   if (npl == 2) conv3_dispatch<2>(a, tg, tc, st, fl);
   else conv3_dispatch<3>(a, tg, tc, st, fl);

@@ -40,8 +40,13 @@ __device__ __forceinline__ void wbarrier() {
 
 // ABL: diagnostic ablations (timing only, wrong results): 1 no DMA after the prologue, 2 no MFMA, 3 no
 // barrier in the main loop
-template <int ABL>
-__global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv_taps TG, const int flags) {
+// DM: the next step's 8 DMA pieces are issued over the first DM cout blocks of a step (8 / DM per
+// block, after its correction MFMAs)
+// HEAD: the fused 1x1 head (zp_conv2d_head): the conv output feeds the head's MFMAs instead of
+// being stored
+template <int ABL, int DM, bool HEAD>
+__global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv_taps TG, const int flags,
+                                                const zp_head_args H) {
   constexpr int NPL = 2;
   constexpr int TC = 256, TP = 256;
   constexpr int NTW = TC / 16, NT = (TC + TP) / 16;  // weight tiles / all tiles per plane (16 rows each)
@@ -219,7 +224,10 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
           MT::mma(c2[j], af[i % 3][1], bf[0][j]);
         }
       }
-      if (more && !abl_dma) piece(std::integral_constant<int, i>{}, s ^ 1, dn);
+      if constexpr (i < DM) {
+        if (more && !abl_dma)
+          static_for<8 / DM>([&](auto q_c) { piece(std::integral_constant<int, i * (8 / DM) + decltype(q_c)::value>{}, s ^ 1, dn); });
+      }
 #pragma unroll
       for (int j = 0; j < WP; ++j) {
         if constexpr (!abl_mfma) MT::mma(acc[i][j], af[i % 3][0], bf[0][j]);
@@ -272,39 +280,86 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
   const int g = lane >> 4;
   const long psy = (long)A.N * S.OH * S.OW * S.ldy;
   const long psr = (long)A.N * S.OH * S.OW * A.ldr;
-  int pn[WP], poy[WP], pox[WP];
-  bool pok[WP];
-#pragma unroll
-  for (int j = 0; j < WP; ++j) {
+  // output pixel of the lane in pixel block j: image, row, column, in range (the HEAD variant
+  // recomputes it per use -- register pressure -- the plain epilogue keeps the four)
+  struct PixInfo {
+    int n, oy, ox;
+    bool ok;
+  };
+  auto pixinfo = [&](int j) {
     const int p = p0 + wp * 16 * WP + j * 16 + lr;
-    pok[j] = p < M;
-    const int pp = pok[j] ? p : 0;
+    PixInfo q;
+    q.ok = p < M;
+    const int pp = q.ok ? p : 0;
     const int n = pp / GHW, rr = pp - n * GHW;
     const int gy = rr / A.GW, gx = rr - gy * A.GW;
-    pn[j] = n;
-    poy[j] = gy * S.oys + S.oyo;
-    pox[j] = gx * S.oxs + S.oxo;
+    q.n = n;
+    q.oy = gy * S.oys + S.oyo;
+    q.ox = gx * S.oxs + S.oxo;
+    return q;
+  };
+  PixInfo pi[WP];
+  if constexpr (!HEAD) {
+#pragma unroll
+    for (int j = 0; j < WP; ++j) pi[j] = pixinfo(j);
   }
+  // HEAD: the 1x1 head's sums (rows hb * 16 + 4 g + q, pixel block j) over this wave's channels
+  f32x4 hacc[2][WP];
+  const long hps = (long)32 * H.k_pad;  // head weight plane stride (elements; rows padded to 32)
+  const unsigned short* HW = (const unsigned short*)H.w;
+  if constexpr (HEAD) {
+#pragma unroll
+    for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+      for (int j = 0; j < WP; ++j) hacc[hb][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+  // one 32-channel K slice of the head: weight fragments wf[hb][plane] (k slot g of lane group g),
+  // activation fragment planes (xh, xl) of pixel block j
+  // (wofs: the element offset of this lane's 8 weights in row lr of plane 0; read per use from L1)
+  auto head_mma = [&](const long wofs, const uint4& xh, const uint4& xl, const int j) {
+#pragma unroll
+    for (int hb = 0; hb < 2; ++hb) {
+      uint4 wf[2][NPL];
+#pragma unroll
+      for (int pl = 0; pl < NPL; ++pl) wf[hb][pl] = *(const uint4*)(HW + pl * hps + (long)hb * 16 * H.k_pad + wofs);
+      f32x4 c2 = (f32x4){0.f, 0.f, 0.f, 0.f};
+      MT::mma(c2, wf[hb][0], xl);
+      MT::mma(c2, wf[hb][1], xh);
+      MT::mma(hacc[hb][j], wf[hb][0], xh);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) hacc[hb][j][r] = __builtin_fmaf(c2[r], SplitF32<2>::CS, hacc[hb][j][r]);
+    }
+  };
 #pragma unroll
   for (int i = 0; i < WC; i += 2) {
+    // (HEAD: one channel pair at a time -- loads hoisted over the pairs would keep every pair's head
+    // weights live beside the accumulators)
+    if constexpr (HEAD) __builtin_amdgcn_sched_barrier(0);
     const int cs = c0 + wc * 16 * WC + (i + (g & 1)) * 16 + (g >> 1) * 8;  // this lane's 8 channels
     const bool cok = cs < A.Cout;
+    // BN scale / shift of the lane's 8 channels (HEAD: re-read per pixel block from L1, register pressure)
     float sc[8], sh[8];
+    auto load_bn = [&]() {
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      sc[r] = 1.f;
-      sh[r] = 0.f;
-    }
-    if (cok && S.scale) {
-      const float4 s0 = *(const float4*)(S.scale + cs), s1 = *(const float4*)(S.scale + cs + 4);
-      sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w;
-      sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
-    }
-    if (cok && S.shift) {
-      const float4 s0 = *(const float4*)(S.shift + cs), s1 = *(const float4*)(S.shift + cs + 4);
-      sh[0] = s0.x; sh[1] = s0.y; sh[2] = s0.z; sh[3] = s0.w;
-      sh[4] = s1.x; sh[5] = s1.y; sh[6] = s1.z; sh[7] = s1.w;
-    }
+      for (int r = 0; r < 8; ++r) {
+        sc[r] = 1.f;
+        sh[r] = 0.f;
+      }
+      if (cok && S.scale) {
+        const float4 s0 = *(const float4*)(S.scale + cs), s1 = *(const float4*)(S.scale + cs + 4);
+        sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w;
+        sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
+      }
+      if (cok && S.shift) {
+        const float4 s0 = *(const float4*)(S.shift + cs), s1 = *(const float4*)(S.shift + cs + 4);
+        sh[0] = s0.x; sh[1] = s0.y; sh[2] = s0.z; sh[3] = s0.w;
+        sh[4] = s1.x; sh[5] = s1.y; sh[6] = s1.z; sh[7] = s1.w;
+      }
+    };
+    if constexpr (!HEAD) load_bn();
+    // HEAD: the head weights of these 32 channels in the lanes' channel order (lane group g holds
+    // channels (g & 1) * 16 + (g >> 1) * 8 .. + 7 of the slice; the MFMA reads them as k slot g)
+    const long wofs = (long)lr * H.k_pad + cs;
 #pragma unroll
     for (int j = 0; j < WP; ++j) {
       float v[8];
@@ -315,11 +370,16 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
         v[r] = __uint_as_float(sw[0]);
         v[r + 4] = __uint_as_float(sw[1]);
       }
-      if (!pok[j] || !cok) continue;
-      const size_t pix = ((size_t)pn[j] * S.OH + poy[j]) * S.OW + pox[j];
+      if constexpr (HEAD) {
+        pi[j] = pixinfo(j);
+        load_bn();
+      }
+      const bool live = pi[j].ok && cok;
+      if (!HEAD && !live) continue;
+      const size_t pix = ((size_t)pi[j].n * S.OH + pi[j].oy) * S.OW + pi[j].ox;
 #pragma unroll
       for (int r = 0; r < 8; ++r) v[r] = v[r] * sc[r] + sh[r];
-      if (A.res) {
+      if (A.res && live) {
         const unsigned short* R = (const unsigned short*)A.res + pix * A.ldr + A.cr0 + cs;
         uint4 rq[NPL];
 #pragma unroll
@@ -339,6 +399,10 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
 #pragma unroll
         for (int r = 0; r < 8; ++r) v[r] = fmaxf(v[r], 0.f);
       }
+      if (HEAD && !live) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) v[r] = 0.f;
+      }
       uint32_t o[NPL][4];
 #pragma unroll
       for (int r = 0; r < 8; r += 2) {
@@ -349,6 +413,11 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
 #pragma unroll
         for (int p = 0; p < NPL; ++p) o[p][r >> 1] = (uint32_t)q0[p] | ((uint32_t)q1[p] << 16);
       }
+      if constexpr (HEAD) {  // the conv output is not stored: it feeds the head
+        head_mma(wofs, make_uint4(o[0][0], o[0][1], o[0][2], o[0][3]), make_uint4(o[1][0], o[1][1], o[1][2], o[1][3]), j);
+        __builtin_amdgcn_sched_barrier(0);  // one pixel block at a time (register pressure)
+        continue;
+      }
       if ((flags & 16384) && v[0] != 1.f) continue;  // diagnostic: no stores (unless a value is exactly 1)
       unsigned short* Y = (unsigned short*)S.y + pix * S.ldy + S.cy0 + cs;
 #pragma unroll
@@ -356,6 +425,55 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
     }
   }
   raise_range_flag(TG.rflag, bad);
+  if constexpr (HEAD) {
+    // the second concat part (x2: the skip features, already split NHWC on the output grid) in the
+    // cout-half-0 waves, its weights at k = Cout + c
+    if (wc == 0) {
+      const long psx2 = (long)A.N * S.OH * S.OW * H.ldx2;
+      for (int q = 0; q < H.C2 / 32; ++q) {
+        const long wofs = (long)lr * H.k_pad + A.Cout + q * 32 + g * 8;
+#pragma unroll
+        for (int j = 0; j < WP; ++j) {
+          uint4 xq[NPL];
+          const PixInfo q2 = pixinfo(j);
+          const size_t pix = ((size_t)q2.n * S.OH + q2.oy) * S.OW + q2.ox;
+          const unsigned short* X2 = (const unsigned short*)H.x2 + pix * H.ldx2 + H.cx20 + q * 32 + g * 8;
+#pragma unroll
+          for (int pl = 0; pl < NPL; ++pl) xq[pl] = q2.ok ? *(const uint4*)(X2 + pl * psx2) : make_uint4(0u, 0u, 0u, 0u);
+          head_mma(wofs, xq[0], xq[1], j);
+        }
+      }
+    }
+    // the two cout halves' sums meet in LDS (free: every wave passed the main loop's last barrier)
+    f32x4* red = (f32x4*)lds;  // [wp][hb][j][lane]
+    if (wc == 1) {
+#pragma unroll
+      for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+        for (int j = 0; j < WP; ++j) red[((wp * 2 + hb) * WP + j) * 64 + lane] = hacc[hb][j];
+    }
+    __syncthreads();
+    if (wc == 0) {
+      const size_t plane = (size_t)S.OH * S.OW;
+#pragma unroll
+      for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+        for (int j = 0; j < WP; ++j) {
+          const f32x4 o = red[((wp * 2 + hb) * WP + j) * 64 + lane];
+          const PixInfo q2 = pixinfo(j);
+          if (!q2.ok) continue;
+          const size_t sp = (size_t)q2.oy * S.OW + q2.ox;
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) {
+            const int r = hb * 16 + g * 4 + qq;
+            if (r >= H.cout) continue;
+            const float val = (hacc[hb][j][qq] + o[qq]) + (H.bias ? H.bias[r] : 0.f);
+            if (r == 0) H.mask[(size_t)q2.n * plane + sp] = val;
+            else H.code[((size_t)q2.n * (H.cout - 1) + (r - 1)) * plane + sp] = val;
+          }
+        }
+    }
+  }
 }
 
 // eligibility of the wide tile: two planes, NHWC output with 16-byte-aligned channel slices, Cout a
@@ -389,10 +507,19 @@ bool conv3w_ok(const zp_conv_args& a) {
 
 void conv3w_launch(const zp_conv_args& a, const conv_taps& tg, hipStream_t st, int fl) {
   const dim3 grid((unsigned)(((long)a.N * a.GH * a.GW + 255) / 256), (unsigned)(a.Cout / 256), (unsigned)a.nsub);
-  if (fl & 4096) hipLaunchKernelGGL(k_conv3w<1>, grid, dim3(512), 0, st, a, tg, fl);  // diagnostic: no DMA
-  else if (fl & 8192) hipLaunchKernelGGL(k_conv3w<2>, grid, dim3(512), 0, st, a, tg, fl);  // diagnostic: no MFMA
-  else if (fl & 131072) hipLaunchKernelGGL(k_conv3w<3>, grid, dim3(512), 0, st, a, tg, fl);  // diagnostic: no barrier
-  else hipLaunchKernelGGL(k_conv3w<0>, grid, dim3(512), 0, st, a, tg, fl);
+  // flags 262144 / 524288: the DMA pieces over the first 2 / 8 cout blocks (default: the first one)
+  const zp_head_args H{};
+  if (fl & 4096) hipLaunchKernelGGL((k_conv3w<1, 1, false>), grid, dim3(512), 0, st, a, tg, fl, H);  // diagnostic: no DMA
+  else if (fl & 8192) hipLaunchKernelGGL((k_conv3w<2, 1, false>), grid, dim3(512), 0, st, a, tg, fl, H);  // diagnostic: no MFMA
+  else if (fl & 131072) hipLaunchKernelGGL((k_conv3w<3, 1, false>), grid, dim3(512), 0, st, a, tg, fl, H);  // diagnostic: no barrier
+  else if (fl & 262144) hipLaunchKernelGGL((k_conv3w<0, 2, false>), grid, dim3(512), 0, st, a, tg, fl, H);
+  else if (fl & 524288) hipLaunchKernelGGL((k_conv3w<0, 8, false>), grid, dim3(512), 0, st, a, tg, fl, H);
+  else hipLaunchKernelGGL((k_conv3w<0, 1, false>), grid, dim3(512), 0, st, a, tg, fl, H);
+}
+
+void conv3w_head_launch(const zp_conv_args& a, const conv_taps& tg, const zp_head_args& h, hipStream_t st, int fl) {
+  const dim3 grid((unsigned)(((long)a.N * a.GH * a.GW + 255) / 256), 1u, 1u);
+  hipLaunchKernelGGL((k_conv3w<0, 1, true>), grid, dim3(512), 0, st, a, tg, fl, h);
 }
 
 }  // namespace zp

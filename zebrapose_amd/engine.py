@@ -160,6 +160,9 @@ class Engine:
         self._side = None
         self._side_used = False
         self.bn_mask_from_raw = True  # BN+ReLU backward without residual: mask from raw (A/B knob)
+        # two-plane eval forward: up2's last conv and the head in one launch (zp_conv2d_head);
+        # ZP_FUSE_HEAD=0 keeps them apart
+        self.fuse_head = os.environ.get("ZP_FUSE_HEAD", "1") != "0"
 
     # ------------------------------------------------------------------ weight / BN caches
     def invalidate(self):
@@ -263,9 +266,10 @@ class Engine:
 
     # ------------------------------------------------------------------ conv launch
     def _conv(self, x: Act, plan, cout, weights, k_pad, rows, outs, res=None, relu=False,
-              out_mode=L.ZP_OUT_NHWC, stats=None, small=None, label=None, dt=None):
+              out_mode=L.ZP_OUT_NHWC, stats=None, small=None, label=None, dt=None, head=None):
         """weights / outs: per sub.  outs[i] = (y_ptr, ldy, cy0, OH, OW, scale, shift, y2).  dt
-        overrides the engine's dtype code (the x3 engine's f32 stem)."""
+        overrides the engine's dtype code (the x3 engine's f32 stem).  head: (L.HeadArgs, head FLOPs,
+        head bytes) -- the conv feeds the fused 1x1 head (zp_conv2d_head) instead of storing."""
         dt = self.dt if dt is None else dt
         a = L.ConvArgs()
         a.dtype = dt
@@ -302,16 +306,25 @@ class Engine:
                 stats = torch.empty(nb // 4, dtype=torch.float32, device=x.buf.device)
                 a.stats = stats.data_ptr()
         st = L.stream_ptr()
+
+        def launch():
+            if head is not None:
+                L.check(L.lib.zp_conv2d_head(C.byref(a), C.byref(head[0]), st), "zp_conv2d_head")
+            else:
+                L.check(L.lib.zp_conv2d(C.byref(a), st), "zp_conv2d")
         if self.timing is not None or self.stage_log is not None:
             if self.timing is not None:
                 e0 = torch.cuda.Event(enable_timing=True)
                 e1 = torch.cuda.Event(enable_timing=True)
                 e0.record()
-            L.check(L.lib.zp_conv2d(C.byref(a), st), "zp_conv2d")
+            launch()
             if self.timing is not None:
                 e1.record()
             flops = 2.0 * x.B * plan.GH * plan.GW * sum(len(sb.taps) for sb in plan.subs) * x.C * cout
             kname = self._kname(a, plan, x, dt)
+            if head is not None:
+                flops += head[1]
+                kname = kname.replace("k_conv3w<", "k_conv3w_head<")
             geo = (f"{label}:{x.C}->{cout} taps{max(len(sb.taps) for sb in plan.subs)} "
                    f"{x.H}x{x.W}->{plan.GH}x{plan.GW}x{a.nsub}")
             # algorithmic HBM bytes: the input slice and every output read / written once, the
@@ -322,12 +335,14 @@ class Engine:
             mgrid = x.B * plan.GH * plan.GW
             nbytes = (x.P * x.C * es + len(plan.subs) * mgrid * cout * osz
                       + sum(w.numel() * w.element_size() for w in weights) + (0 if res is None else mgrid * cout * es))
+            if head is not None:  # no conv output stored; the head's inputs / outputs instead
+                nbytes += head[2] - len(plan.subs) * mgrid * cout * osz
             if self.timing is not None:
                 self.timing.append((geo, e0, e1, flops, kname, nbytes))
             if self.stage_log is not None:
                 self.stage_log.append((self.stage, kname, flops, nbytes, geo))
         else:
-            L.check(L.lib.zp_conv2d(C.byref(a), st), "zp_conv2d")
+            launch()
         return stats, parts
 
     def _kname(self, a, plan, x, dt=None):
@@ -337,6 +352,8 @@ class Engine:
         tc, tp, stages, var = C.c_int(), C.c_int(), C.c_int(), C.c_int()
         L.call("zp_conv2d_config", C.byref(a), C.byref(tc), C.byref(tp), C.byref(stages), C.byref(var))
         tn = _TN[dt]
+        if var.value == 6:  # rocprofv3 name: k_conv3w<ABL, DM, HEAD>
+            return f"k_conv3w<{tn}>"
         if var.value == 5:  # rocprofv3 name: k_conv3s<NPL, WC>
             return f"k_conv3s<{tn},WC={tc.value // 32}>"
         if var.value == 4:  # rocprofv3 name: k_conv3<NPL, WC, WP, NWP, ST, PIPE>
@@ -475,6 +492,39 @@ class Engine:
             tape.recs.append(("head", unit, x, key, None, None, None))
         elif self.trace is not None:
             self.trace.append(("head", unit, x, (mask, code), None))
+
+    def head_fusable(self, B, H, W):
+        """True when the two-plane engine runs up2's last conv and the 1x1 head as one launch
+        (zp_conv2d_head): eval forward, no trace, and the 256 x 256 tile eligible at this grid."""
+        if self.dt != L.ZP_F32H2 or not self.fuse_head or self.trace is not None:
+            return False
+        a = L.ConvArgs()
+        a.dtype, a.Cin, a.Cout, a.w_rows, a.N, a.GH, a.GW = L.ZP_F32H2, 256, 256, 256, B, H, W
+        a.out_mode, a.nsub = L.ZP_OUT_NHWC, 1
+        a.sub[0].ldy, a.sub[0].cy0 = 256, 0
+        return bool(L.lib.zp_conv2d_head_ok(C.byref(a)))
+
+    def unit_fwd_head(self, unit, x: Act, head_unit, x2: Act, mask, code):
+        """unit (3x3 conv + BN + ReLU, Cout 256) feeding the head conv over [its output | x2] in one
+        launch (zp_conv2d_head): the reference's upsample_2[6:9] then conv_1x1_4(torch.cat([x, x_128]))
+        (aspp.py:105-112) and the mask / code split (BinaryCodeNet.py:172)."""
+        plan = unit.fwd_plan(x.H, x.W)
+        OH, OW = unit.out_hw(x.H, x.W)
+        ws, kp, rows = self._fwd_weights(unit, plan, cache=True)
+        scale, shift = self._fold(unit)
+        hp = head_unit.fwd_plan(OH, OW)
+        hk = G.ceil_to(head_unit.cin, 32)
+        hw = self._pack(head_unit, hp.subs[0], 0, head_unit.cin, hk, 32, "head_fused", True)
+        h = L.HeadArgs()
+        h.w, h.k_pad, h.bias, h.cout = hw.data_ptr(), hk, L.ptr(head_unit.conv.bias), head_unit.cout
+        h.x2, h.ldx2, h.cx20, h.C2 = x2.ptr, x2.ld, x2.c0, x2.C
+        h.mask, h.code = mask.data_ptr(), L.ptr(code)
+        B = x.B
+        hflops = 2.0 * B * OH * OW * head_unit.cin * head_unit.cout
+        hbytes = B * OH * OW * (x2.C * _ES[self.dt] + head_unit.cout * 4) + hw.numel() * hw.element_size()
+        outs = [(mask.data_ptr(), 256, 0, OH, OW, scale, shift, None)]  # (y: never written by the fused launch)
+        self._conv(x, plan, unit.cout, ws, kp, rows, outs, None, unit.relu, label="upconv+head",
+                   head=(h, hflops, hbytes))
 
     # ------------------------------------------------------------------ backward pieces
     def _grad_buf(self, gmap, act: Act):
@@ -730,8 +780,13 @@ class Engine:
         H2, W2 = H // 2, W // 2
         H4, W4, H8, W8 = H // 4, W // 4, H // 8, W // 8
         c64 = 64 if rn.num_layers == 34 else 256
-        head_in = self._empty((B, H2, W2, 320), dev)
-        x128 = Act(head_in, 256, 64)
+        fuse = tape is None and rn.num_layers == 34 and self.head_fusable(B, H2, W2)
+        if fuse:  # the head reads x_128 itself: no [up2 | x_128] concat buffer
+            head_in = None
+            x128 = Act(self._empty((B, H2, W2, 64), dev))
+        else:
+            head_in = self._empty((B, H2, W2, 320), dev)
+            x128 = Act(head_in, 256, 64)
         self.unit_fwd(self._u(r[0], r[1], True, cin_act=8), xin, x128, tape, label="stem")
         self.stage = "layer1"
         pooled = new(H4, W4, 64)
@@ -774,12 +829,16 @@ class Engine:
         self.stage = "up1"
         self._upsample(aspp.upsample_1, o, Act(up2_in, 0, 256), tape)
         self.stage = "up2"
-        self._upsample(aspp.upsample_2, Act(up2_in), Act(head_in, 0, 256), tape)
-        self.stage = "head"
         ncls = aspp.conv_1x1_4.out_channels
         mask = torch.empty((B, 1, H2, W2), dtype=torch.float32, device=dev)
         code = torch.empty((B, ncls - 1, H2, W2), dtype=torch.float32, device=dev)
-        self.head_fwd(self._u(aspp.conv_1x1_4, None, False), Act(head_in), mask, code, tape)
+        if fuse:
+            self._upsample(aspp.upsample_2, Act(up2_in), None, tape,
+                           head=(self._u(aspp.conv_1x1_4, None, False), x128, mask, code))
+        else:
+            self._upsample(aspp.upsample_2, Act(up2_in), Act(head_in, 0, 256), tape)
+            self.stage = "head"
+            self.head_fwd(self._u(aspp.conv_1x1_4, None, False), Act(head_in), mask, code, tape)
         r = {"mask": mask, "code": code, "tape": tape, "xh": xh, "x64": x64, "x128": x128}
         if tape is not None and self.bwd_trace is not None:
             self.last_fwd = r  # the traced training step's outputs and tape (teacher-forced tests)
@@ -851,7 +910,9 @@ class Engine:
             u = cache[key] = Unit(conv, bn, relu, cin_act)
         return u
 
-    def _upsample(self, seq, x: Act, out: Act, tape, cin_act=None):
+    def _upsample(self, seq, x: Act, out: Act, tape, cin_act=None, head=None):
+        """aspp.py:60-80 (ConvT + BN + ReLU, 2 x (conv + BN + ReLU)); head = (head unit, x2, mask,
+        code): the last conv feeds the fused head instead of writing ``out``."""
         h1 = self._u(seq[0], seq[1], cin_act=cin_act)
         OH, OW = h1.out_hw(x.H, x.W)
         dev = x.buf.device
@@ -859,7 +920,10 @@ class Engine:
         self.unit_fwd(h1, x, t1, tape, label="upconvT")
         t2 = Act(self._empty((x.B, OH, OW, 256), dev))
         self.unit_fwd(self._u(seq[3], seq[4]), t1, t2, tape, label="upconv")
-        self.unit_fwd(self._u(seq[6], seq[7]), t2, out, tape, label="upconv")
+        if head is not None:
+            self.unit_fwd_head(self._u(seq[6], seq[7]), t2, head[0], head[1], head[2], head[3])
+        else:
+            self.unit_fwd(self._u(seq[6], seq[7]), t2, out, tape, label="upconv")
 
     def _layer(self, seq, x: Act, final_out: Act, tape):
         n = len(seq)
