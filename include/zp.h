@@ -278,6 +278,15 @@ int zp_nchw_to_nhwc(const float* x, int B, int C, int H, int W, int cpad, int dt
  * split-fp32 conv over kpad channels, weights packed with zp_pack_weight(..., cstride = C, ...). */
 int zp_im2col_split(const float* x, int B, int H, int W, int ldx, int C, int k, int s, int p, int OH, int OW,
                     int kpad, int dtype, void* y, void* stream);
+/* The stem conv of the two-plane engine in one launch (ZP_F32H2 only): torchvision conv1 (7x7,
+ * stride 2, pad 3, 3 -> 64 channels; reference model/resnet.py:195) + folded BN (scale, shift) +
+ * ReLU, from the f32 NHWC image x [B][H][W][ldx] (channels 0..2; ldx a multiple of 4) to a ZP_F32H2
+ * NHWC slice y [2][B][OH][OW][ldy] at channel cy0.  Weights: zp_pack_weight of the 7x7 kernel in
+ * the zp_im2col_split order (taps row-major, cstride 3, k_pad 160, dtype ZP_F32H2, w_rows >= 64).
+ * Replaces zp_im2col_split + the 1x1 split GEMM (no patch tensor).  OW must divide 256. */
+int zp_stem_split(const float* x, int B, int H, int W, int ldx, const void* w, int w_rows, int k_pad,
+                  const float* scale, const float* shift, int dtype, void* y, int ldy, int cy0, int OH, int OW,
+                  void* stream);
 /* 3x3 / stride 2 / pad 1 max pool, NHWC slices; C multiple of 8 */
 int zp_maxpool3s2(const void* x, int B, int IH, int IW, int ldx, int cx0, int C, int dtype,
                   void* y, int OH, int OW, int ldy, int cy0, void* stream);

@@ -155,7 +155,7 @@ def stage_table(src, prec):
         k["grbm"] += m[2].get("GRBM_GUI_ACTIVE", 0.0)
     rows = []
     labels = " ".join(per_kernel)
-    form = "h2" if "k_conv3<h2" in labels or "k_conv3s<h2" in labels else (
+    form = "h2" if any(k in labels for k in ("k_conv3<h2", "k_conv3s<h2", "k_conv3w<h2", "k_conv3w_head<h2")) else (
         "x3" if "k_conv3<x3" in labels or "k_conv3s<x3" in labels else None)
     tot = defaultdict(float)
     for s in STAGES + ["other"]:

@@ -122,6 +122,7 @@ _SIGS = {
     "zp_adam_multi": (i32, [i32, vp, vp, vp, vp, vp, f64, f64, f64, f64, i64, vp]),
     "zp_adam_multi_dev": (i32, [i32, vp, vp, vp, vp, vp, f64, f64, f64, f64, vp, vp]),
     "zp_split_range_flag": (i32, [vp]),
+    "zp_stem_split": (i32, [vp, i32, i32, i32, i32, vp, i32, i32, vp, vp, i32, vp, i32, i32, i32, i32, vp]),
     "zp_conv2d_head_ok": (i32, [C.POINTER(ConvArgs)]),
     "zp_conv2d_head": (i32, [C.POINTER(ConvArgs), C.POINTER(HeadArgs), vp]),
 }

@@ -2767,7 +2767,7 @@ extern "C" int zp_conv2d_stat_parts(const zp_conv_args* a) {
 
 extern "C" int zp_conv2d_head_ok(const zp_conv_args* a) {
   return a && a->dtype == ZP_F32H2 && a->nsub == 1 && a->Cout == 256 && a->out_mode == ZP_OUT_NHWC &&
-         conv3_tc(*a) == 256;
+         conv3_tc(*a) == 256 && conv3w_splitk(*a) == 1;
 }
 
 extern "C" int zp_conv2d_head(const zp_conv_args* a, const zp_head_args* h, void* stream) {
@@ -2839,6 +2839,7 @@ extern "C" int zp_conv_tuning(int key, int value) {
   if (key == 9) return conv3_splitk_mode(value);
   if (key == 10) return conv3w_mode(value);
   if (key == 11) return conv3w_min_blocks(value);
+  if (key == 12) return conv3w_splitk_mode(value);
   if (key == 4) {
     const int old = g_wgrad2_rounds;
     g_wgrad2_rounds = value > 0 ? value : 1;

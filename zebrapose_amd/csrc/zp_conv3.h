@@ -16,6 +16,8 @@ struct conv_taps;
 bool conv3w_ok(const zp_conv_args& a);            // eligible (and enabled)
 int conv3w_mode(int v);                           // zp_conv_tuning key 10; returns the previous value
 int conv3w_min_blocks(int v);                     // zp_conv_tuning key 11; returns the previous value
-void conv3w_launch(const zp_conv_args& a, const conv_taps& tg, hipStream_t st, int flags);
+void conv3w_launch(const zp_conv_args& a, const conv_taps& tg, hipStream_t st, int flags, float* ws, int nsplit);
+int conv3w_splitk(const zp_conv_args& a);         // split-K slices of the wide tile (1: none)
+int conv3w_splitk_mode(int v);                    // zp_conv_tuning key 12; returns the previous value
 void conv3w_head_launch(const zp_conv_args& a, const conv_taps& tg, const zp_head_args& h, hipStream_t st, int flags);
 }  // namespace zp

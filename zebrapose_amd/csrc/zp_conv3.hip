@@ -1002,6 +1002,7 @@ int conv3_splitk_mode(int v) {
 int conv3_nsplit(const zp_conv_args& a) {
   if (!g_splitk || a.out_mode != ZP_OUT_NHWC || a.nsub < 1) return 1;
   const int tc = conv3_tc(a);
+  if (tc == 256) return conv3w_splitk(a);
   const long blocks = (long)ceil_div((long)a.N * a.GH * a.GW, conv3_tp(a, tc)) * ceil_div(a.Cout, tc) * a.nsub;
   int nK = 1 << 30;  // the shortest sub-problem's K steps (ConvT phases: 1 .. 4 taps)
   for (int s = 0; s < a.nsub; ++s) nK = min(nK, a.sub[s].ntaps * (a.Cin / 32));
@@ -1014,8 +1015,15 @@ int conv3_nsplit(const zp_conv_args& a) {
 // kernel launches for one split form (NPL planes: 3 = ZP_F32X3, 2 = ZP_F32H2)
 template <int NPL>
 static void conv3_dispatch(const zp_conv_args& a, const conv_taps& tg, int tc, hipStream_t st, int fl) {
-  if (tc == 256) {  // 256 x 256 two-plane tile (zp_conv3w.hip)
-    conv3w_launch(a, tg, st, fl);
+  if (tc == 256) {  // 256 x 256 two-plane tile (zp_conv3w.hip), split-K for small grids
+    const int ns = a.stats ? conv3w_splitk(a) : 1;
+    conv3w_launch(a, tg, st, fl, (float*)a.stats, ns);
+    if (ns > 1) {
+      const long total = (long)a.N * a.GH * a.GW * ((a.Cout + 3) / 4);
+      const int blocks = (int)(total + 255) / 256 < 8192 ? (int)((total + 255) / 256) : 8192;
+      hipLaunchKernelGGL((k_splitk_epi<NPL>), dim3(blocks, a.nsub), dim3(256), 0, st, a, (const float*)a.stats, ns,
+                         tg.rflag);
+    }
     return;
   }
   const int ns = a.stats ? conv3_nsplit(a) : 1;

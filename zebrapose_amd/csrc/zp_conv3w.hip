@@ -44,9 +44,11 @@ __device__ __forceinline__ void wbarrier() {
 // block, after its correction MFMAs)
 // HEAD: the fused 1x1 head (zp_conv2d_head): the conv output feeds the head's MFMAs instead of
 // being stored
+// nsplit > 1 (small grids, e.g. bs = 1): blockIdx.z = sub * nsplit + K slice; the slice's raw f32
+// sums go to ws [nsub][nsplit][M][Cout] and k_splitk_epi (zp_conv3.hip) finishes them
 template <int ABL, int DM, bool HEAD>
 __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv_taps TG, const int flags,
-                                                const zp_head_args H) {
+                                                const zp_head_args H, float* __restrict__ ws, const int nsplit) {
   constexpr int NPL = 2;
   constexpr int TC = 256, TP = 256;
   constexpr int NTW = TC / 16, NT = (TC + TP) / 16;  // weight tiles / all tiles per plane (16 rows each)
@@ -58,7 +60,7 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
   __shared__ uint4 lds[2 * UNITS * 64];
   static_assert(2 * UNITS * 1024 <= 160 * 1024, "LDS");
   static_assert(((NPL - 1) * NT + NT - 1) * 1024 < 65536, "ds_read immediate range");
-  const int tb = (int)blockIdx.z;
+  const int tb = (int)blockIdx.z / nsplit, kz = (int)blockIdx.z - tb * nsplit;
   const zp_conv_sub& S = A.sub[tb];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -76,7 +78,9 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
   const int p0 = bx * TP, c0 = by * TC;
   const int CB = A.Cin / 32;
   const int ny = TG.ny[tb], nx = TG.nx[tb], dty = TG.dty[tb], dtx = TG.dtx[tb];
-  const int nK = S.ntaps * CB;
+  const int nK_all = S.ntaps * CB;
+  const int ks0 = (int)((long)kz * nK_all / nsplit);
+  const int nK = (int)((long)(kz + 1) * nK_all / nsplit) - ks0;  // this slice's K steps
   const int lr = lane & 15, lk = (lane >> 4) * 8;
   const unsigned psx_b = (unsigned)((long)A.N * A.IH * A.IW * A.ldx * 2);
   const unsigned psw_b = (unsigned)((long)A.w_rows * A.k_pad * 2);
@@ -111,10 +115,12 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
 #endif
   // scalar walk of the next step to issue: 32-channel chunk outer, taps inner (k_conv3's order: the
   // taps of one chunk re-read nearly the same input rows from L2)
-  int w_cb = 0, w_tyi = 0, w_txi = 0;
+  // (the walk starts at step ks0 = (chunk w_cb, tap w_tyi * nx + w_txi))
+  const int t0 = ks0 % S.ntaps;
+  int w_cb = ks0 / S.ntaps, w_tyi = t0 / nx, w_txi = t0 - (t0 / nx) * nx;
   const int step_x = dtx * A.ldx * 2, step_y = dty * A.IW * A.ldx * 2;
-  int act_off = ((TG.ty0[tb] * A.IW + TG.tx0[tb]) * A.ldx) * 2;
-  int w_koff = 0;
+  int act_off = ((TG.ty0[tb] * A.IW + TG.tx0[tb]) * A.ldx) * 2 + w_tyi * step_y + w_txi * step_x + w_cb * 64;
+  int w_koff = (t0 * A.Cin + w_cb * 32) * 2;
   const int cin2 = A.Cin * 2;
   // the DMA of one K step as 8 pieces (tile k = q / 2 of this wave, plane q % 2): prep() forms the
   // per-lane offsets of the next step to issue and advances the walk; piece<q>() issues one piece
@@ -272,6 +278,21 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
     vm_wait<0>();
     if constexpr (!abl_bar) wbarrier();
     __builtin_amdgcn_sched_barrier(0);
+  }
+
+  if (!HEAD && nsplit > 1) {  // split-K slice: raw f32 sums (acc[i][j] = 4 channels x one grid point)
+    float* wsl = ws + ((size_t)tb * nsplit + kz) * M * A.Cout;
+#pragma unroll
+    for (int j = 0; j < WP; ++j) {
+      const int p = p0 + wp * 16 * WP + j * 16 + lr;
+      if (p >= M) continue;
+#pragma unroll
+      for (int i = 0; i < WC; ++i) {
+        const int cf = c0 + wc * 16 * WC + i * 16 + (lane >> 4) * 4;
+        *(float4*)(wsl + (size_t)p * A.Cout + cf) = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+      }
+    }
+    return;
   }
 
   // ---------------- epilogue: paired lane groups, 16 B per lane and plane ----------------
@@ -479,6 +500,7 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
 // eligibility of the wide tile: two planes, NHWC output with 16-byte-aligned channel slices, Cout a
 // multiple of 256 and a grid of at least g_conv3w_min workgroups (fewer: k_conv3's 128 x 256 tile
 // keeps more CUs busy)
+int conv3w_splitk(const zp_conv_args& a);
 static int g_conv3w = -1;       // zp_conv_tuning key 10 (-1: ZP_CONV3W or the default 1)
 static int g_conv3w_min = 256;  // zp_conv_tuning key 11
 
@@ -502,24 +524,44 @@ bool conv3w_ok(const zp_conv_args& a) {
     if (a.sub[s].ldy % 8 != 0 || a.sub[s].cy0 % 8 != 0) return false;
   if (a.res && (a.ldr % 8 != 0 || a.cr0 % 8 != 0)) return false;
   const long blocks = (((long)a.N * a.GH * a.GW + 255) / 256) * (a.Cout / 256) * a.nsub;
-  return blocks >= g_conv3w_min;
+  return blocks >= g_conv3w_min || conv3w_splitk(a) > 1;
 }
 
-void conv3w_launch(const zp_conv_args& a, const conv_taps& tg, hipStream_t st, int fl) {
-  const dim3 grid((unsigned)(((long)a.N * a.GH * a.GW + 255) / 256), (unsigned)(a.Cout / 256), (unsigned)a.nsub);
+// split-K of the wide tile (zp_conv_tuning key 12, default 1): a one-sub NHWC launch under 64 tiles
+// (bs = 1: up2's 3 x 3 at 128 x 128 is 64 tiles, layer5's 512 -> 512 32) is cut along K into up to
+// 8 slices of >= 12 steps, for 256..512 workgroups
+static int g_conv3w_splitk = 1;
+int conv3w_splitk_mode(int v) {
+  const int old = g_conv3w_splitk;
+  g_conv3w_splitk = v;
+  return old;
+}
+int conv3w_splitk(const zp_conv_args& a) {
+  if (!g_conv3w_splitk || a.nsub != 1 || a.out_mode != ZP_OUT_NHWC || a.dtype != ZP_F32H2 || a.Cout % 256 != 0)
+    return 1;
+  const long blocks = (((long)a.N * a.GH * a.GW + 255) / 256) * (a.Cout / 256);
+  if (blocks > 64) return 1;
+  const int nK = a.sub[0].ntaps * (a.Cin / 32);
+  int ns = 1;
+  while (ns < 8 && blocks * ns * 2 <= 512 && nK / (ns * 2) >= 12) ns *= 2;
+  return ns;
+}
+
+void conv3w_launch(const zp_conv_args& a, const conv_taps& tg, hipStream_t st, int fl, float* ws, int ns) {
+  const dim3 grid((unsigned)(((long)a.N * a.GH * a.GW + 255) / 256), (unsigned)(a.Cout / 256), (unsigned)(a.nsub * ns));
   // flags 262144 / 524288: the DMA pieces over the first 2 / 8 cout blocks (default: the first one)
   const zp_head_args H{};
-  if (fl & 4096) hipLaunchKernelGGL((k_conv3w<1, 1, false>), grid, dim3(512), 0, st, a, tg, fl, H);  // diagnostic: no DMA
-  else if (fl & 8192) hipLaunchKernelGGL((k_conv3w<2, 1, false>), grid, dim3(512), 0, st, a, tg, fl, H);  // diagnostic: no MFMA
-  else if (fl & 131072) hipLaunchKernelGGL((k_conv3w<3, 1, false>), grid, dim3(512), 0, st, a, tg, fl, H);  // diagnostic: no barrier
-  else if (fl & 262144) hipLaunchKernelGGL((k_conv3w<0, 2, false>), grid, dim3(512), 0, st, a, tg, fl, H);
-  else if (fl & 524288) hipLaunchKernelGGL((k_conv3w<0, 8, false>), grid, dim3(512), 0, st, a, tg, fl, H);
-  else hipLaunchKernelGGL((k_conv3w<0, 1, false>), grid, dim3(512), 0, st, a, tg, fl, H);
+  if (fl & 4096) hipLaunchKernelGGL((k_conv3w<1, 1, false>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);  // diagnostic: no DMA
+  else if (fl & 8192) hipLaunchKernelGGL((k_conv3w<2, 1, false>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);  // diagnostic: no MFMA
+  else if (fl & 131072) hipLaunchKernelGGL((k_conv3w<3, 1, false>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);  // diagnostic: no barrier
+  else if (fl & 262144) hipLaunchKernelGGL((k_conv3w<0, 2, false>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
+  else if (fl & 524288) hipLaunchKernelGGL((k_conv3w<0, 8, false>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
+  else hipLaunchKernelGGL((k_conv3w<0, 1, false>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
 }
 
 void conv3w_head_launch(const zp_conv_args& a, const conv_taps& tg, const zp_head_args& h, hipStream_t st, int fl) {
   const dim3 grid((unsigned)(((long)a.N * a.GH * a.GW + 255) / 256), 1u, 1u);
-  hipLaunchKernelGGL((k_conv3w<0, 1, true>), grid, dim3(512), 0, st, a, tg, fl, h);
+  hipLaunchKernelGGL((k_conv3w<0, 1, true>), grid, dim3(512), 0, st, a, tg, fl, h, nullptr, 1);
 }
 
 }  // namespace zp

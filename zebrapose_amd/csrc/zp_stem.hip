@@ -1,0 +1,178 @@
+// k_stem_h2: the ResNet stem conv (torchvision conv1: 7x7, stride 2, pad 3, 3 -> 64 channels;
+// reference model/resnet.py:195, 233-236) + folded BN + ReLU for the two-plane split-fp32 engine
+// (ZP_F32H2), straight from the f32 NHWC image.
+//
+// The round-3 split stem was two launches: zp_im2col_split wrote the 7 x 7 x 3 patches of every
+// output pixel in split form (160 elements x 2 planes x 2 B = 640 B per pixel: 335 MB at bs 32, 171
+// us), then a 1 x 1 split GEMM read them back (K = 160: five K steps per tile, ~190 us).  Here a
+// workgroup stages the f32 input rows its 256 output pixels need (2 TR + 5 rows of 2 OW + 5 pixels,
+// 3 channels: 28 KB at OW = 128) in LDS once, and every lane builds its own MFMA B fragments from
+// them: the 16 x 16 x 32 B operand of lane l is pixel l & 15, patch elements (l >> 4) * 8 .. + 7 of
+// the K step -- exactly what the lane itself can gather -- split into the two fp16 planes in
+// registers.  No patch tensor exists.  Weights (packed for the im2col order k = tap * 3 + c,
+// zp_pack_weight with cstride 3) are read as fragments from L2 / L1 (40 KB, every workgroup).
+// Numerics: SplitF32<2> operands, hi*hi + (hi*lo' + lo'*hi) * 2^-11 per product, the correction
+// accumulator flushed after each K step (k_conv3w's arithmetic).
+// Tile: 4 waves, 64 output channels x 256 pixels (a wave: 64 x 64, 4 x 4 blocks of 16 x 16).
+#include "zp_conv_kern.h"
+
+namespace zp {
+
+constexpr int STEM_K = 7, STEM_S = 2, STEM_P = 3, STEM_C = 3, STEM_KP = 160;  // 147 patch elements -> 160
+
+__global__ void __launch_bounds__(256) k_stem_h2(const float* __restrict__ x, int H, int W, int ldx,
+                                                 const unsigned short* __restrict__ w, int w_rows,
+                                                 const float* __restrict__ scale, const float* __restrict__ shift,
+                                                 unsigned short* __restrict__ y, int ldy, int cy0, int OH, int OW,
+                                                 long psy, unsigned* rflag) {
+  constexpr int NPL = 2, WC = 4, WP = 4;
+  using MT = MfmaTraits<f16_t>;
+  using SP = SplitF32<NPL>;
+  extern __shared__ float region[];  // [IR][IC][3] f32
+  const int TR = 256 / OW;           // output rows per tile
+  const int IR = STEM_S * TR + STEM_K - STEM_S, IC = STEM_S * OW + STEM_K - STEM_S;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wp = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lr = lane & 15, g = lane >> 4;
+  const int tiles_per_img = (OH * OW) / 256;
+  const int n = blockIdx.x / tiles_per_img;
+  const int oy0 = (blockIdx.x - n * tiles_per_img) * TR;
+  const int iy0 = oy0 * STEM_S - STEM_P, ix0 = -STEM_P;
+  // stage the input region (zeros outside the image)
+  for (int e = tid; e < IR * IC; e += 256) {
+    const int r = e / IC, c = e - r * IC;
+    const int iy = iy0 + r, ix = ix0 + c;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) v = *(const float4*)(x + (((size_t)n * H + iy) * W + ix) * ldx);
+    region[e * 3 + 0] = v.x;
+    region[e * 3 + 1] = v.y;
+    region[e * 3 + 2] = v.z;
+  }
+  __syncthreads();
+  // this lane's pixels: block j -> tile pixel wp * 64 + j * 16 + lr -> (oy - oy0, ox)
+  int pbase[WP];
+#pragma unroll
+  for (int j = 0; j < WP; ++j) {
+    const int q = wp * 64 + j * 16 + lr;
+    const int ty = q / OW, tx = q - ty * OW;
+    pbase[j] = (ty * STEM_S * IC + tx * STEM_S) * 3;  // region offset of the patch's (0, 0, 0)
+  }
+  f32x4 acc[WC][WP];
+#pragma unroll
+  for (int i = 0; i < WC; ++i)
+#pragma unroll
+    for (int j = 0; j < WP; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const long wps = (long)w_rows * STEM_KP;  // weight plane stride
+  bool bad = false;
+#pragma unroll 1
+  for (int ks = 0; ks < STEM_KP / 32; ++ks) {
+    // weight fragments (rows i * 16 + lr, k = ks * 32 + 8 g ..)
+    uint4 af[WC][NPL];
+#pragma unroll
+    for (int i = 0; i < WC; ++i)
+#pragma unroll
+      for (int pl = 0; pl < NPL; ++pl)
+        af[i][pl] = *(const uint4*)(w + pl * wps + (long)(i * 16 + lr) * STEM_KP + ks * 32 + g * 8);
+    // the region offsets of this lane's 8 patch elements kk = ks * 32 + 8 g + e (kk >= 147: zero)
+    int eo[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int kk = ks * 32 + g * 8 + e;
+      const int t = kk / STEM_C, c = kk - t * STEM_C;
+      const int ky = t / STEM_K, kx = t - ky * STEM_K;
+      eo[e] = kk < STEM_K * STEM_K * STEM_C ? (ky * IC + kx) * 3 + c : -1;
+    }
+#pragma unroll
+    for (int j = 0; j < WP; ++j) {
+      uint32_t hw[NPL][4];
+#pragma unroll
+      for (int e = 0; e < 8; e += 2) {
+        const float v0 = eo[e] >= 0 ? region[pbase[j] + eo[e]] : 0.f;
+        const float v1 = eo[e + 1] >= 0 ? region[pbase[j] + eo[e + 1]] : 0.f;
+        unsigned short q0[NPL], q1[NPL];
+        SP::split(v0, q0);
+        SP::split(v1, q1);
+        bad |= h2_overflow(v0) || h2_overflow(v1);
+#pragma unroll
+        for (int pl = 0; pl < NPL; ++pl) hw[pl][e >> 1] = (uint32_t)q0[pl] | ((uint32_t)q1[pl] << 16);
+      }
+      const uint4 bh = make_uint4(hw[0][0], hw[0][1], hw[0][2], hw[0][3]);
+      const uint4 bl = make_uint4(hw[1][0], hw[1][1], hw[1][2], hw[1][3]);
+#pragma unroll
+      for (int i = 0; i < WC; ++i) {
+        f32x4 c2 = (f32x4){0.f, 0.f, 0.f, 0.f};
+        MT::mma(c2, af[i][0], bl);
+        MT::mma(c2, af[i][1], bh);
+        MT::mma(acc[i][j], af[i][0], bh);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = __builtin_fmaf(c2[r], SP::CS, acc[i][j][r]);
+      }
+    }
+  }
+  // epilogue: BN scale / shift, ReLU, split; lane groups of cout blocks (i, i + 1) paired so a lane
+  // holds 8 consecutive channels of one pixel (16 B stores per plane)
+#pragma unroll
+  for (int i = 0; i < WC; i += 2) {
+    const int cs = (i + (g & 1)) * 16 + (g >> 1) * 8;
+    float sc[8], sh[8];
+    const float4 s0 = *(const float4*)(scale + cs), s1 = *(const float4*)(scale + cs + 4);
+    const float4 h0 = *(const float4*)(shift + cs), h1 = *(const float4*)(shift + cs + 4);
+    sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w; sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
+    sh[0] = h0.x; sh[1] = h0.y; sh[2] = h0.z; sh[3] = h0.w; sh[4] = h1.x; sh[5] = h1.y; sh[6] = h1.z; sh[7] = h1.w;
+#pragma unroll
+    for (int j = 0; j < WP; ++j) {
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {  // all lanes active (cross-lane op)
+        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][j][r]), __float_as_uint(acc[i + 1][j][r]),
+                                                         false, false);
+        v[r] = __uint_as_float(sw[0]);
+        v[r + 4] = __uint_as_float(sw[1]);
+      }
+      const int q = wp * 64 + j * 16 + lr;
+      const int oy = oy0 + q / OW, ox = q % OW;
+      uint32_t o[NPL][4];
+#pragma unroll
+      for (int r = 0; r < 8; r += 2) {
+        const float a = fmaxf(v[r] * sc[r] + sh[r], 0.f), b = fmaxf(v[r + 1] * sc[r + 1] + sh[r + 1], 0.f);
+        unsigned short q0[NPL], q1[NPL];
+        SP::split(a, q0);
+        SP::split(b, q1);
+        bad |= h2_overflow(a) || h2_overflow(b);
+#pragma unroll
+        for (int pl = 0; pl < NPL; ++pl) o[pl][r >> 1] = (uint32_t)q0[pl] | ((uint32_t)q1[pl] << 16);
+      }
+      unsigned short* Y = y + (((size_t)n * OH + oy) * OW + ox) * ldy + cy0 + cs;
+#pragma unroll
+      for (int pl = 0; pl < NPL; ++pl) *(uint4*)(Y + pl * psy) = make_uint4(o[pl][0], o[pl][1], o[pl][2], o[pl][3]);
+    }
+  }
+  raise_range_flag(rflag, bad);
+}
+
+}  // namespace zp
+
+using namespace zp;
+
+extern "C" int zp_stem_split(const float* x, int B, int H, int W, int ldx, const void* w, int w_rows, int k_pad,
+                             const float* scale, const float* shift, int dtype, void* y, int ldy, int cy0, int OH,
+                             int OW, void* stream) {
+  ZP_CHECK_ARG(dtype == ZP_F32H2, "zp_stem_split: dtype %d (the two-plane form only)", dtype);
+  ZP_CHECK_ARG(x && w && scale && shift && y && B > 0 && H > 0 && W > 0, "zp_stem_split: bad args");
+  ZP_CHECK_ARG(ldx >= 4 && ldx % 4 == 0, "zp_stem_split: input ldx %d (f32 NHWC, 16-byte pixels)", ldx);
+  ZP_CHECK_ARG(k_pad == STEM_KP && w_rows >= 64, "zp_stem_split: weights [2][w_rows >= 64][160] (got %d / %d)", w_rows,
+               k_pad);
+  ZP_CHECK_ARG(OH == (H + 2 * STEM_P - STEM_K) / STEM_S + 1 && OW == (W + 2 * STEM_P - STEM_K) / STEM_S + 1,
+               "zp_stem_split: OH / OW");
+  ZP_CHECK_ARG(OW <= 256 && 256 % OW == 0 && (OH * OW) % 256 == 0, "zp_stem_split: OW %d must divide 256", OW);
+  ZP_CHECK_ARG(ldy % 8 == 0 && cy0 % 8 == 0 && ldy >= cy0 + 64, "zp_stem_split: ldy / cy0");
+  const int TR = 256 / OW;
+  const size_t lds = (size_t)(STEM_S * TR + STEM_K - STEM_S) * (STEM_S * OW + STEM_K - STEM_S) * 3 * sizeof(float);
+  ZP_CHECK_ARG(lds <= 64 * 1024, "zp_stem_split: region %zu B", lds);
+  const long psy = (long)B * OH * OW * ldy;
+  hipLaunchKernelGGL(k_stem_h2, dim3((unsigned)((long)B * OH * OW / 256)), dim3(256), lds, (hipStream_t)stream, x, H, W,
+                     ldx, (const unsigned short*)w, w_rows, scale, shift, (unsigned short*)y, ldy, cy0, OH, OW, psy,
+                     range_flag());
+  ZP_LAUNCH_CHECK("zp_stem_split");
+  return ZP_OK;
+}

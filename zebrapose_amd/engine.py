@@ -131,6 +131,9 @@ class Engine:
         # split forms: the stem as im2col + split GEMM (ZP_SPLIT_STEM=0: the exact-f32 small-Cin
         # kernel writing split output)
         self.split_stem = os.environ.get("ZP_SPLIT_STEM", "1") != "0"
+        # two planes: the stem in one launch from the f32 image (zp_stem_split); ZP_STEM_DIRECT=0 keeps
+        # im2col + GEMM
+        self.stem_direct = os.environ.get("ZP_STEM_DIRECT", "1") != "0"
         self._packed = {}
         self._jobs = []  # (cache key, weight, PackJob) of every cached packing, for _prepack
         self._job_table = None
@@ -396,6 +399,23 @@ class Engine:
             assert not train, "the split engine runs eval forwards only"
             cr = unit.conv.weight.shape[1]
             kp = G.ceil_to(unit.k * unit.k * cr, 32)
+            if (self.dt == L.ZP_F32H2 and self.stem_direct and (unit.k, unit.s, unit.p, cr, unit.cout) == (7, 2, 3, 3, 64)
+                    and OW <= 256 and 256 % OW == 0 and (OH * OW) % 256 == 0 and out.ld % 8 == 0 and out.c0 % 8 == 0
+                    and x.ld % 4 == 0):
+                # one launch from the f32 image (zp_stem_split): no patch tensor
+                taps = [(ky, kx) for ky in range(unit.k) for kx in range(unit.k)]
+                rows = G.ceil_to(unit.cout, 128)
+                w = self._pack(unit, G.Sub(taps, [(0, 0)] * len(taps)), 0, cr, kp, rows, "stem_im2col")
+                scale, shift = self._fold(unit)
+                L.call("zp_stem_split", x.ptr, x.B, x.H, x.W, x.ld, w.data_ptr(), rows, kp, scale.data_ptr(),
+                       shift.data_ptr(), self.dt, out.ptr, out.ld, out.c0, OH, OW, L.stream_ptr())
+                if self.stage_log is not None:
+                    fl = 2.0 * x.B * OH * OW * unit.k * unit.k * cr * unit.cout
+                    nb = x.P * x.ld * 4 + x.B * OH * OW * unit.cout * 4 + w.numel() * w.element_size()
+                    self.stage_log.append((self.stage, "k_stem_h2", fl, nb, f"{label}:{cr}->{unit.cout} 7x7s2"))
+                if self.trace is not None:
+                    self.trace.append(("conv", unit, x, out, res))
+                return
             col = Act(self._empty((x.B, OH, OW, kp), x.buf.device))
             L.call("zp_im2col_split", x.ptr, x.B, x.H, x.W, x.ld, cr, unit.k, unit.s, unit.p, OH, OW, kp, self.dt,
                    col.ptr, L.stream_ptr())
