@@ -44,6 +44,23 @@ def main():
     res = {}
     setups = []
     for name in a.layers.split(","):
+        if name == "aspp":  # the merged ASPP launch: 1x1 + 3x3 d6 / d12 / d18, 512 -> 4 x 256 at 32 x 32
+            eng = Engine(torch.nn.Module(), torch.float32, split=a.form)
+            units = []
+            for kk, dd in ((1, 1), (3, 6), (3, 12), (3, 18)):
+                conv = LY.Conv2d(512, 256, kk, 1, 0 if kk == 1 else dd, dd, bias=True).to(dev)
+                units.append(Unit(conv, LY.BatchNorm2d(256).to(dev).eval(), relu=True))
+            xs = eng._empty((a.batch, 32, 32, 512), dev)
+            xs._base.copy_(torch.randn(xs._base.shape, device=dev).clamp(min=0).to(xs.dtype))
+            A = eng._empty((a.batch, 32, 32, 1280), dev)
+            outs = [Act(A, 256 * i, 256) for i in range(4)]
+            fl = 2.0 * a.batch * 32 * 32 * (1 + 9 + 9 + 9) * 512 * 256
+
+            class _Aspp:
+                def __init__(s2, units, outs):
+                    s2.units, s2.outs = units, outs
+            setups.append((name, eng, _Aspp(units, outs), Act(xs), Act(A), fl))
+            continue
         kind, cin, cout, k, d, hw = LAYERS[name]
         if kind == "conv":
             conv = LY.Conv2d(cin, cout, k, 1, d * (k // 2), d, bias=False).to(dev)
@@ -74,8 +91,13 @@ def main():
              L.lib.zp_conv_tuning(10, wd)
              f = (f0, mb, sm, wd)
              for name, eng, unit, x, y, fl in setups:
+                def run1():
+                    if hasattr(unit, "outs"):
+                        eng.aspp_branches_fwd(unit.units, x, unit.outs, None)
+                    else:
+                        eng.unit_fwd(unit, x, y, None)
                 for _ in range(2):
-                    eng.unit_fwd(unit, x, y, None)
+                    run1()
                 torch.cuda.synchronize()
                 if r == 0:  # outputs of every setting against the first one (bit-identical expected)
                     ref = first.setdefault(name, y.buf._base.clone())
@@ -85,7 +107,7 @@ def main():
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(a.iters):
-                    eng.unit_fwd(unit, x, y, None)
+                    run1()
                 e1.record()
                 torch.cuda.synchronize()
                 us = e0.elapsed_time(e1) * 1e3 / a.iters

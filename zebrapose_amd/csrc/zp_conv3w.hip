@@ -46,7 +46,9 @@ __device__ __forceinline__ void wbarrier() {
 // being stored
 // nsplit > 1 (small grids, e.g. bs = 1): blockIdx.z = sub * nsplit + K slice; the slice's raw f32
 // sums go to ws [nsub][nsplit][M][Cout] and k_splitk_epi (zp_conv3.hip) finishes them
-template <int ABL, int DM, bool HEAD>
+// SGB: the cout block's MFMAs and the previous block's flush FMAs interleaved by
+// sched_group_barrier (1 MFMA, 2 VALU, ...) instead of the compiler's own order
+template <int ABL, int DM, bool HEAD, bool SGB = false>
 __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv_taps TG, const int flags,
                                                 const zp_head_args H, float* __restrict__ ws, const int nsplit) {
   constexpr int NPL = 2;
@@ -188,7 +190,12 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
     // step which read it): one piece per cout block, after that block's correction MFMAs, so that
     // the issue cost (~60 cycles per piece beside MFMAs) is spread over the step
     DmaStep dn;
-    if (more) prep(dn);
+    prep(dn);
+    if (!more) {  // no next step: every piece's offset out of the buffers' range (the unit returns, stores nothing)
+#pragma unroll
+      for (int k = 0; k < TPW; ++k) dn.voff[k] = 0x80000000u;
+      dn.koff = 0;
+    }
     const unsigned ab = s ? abase1 : abase0, bb = s ? bbase1 : bbase0;
     uint4 bf[NPL][WP];
     uint4 af[3][NPL];  // weight fragments: a 3-slot ring
@@ -230,10 +237,8 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
           MT::mma(c2[j], af[i % 3][1], bf[0][j]);
         }
       }
-      if constexpr (i < DM) {
-        if (more && !abl_dma)
-          static_for<8 / DM>([&](auto q_c) { piece(std::integral_constant<int, i * (8 / DM) + decltype(q_c)::value>{}, s ^ 1, dn); });
-      }
+      if constexpr (i < DM && !abl_dma)  // (no branch: after the last step the pieces are out of range -> no-ops)
+        static_for<8 / DM>([&](auto q_c) { piece(std::integral_constant<int, i * (8 / DM) + decltype(q_c)::value>{}, s ^ 1, dn); });
 #pragma unroll
       for (int j = 0; j < WP; ++j) {
         if constexpr (!abl_mfma) MT::mma(acc[i][j], af[i % 3][0], bf[0][j]);
@@ -248,6 +253,13 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
       }
 #pragma unroll
       for (int j = 0; j < WP; ++j) c2p[j] = c2[j];
+      if constexpr (SGB && i > 0) {
+        static_for<8>([&](auto) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+          __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // 2 VALU
+        });
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+      }
       __builtin_amdgcn_sched_barrier(0);
     });
 #pragma unroll
@@ -523,6 +535,15 @@ bool conv3w_ok(const zp_conv_args& a) {
   for (int s = 0; s < a.nsub; ++s)
     if (a.sub[s].ldy % 8 != 0 || a.sub[s].cy0 % 8 != 0) return false;
   if (a.res && (a.ldr % 8 != 0 || a.cr0 % 8 != 0)) return false;
+  // several sub-problems in one launch: only with comparable K (the ConvT phases, 1 / 2 / 2 / 4 taps);
+  // the merged ASPP (1 + 9 + 9 + 9 taps) leaves its 1x1 tiles idle early -- measured 612 -> 644 us
+  // (tools/conv3_ab.py aspp): k_conv3's smaller tiles balance it
+  int tmin = 1 << 30, tmax = 0;
+  for (int s = 0; s < a.nsub; ++s) {
+    tmin = min(tmin, a.sub[s].ntaps);
+    tmax = max(tmax, a.sub[s].ntaps);
+  }
+  if (tmax > 4 * tmin) return false;
   const long blocks = (((long)a.N * a.GH * a.GW + 255) / 256) * (a.Cout / 256) * a.nsub;
   return blocks >= g_conv3w_min || conv3w_splitk(a) > 1;
 }
@@ -549,13 +570,16 @@ int conv3w_splitk(const zp_conv_args& a) {
 
 void conv3w_launch(const zp_conv_args& a, const conv_taps& tg, hipStream_t st, int fl, float* ws, int ns) {
   const dim3 grid((unsigned)(((long)a.N * a.GH * a.GW + 255) / 256), (unsigned)(a.Cout / 256), (unsigned)(a.nsub * ns));
-  // flags 262144 / 524288: the DMA pieces over the first 2 / 8 cout blocks (default: the first one)
+  // flags 262144 / 524288: the DMA pieces over the first 2 / 8 cout blocks (default: the first one);
+  // 1048576 / 2097152: DM 1 / 8 with the MFMA / flush interleave (SGB)
   const zp_head_args H{};
   if (fl & 4096) hipLaunchKernelGGL((k_conv3w<1, 1, false>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);  // diagnostic: no DMA
   else if (fl & 8192) hipLaunchKernelGGL((k_conv3w<2, 1, false>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);  // diagnostic: no MFMA
   else if (fl & 131072) hipLaunchKernelGGL((k_conv3w<3, 1, false>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);  // diagnostic: no barrier
   else if (fl & 262144) hipLaunchKernelGGL((k_conv3w<0, 2, false>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
   else if (fl & 524288) hipLaunchKernelGGL((k_conv3w<0, 8, false>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
+  else if (fl & 1048576) hipLaunchKernelGGL((k_conv3w<0, 1, false, true>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
+  else if (fl & 2097152) hipLaunchKernelGGL((k_conv3w<0, 8, false, true>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
   else hipLaunchKernelGGL((k_conv3w<0, 1, false>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
 }
 
