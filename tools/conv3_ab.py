@@ -103,7 +103,14 @@ def main():
                     ref = first.setdefault(name, y.buf._base.clone())
                     nd = int((ref != y.buf._base).sum())
                     if nd:
-                        print(f"{name} {f}: {nd} of {ref.numel()} stored halves differ from the first setting")
+                        msg = ""
+                        if a.form == "h2" and ref.dim() == 5 and ref.dtype == torch.float16:
+                            def join(b):
+                                return b[0].float() + b[1].float() / 2048.0
+                            jr, jy = join(ref), join(y.buf._base)
+                            msg = (f"; joined f32: max |diff| {float((jr - jy).abs().max()):.3e}, "
+                                   f"max |ref| {float(jr.abs().max()):.3e}")
+                        print(f"{name} {f}: {nd} of {ref.numel()} stored halves differ from the first setting{msg}")
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(a.iters):

@@ -90,6 +90,13 @@ __device__ __forceinline__ bool h2_overflow(float v) {
   const float a = __builtin_fabsf(v);
   return a >= 65520.f && a < __builtin_inff();
 }
+// Weights of the two-plane form carry a tighter bound: k_conv3w forms 2^11 * hi in fp16 (its single
+// scaled accumulator), which overflows for |w| >= 65504 / 2048 = 31.984375.  The weight packs flag
+// it (the engine falls back to SplitF32<3> as for activations; trained conv weights sit far below).
+__device__ __forceinline__ bool h2w_overflow(float v) {
+  const float a = __builtin_fabsf(v);
+  return a >= 31.984375f && a < __builtin_inff();
+}
 __device__ __forceinline__ void raise_range_flag(unsigned* flag, bool bad) {
   if (bad && flag) *flag = 1u;
 }

@@ -9,13 +9,15 @@
 // thirds of the bytes per FLOP, and halves the per-step fixed costs (barrier, first-read latency,
 // DMA issue) per FLOP.
 //
-// Numerics are k_conv3's (SplitF32<2>): every product a*b from hi*hi + (hi*lo' + lo'*hi) * 2^-11
-// on v_mfma_f32_16x16x32_f16; the two correction products of a 16 x 16 block go into a fresh
-// accumulator c2 (per block and K step), flushed into the block's accumulator by one f32 FMA
-// (acc = fma(c2, 2^-11, acc), exact scaling, round to nearest) -- the same per-step flush the
-// 8-wave k_conv3 does per half tile.  Results equal k_conv3's up to the f32 accumulation order of
-// the flushes (both flush per K step: they are bit-identical).
-//
+// Numerics (round 4, "one scaled accumulator"): every product a*b = hi*hi + (hi*lo' + lo'*hi) * 2^-11
+// on v_mfma_f32_16x16x32_f16 (SplitF32<2> operands), but the three products of a 16 x 16 block go
+// into ONE f32 accumulator on the 2^11 scale: (2^11 w_hi)*x_hi + w_hi*x_lo' + w_lo'*x_hi, with
+// 2^11 w_hi formed from the fragment by v_pk_mul_f16 (exact: an exponent shift; weights |w| < 32,
+// flagged at packing otherwise).  The epilogue folds 2^-11 into the BN scale (exact).  k_conv3 keeps
+// a separate correction accumulator flushed per K step (acc = fma(c2, 2^-11, acc): 4 VALU FMAs per
+// block and step); removing that flush took 4x the VALU work off the step and the dependency of
+// every flush on its block's MFMAs (tools/conv3_ab.py: the flush-free ablation ran 6-12% faster).
+// Both are f32 accumulations of exact products: results agree with k_conv3's to f32 rounding.
 // Tile: 8 waves = 2 (cout halves of 128) x 4 (pixel quarters of 64); a wave owns 8 x 4 blocks of
 // 16 x 16 (128 accumulator registers).  Its 8 weight fragments are streamed through a 3-deep
 // register ring, the 4 pixel fragments of both planes are held for the step: ~210 VGPRs, no spill
@@ -38,8 +40,21 @@ __device__ __forceinline__ void wbarrier() {
   asm volatile("" ::: "memory");
 }
 
+// 2^11 * x for the 8 fp16 values of a fragment (v_pk_mul_f16; exact: fp16 exponent shift, no
+// overflow for |x| < 32 -- the two-plane weight packs flag larger weights, zp_misc.hip)
+__device__ __forceinline__ uint4 scale_hi(const uint4 a) {
+  typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+  const h2v k = {(_Float16)2048.f, (_Float16)2048.f};
+  uint4 r;
+  r.x = __builtin_bit_cast(unsigned, __builtin_bit_cast(h2v, a.x) * k);
+  r.y = __builtin_bit_cast(unsigned, __builtin_bit_cast(h2v, a.y) * k);
+  r.z = __builtin_bit_cast(unsigned, __builtin_bit_cast(h2v, a.z) * k);
+  r.w = __builtin_bit_cast(unsigned, __builtin_bit_cast(h2v, a.w) * k);
+  return r;
+}
+
 // ABL: diagnostic ablations (timing only, wrong results): 1 no DMA after the prologue, 2 no MFMA, 3 no
-// barrier in the main loop
+// barrier in the main loop, 4 / 5 no weight / activation DMA after the prologue
 // DM: the next step's 8 DMA pieces are issued over the first DM cout blocks of a step (8 / DM per
 // block, after its correction MFMAs)
 // HEAD: the fused 1x1 head (zp_conv2d_head): the conv output feeds the head's MFMAs instead of
@@ -48,7 +63,16 @@ __device__ __forceinline__ void wbarrier() {
 // sums go to ws [nsub][nsplit][M][Cout] and k_splitk_epi (zp_conv3.hip) finishes them
 // SGB: the cout block's MFMAs and the previous block's flush FMAs interleaved by
 // sched_group_barrier (1 MFMA, 2 VALU, ...) instead of the compiler's own order
-template <int ABL, int DM, bool HEAD, bool SGB = false>
+// PF: L2 prefetch of the next chunk's activation rows (see prep below; measured no gain, off)
+// BF: the activation pieces of a step issued before its weight pieces
+// STR: strip staging of the activations (stride-1 convs with >= 2 tap columns, conv3w_strip_ok):
+//   the input rows of a (32-channel chunk, tap row) group -- TR = 256 / GW output rows' input row
+//   plus the tap-column halo, TR x (GW + (nx - 1) dtx) pixels -- are staged ONCE per group, in
+//   1 KB pieces of 16 pixels, and the group's nx steps read their pixel fragments from it at a
+//   shift of txi * dtx pixels.  For a 3x3 conv that is a third of the activation pieces of the
+//   per-step tiles (the part of the staging that costs: tools/conv3_ab.py ablations), and a
+//   strip is issued a step and a half before its first use.
+template <int ABL, int DM, bool HEAD, bool SGB = false, bool PF = false, bool BF = false, bool STR = false>
 __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv_taps TG, const int flags,
                                                 const zp_head_args H, float* __restrict__ ws, const int nsplit) {
   constexpr int NPL = 2;
@@ -59,8 +83,12 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
   constexpr int TPW = NT / 8;                        // tiles per wave: 2 weight + 2 activation
   static_assert(2 * TPW == WC, "one DMA piece per cout block");
   using MT = MfmaTraits<f16_t>;
-  __shared__ uint4 lds[2 * UNITS * 64];
-  static_assert(2 * UNITS * 1024 <= 160 * 1024, "LDS");
+  constexpr int SPMAX = 20;              // STR: strip pieces per plane (320 pixels)
+  constexpr int APL = STR ? NTW : NT;    // units per plane of a stage of the per-step ring
+  constexpr int ASTG = NPL * APL;        // units per stage of the per-step ring (STR: weights only)
+  constexpr int LDSU = STR ? 2 * ASTG + 2 * NPL * SPMAX : 2 * UNITS;
+  __shared__ uint4 lds[LDSU * 64];
+  static_assert(LDSU * 1024 <= 160 * 1024, "LDS");
   static_assert(((NPL - 1) * NT + NT - 1) * 1024 < 65536, "ds_read immediate range");
   const int tb = (int)blockIdx.z / nsplit, kz = (int)blockIdx.z - tb * nsplit;
   const zp_conv_sub& S = A.sub[tb];
@@ -111,6 +139,33 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
       uxm[k] = xm;
     }
   }
+  // STR: this wave's strip pieces P = wid + 8 k (k < 3, P < nsp; both planes): lane (lr, lk) loads
+  // strip pixel s = 16 P + lr = r * SW + c (output row r of the tile, input column c + tx0) at the
+  // group's tap row; sym: tap rows whose input row is in the image (0: column / row outside)
+  int nsp = 16, SW = 0;
+  unsigned sbase[3], sym[3];
+  int sj[WP];  // the strip pixel of this lane's pixel block j at tap column 0
+  if constexpr (STR) {
+    SW = A.GW + (nx - 1) * dtx;
+    const int TR = TP / A.GW;
+    nsp = (TR * SW + 15) >> 4;
+    const int n = p0 / GHW, oy0 = (p0 - n * GHW) / A.GW;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int sp = (wid + 8 * k) * 16 + lr;
+      const int r = sp / SW, c = sp - (sp / SW) * SW;
+      const int ix = c + TG.tx0[tb], iyb = oy0 + r + TG.ty0[tb];
+      unsigned ym = 0;
+      for (int q = 0; q < ny; ++q) ym |= (unsigned)((unsigned)(iyb + q * dty) < (unsigned)A.IH) << q;
+      sym[k] = (r < TR && (unsigned)ix < (unsigned)A.IW) ? ym : 0u;
+      sbase[k] = (unsigned)(((((long)n * A.IH + iyb) * A.IW + ix) * A.ldx + A.cx0 + lk) * 2);
+    }
+#pragma unroll
+    for (int j = 0; j < WP; ++j) {
+      const int q = wp * 16 * WP + j * 16 + lr;
+      sj[j] = (q / A.GW) * SW + q % A.GW;
+    }
+  }
 #if defined(__HIP_DEVICE_COMPILE__)
   const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)A.x, (short)0, (int)TG.x_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)S.w, (short)0, (int)TG.w_bytes[tb], 0x00020000);
@@ -130,12 +185,31 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
     unsigned voff[TPW];
     int koff;
   };
+  // L2 prefetch of the next 32-channel chunk's activation rows.  Measured (flags 4194304 / 8388608:
+  // builds without the weight / the activation DMA): the weight pieces (L2-resident, read by every
+  // workgroup) cost nothing, the activation pieces 25% of the kernel -- each chunk's first tap
+  // misses L2 (~14% of the activation rows per launch, TCC counters) and the step's barrier waits
+  // for the slowest piece.  So at the first tap of chunk cb, one dword per 64-byte row of chunk
+  // cb + 1's first tap (this wave's two activation tiles x two planes = the 64 lanes) is loaded and
+  // discarded: nine steps later those rows are L2 hits.
+  unsigned pf_sink = 0;
+  const bool pf_hi = (lane >> 5) & 1;  // lane groups 0, 1 -> activation tile 2; 2, 3 -> tile 3
+  const unsigned pf_base = pf_hi ? ubase[3] : ubase[2], pf_ym = pf_hi ? uym[3] : uym[2], pf_xm = pf_hi ? uxm[3] : uxm[2];
+  const unsigned pf_plane = ((lane >> 4) & 1) ? psx_b : 0u;
   auto prep = [&](DmaStep& d) {
 #pragma unroll
     for (int k = 0; k < TPW; ++k) {
-      const bool ok = (uym[k] >> w_tyi) & (uxm[k] >> w_txi) & 1u;
+      bool ok = (uym[k] >> w_tyi) & (uxm[k] >> w_txi) & 1u;
+      if constexpr (ABL == 6) ok = ok && w_txi == 0;  // diagnostic: activation pieces at one tap column in 3
       d.voff[k] = k < 2 ? ubase[k] : (ok ? ubase[k] + (unsigned)act_off : 0x80000000u);
     }
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (PF) {  // every step (no branch, no merge that would wait for the value): out of range
+      const bool ok = w_tyi == 0 && w_txi == 0 && w_cb + 1 < CB && (pf_ym & pf_xm & 1u);  // except at chunk starts
+      const unsigned vo = ok ? pf_base + (unsigned)(act_off + 64) + pf_plane : 0x80000000u;
+      pf_sink = __builtin_amdgcn_raw_buffer_load_b32(xrsrc, vo, 0, 0);
+    }
+#endif
     d.koff = w_koff;
     w_koff += cin2;
     act_off += step_x;
@@ -152,9 +226,11 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
   };
   auto piece = [&](auto q_c, int stage, const DmaStep& d) {
     constexpr int q = decltype(q_c)::value, k = q / 2, pl = q % 2;
+    if constexpr ((ABL == 4 && k < 2) || (ABL == 5 && k >= 2)) return;  // diagnostic: no weight / activation DMA
+    if constexpr (STR && k >= 2) return;                                   // (the strips carry the activations)
     const int t = wid + 8 * k;
 #if defined(__HIP_DEVICE_COMPILE__)
-    auto* dst = (__attribute__((address_space(3))) void*)&lds[(stage * UNITS + pl * NT + t) * 64];
+    auto* dst = (__attribute__((address_space(3))) void*)&lds[(stage * ASTG + pl * APL + t) * 64];
     if constexpr (k < 2) __builtin_amdgcn_raw_ptr_buffer_load_lds(wrsrc, dst, 16, d.voff[k], pl * psw_b + d.koff, 0, 0);
     else __builtin_amdgcn_raw_ptr_buffer_load_lds(xrsrc, dst, 16, d.voff[k], pl * psx_b, 0, 0);
 #else
@@ -166,6 +242,35 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
     prep(d);
     static_for<2 * TPW>([&](auto q_c) { piece(q_c, stage, d); });
   };
+  // STR: the strip walk (next group to issue: chunk g_cb, tap row g_tyi) and its issue into strip
+  // stage gst (4 pieces per wave, 6 on the waves with a third piece)
+  int g_cb = ks0 / S.ntaps, g_tyi = 0;
+  auto strip_issue = [&](int gst) {
+    const unsigned goff = (unsigned)(g_tyi * step_y + g_cb * 64);
+    static_for<3>([&](auto k_c) {
+      constexpr int k = decltype(k_c)::value;
+      const int P = wid + 8 * k;
+      if (k < 2 || P < nsp) {
+        const unsigned vo = ((sym[k] >> g_tyi) & 1u) ? sbase[k] + goff : 0x80000000u;
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+        for (int pl = 0; pl < NPL; ++pl) {
+          auto* dst = (__attribute__((address_space(3))) void*)&lds[(2 * ASTG + (gst * NPL + pl) * SPMAX + P) * 64];
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(xrsrc, dst, 16, vo, pl * psx_b, 0, 0);
+        }
+#else
+        (void)vo;
+#endif
+      }
+    });
+    if (++g_tyi == ny) {
+      g_tyi = 0;
+      ++g_cb;
+    }
+  };
+  // STR: the step being computed reads strip stage r_gs at tap column r_txi
+  int r_txi = 0, r_gs = 0;
+  const unsigned sl0 = lds_addr(lds) + (unsigned)(2 * ASTG) * 1024u + (unsigned)(lane >> 4) * 256u;
 
   f32x4 acc[WC][WP];
 #pragma unroll
@@ -179,12 +284,12 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
   // i.e. wait for the next step's staging before computing this one.
   const unsigned l0 = lds_addr(lds) + (unsigned)lane * 16u;
   const unsigned abase0 = l0 + (unsigned)(wc * WC) * 1024u, bbase0 = l0 + (unsigned)(NTW + wp * WP) * 1024u;
-  const unsigned abase1 = abase0 + UNITS * 1024u, bbase1 = bbase0 + UNITS * 1024u;
+  const unsigned abase1 = abase0 + ASTG * 1024u, bbase1 = bbase0 + UNITS * 1024u;
   // one K step on stage buffer s: the 4 pixel fragments of both planes held for the step, the 8
   // weight fragments streamed 2 ahead; per block: c2 = hi*lo' + lo'*hi, acc += hi*hi, and the flush
   // acc = fma(c2, 2^-11, acc) one cout block later (its MFMAs have finished by then)
   constexpr bool abl_dma = ABL == 1, abl_mfma = ABL == 2, abl_bar = ABL == 3;
-  auto step = [&](auto s_c, const bool more) {
+  auto step = [&](auto s_c, const bool more, const bool strip_now) {
     constexpr int s = decltype(s_c)::value;
     // the next step's DMA (into the other buffer: every wave has passed the barrier that ended the
     // step which read it): one piece per cout block, after that block's correction MFMAs, so that
@@ -199,78 +304,82 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
     const unsigned ab = s ? abase1 : abase0, bb = s ? bbase1 : bbase0;
     uint4 bf[NPL][WP];
     uint4 af[3][NPL];  // weight fragments: a 3-slot ring
-    static_for<NPL>([&](auto p_c) {
-      constexpr int p = decltype(p_c)::value;
+    if constexpr (STR) {  // pixel fragments from the strip: 16 consecutive strip pixels, conflict-free
+      const unsigned sb = sl0 + (unsigned)r_gs * (unsigned)(NPL * SPMAX * 1024);
+      const int sh = r_txi * dtx;
       static_for<WP>([&](auto j_c) {
         constexpr int j = decltype(j_c)::value;
-        bf[p][j] = ds_read16<(p * NT + j) * 1024>(bb);
+        const int sp = sj[j] + sh;
+        const unsigned ad = sb + ((unsigned)(sp >> 4) << 10) + ((unsigned)(sp & 15) << 4);
+        static_for<NPL>([&](auto p_c) {
+          constexpr int p = decltype(p_c)::value;
+          bf[p][j] = ds_read16<p * SPMAX * 1024>(ad);
+        });
       });
-    });
+    } else {
+      static_for<NPL>([&](auto p_c) {
+        constexpr int p = decltype(p_c)::value;
+        static_for<WP>([&](auto j_c) {
+          constexpr int j = decltype(j_c)::value;
+          bf[p][j] = ds_read16<(p * NT + j) * 1024>(bb);
+        });
+      });
+    }
     static_for<2>([&](auto q_c) {
       constexpr int q = decltype(q_c)::value;
       static_for<NPL>([&](auto p_c) {
         constexpr int p = decltype(p_c)::value;
-        af[q][p] = ds_read16<(p * NT + q) * 1024>(ab);
+        af[q][p] = ds_read16<(p * APL + q) * 1024>(ab);
       });
     });
-    f32x4 c2p[WP];  // the previous cout block's correction sums (flushed one block later)
     static_for<WC>([&](auto i_c) {
       constexpr int i = decltype(i_c)::value;
       if constexpr (i + 2 < WC) {
         static_for<NPL>([&](auto p_c) {
           constexpr int p = decltype(p_c)::value;
-          af[(i + 2) % 3][p] = ds_read16<(p * NT + i + 2) * 1024>(ab);
+          af[(i + 2) % 3][p] = ds_read16<(p * APL + i + 2) * 1024>(ab);
         });
       }
       // reads issued after cout block i's: blocks i + 1 and i + 2 (two planes each)
       constexpr int after = (i + 1 < WC ? NPL : 0) + (i + 2 < WC ? NPL : 0);
       asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(after) : "memory");
       __builtin_amdgcn_sched_barrier(0);
-      f32x4 c2[WP];
+      // the three products of every block into its one accumulator, on the 2^11 scale:
+      // lo'*hi + hi*lo' + (2^11 hi)*hi (the small terms first)
+      const uint4 hs = scale_hi(af[i % 3][0]);
 #pragma unroll
-      for (int j = 0; j < WP; ++j) {
-        c2[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-        if constexpr (abl_mfma) {
-          // (the fragment reads are asm volatile: they still issue)
-        } else {
-          MT::mma(c2[j], af[i % 3][0], bf[1][j]);  // k_conv3's term order (Terms<2>): hi*lo', then lo'*hi
-          MT::mma(c2[j], af[i % 3][1], bf[0][j]);
-        }
-      }
+      for (int j = 0; j < WP; ++j)
+        if constexpr (!abl_mfma) MT::mma(acc[i][j], af[i % 3][1], bf[0][j]);
+#pragma unroll
+      for (int j = 0; j < WP; ++j)
+        if constexpr (!abl_mfma) MT::mma(acc[i][j], af[i % 3][0], bf[1][j]);
       if constexpr (i < DM && !abl_dma)  // (no branch: after the last step the pieces are out of range -> no-ops)
-        static_for<8 / DM>([&](auto q_c) { piece(std::integral_constant<int, i * (8 / DM) + decltype(q_c)::value>{}, s ^ 1, dn); });
+        static_for<8 / DM>([&](auto q_c) {
+          constexpr int q = i * (8 / DM) + decltype(q_c)::value;
+          piece(std::integral_constant<int, BF ? (q + 4) % 8 : q>{}, s ^ 1, dn);
+        });
+      if constexpr (STR && i == 1 && !abl_dma) {
+        if (strip_now) strip_issue(r_gs ^ 1);
+      }
 #pragma unroll
       for (int j = 0; j < WP; ++j) {
-        if constexpr (!abl_mfma) MT::mma(acc[i][j], af[i % 3][0], bf[0][j]);
+        if constexpr (!abl_mfma) MT::mma(acc[i][j], hs, bf[0][j]);
+        else asm volatile("" ::"v"(hs.x), "v"(hs.y), "v"(hs.z), "v"(hs.w));
       }
-      if constexpr (i > 0) {
-#pragma unroll
-        for (int j = 0; j < WP; ++j) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc[i - 1][j][r] = __builtin_fmaf(c2p[j][r], SplitF32<2>::CS, acc[i - 1][j][r]);
-          asm volatile("" : "+v"(acc[i - 1][j]));  // pinned here: sunk into the next step, every
-        }                                            // block's c2 would stay live (333 spilled VGPRs)
-      }
-#pragma unroll
-      for (int j = 0; j < WP; ++j) c2p[j] = c2[j];
-      if constexpr (SGB && i > 0) {
-        static_for<8>([&](auto) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
-          __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // 2 VALU
+      if constexpr (SGB) {
+        static_for<4>([&](auto) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // 2 MFMA
+          __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);  // 1 VALU
         });
         __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
       }
       __builtin_amdgcn_sched_barrier(0);
     });
-#pragma unroll
-    for (int j = 0; j < WP; ++j) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) acc[WC - 1][j][r] = __builtin_fmaf(c2p[j][r], SplitF32<2>::CS, acc[WC - 1][j][r]);
-    }
   };
 
-  // prologue: step 0's DMA into buffer 0
+  // prologue: step 0's DMA into buffer 0 (STR: and group 0's strip into strip stage 0)
   issue(0);
+  if constexpr (STR) strip_issue(0);
   vm_wait<0>();
   wbarrier();
   __builtin_amdgcn_sched_barrier(0);
@@ -279,17 +388,30 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
   if (flags & 65536) {  // static priority for the second-dispatched half (MI355X_MICROARCH.md item 4)
     if (wid >= 4) __builtin_amdgcn_s_setprio(1);
   }
+  // STR: a step that issued the next group's strip waits for its own per-step pieces only (issued
+  // before the strip's 4 .. 6: vmcnt counts in order); the strip lands by the next step's full wait
+  auto end_step = [&](const bool sn) {
+    if (STR && sn) vm_wait<4>();
+    else vm_wait<0>();
+    asm volatile("" ::"v"(pf_sink));  // the prefetch's (discarded) value: consumed after the wait
+    if constexpr (!abl_bar) wbarrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (STR) {
+      if (++r_txi == nx) {
+        r_txi = 0;
+        r_gs ^= 1;
+      }
+    }
+  };
   for (int ks = 0; ks < nK; ks += 2) {
     // step ks on buffer 0, issuing the DMA of step ks + 1 into buffer 1
-    step(I0{}, ks + 1 < nK);
-    vm_wait<0>();
-    if constexpr (!abl_bar) wbarrier();
-    __builtin_amdgcn_sched_barrier(0);
+    const bool sn0 = STR && r_txi == 0 && g_cb < CB;
+    step(I0{}, ks + 1 < nK, sn0);
+    end_step(sn0);
     if (ks + 1 >= nK) break;
-    step(I1{}, ks + 2 < nK);
-    vm_wait<0>();
-    if constexpr (!abl_bar) wbarrier();
-    __builtin_amdgcn_sched_barrier(0);
+    const bool sn1 = STR && r_txi == 0 && g_cb < CB;
+    step(I1{}, ks + 2 < nK, sn1);
+    end_step(sn1);
   }
 
   if (!HEAD && nsplit > 1) {  // split-K slice: raw f32 sums (acc[i][j] = 4 channels x one grid point)
@@ -301,7 +423,9 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
 #pragma unroll
       for (int i = 0; i < WC; ++i) {
         const int cf = c0 + wc * 16 * WC + i * 16 + (lane >> 4) * 4;
-        *(float4*)(wsl + (size_t)p * A.Cout + cf) = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+        constexpr float cs = SplitF32<2>::CS;  // (the accumulators are on the 2^11 scale)
+        *(float4*)(wsl + (size_t)p * A.Cout + cf) =
+            make_float4(acc[i][j][0] * cs, acc[i][j][1] * cs, acc[i][j][2] * cs, acc[i][j][3] * cs);
       }
     }
     return;
@@ -388,6 +512,8 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
         sh[0] = s0.x; sh[1] = s0.y; sh[2] = s0.z; sh[3] = s0.w;
         sh[4] = s1.x; sh[5] = s1.y; sh[6] = s1.z; sh[7] = s1.w;
       }
+#pragma unroll
+      for (int r = 0; r < 8; ++r) sc[r] *= SplitF32<2>::CS;  // the accumulators are on the 2^11 scale (exact)
     };
     if constexpr (!HEAD) load_bn();
     // HEAD: the head weights of these 32 channels in the lanes' channel order (lane group g holds
@@ -568,6 +694,16 @@ int conv3w_splitk(const zp_conv_args& a) {
   return ns;
 }
 
+// the strip staging (STR): one sub-problem of stride 1 with >= 2 tap columns, tiles of whole output
+// rows (GW a multiple of 16 dividing 256, whole tiles per image) and a strip of <= 320 pixels
+// (flag 268435456: off, for A/B)
+static bool conv3w_strip_ok(const zp_conv_args& a, const conv_taps& tg, int fl, int ns) {
+  if ((fl & 268435456) || ns != 1 || a.nsub != 1 || a.sx != 1 || a.sy != 1 || tg.nx[0] < 2 || tg.dtx[0] < 1) return false;
+  if (a.GW % 16 != 0 || 256 % a.GW != 0 || ((long)a.GH * a.GW) % 256 != 0) return false;
+  if (a.sub[0].ntaps != tg.ny[0] * tg.nx[0]) return false;
+  return (256 / a.GW) * (a.GW + (tg.nx[0] - 1) * tg.dtx[0]) <= 320;
+}
+
 void conv3w_launch(const zp_conv_args& a, const conv_taps& tg, hipStream_t st, int fl, float* ws, int ns) {
   const dim3 grid((unsigned)(((long)a.N * a.GH * a.GW + 255) / 256), (unsigned)(a.Cout / 256), (unsigned)(a.nsub * ns));
   // flags 262144 / 524288: the DMA pieces over the first 2 / 8 cout blocks (default: the first one);
@@ -576,16 +712,25 @@ void conv3w_launch(const zp_conv_args& a, const conv_taps& tg, hipStream_t st, i
   if (fl & 4096) hipLaunchKernelGGL((k_conv3w<1, 1, false>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);  // diagnostic: no DMA
   else if (fl & 8192) hipLaunchKernelGGL((k_conv3w<2, 1, false>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);  // diagnostic: no MFMA
   else if (fl & 131072) hipLaunchKernelGGL((k_conv3w<3, 1, false>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);  // diagnostic: no barrier
+  else if (fl & 4194304) hipLaunchKernelGGL((k_conv3w<4, 1, false>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);  // diagnostic: no weight DMA
+  else if (fl & 8388608) hipLaunchKernelGGL((k_conv3w<5, 1, false>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);  // diagnostic: no activation DMA
   else if (fl & 262144) hipLaunchKernelGGL((k_conv3w<0, 2, false>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
   else if (fl & 524288) hipLaunchKernelGGL((k_conv3w<0, 8, false>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
   else if (fl & 1048576) hipLaunchKernelGGL((k_conv3w<0, 1, false, true>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
   else if (fl & 2097152) hipLaunchKernelGGL((k_conv3w<0, 8, false, true>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
+  else if (fl & 16777216) hipLaunchKernelGGL((k_conv3w<0, 1, false, false, true>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);  // L2 prefetch
+  else if (fl & 33554432) hipLaunchKernelGGL((k_conv3w<0, 1, false, false, false, true>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);  // activations first
+  else if (fl & 67108864) hipLaunchKernelGGL((k_conv3w<6, 1, false, false, false>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);  // diagnostic: 1/3 of the activation pieces
+  else if (conv3w_strip_ok(a, tg, fl, ns))
+    hipLaunchKernelGGL((k_conv3w<0, 1, false, false, false, false, true>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
   else hipLaunchKernelGGL((k_conv3w<0, 1, false>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
 }
 
 void conv3w_head_launch(const zp_conv_args& a, const conv_taps& tg, const zp_head_args& h, hipStream_t st, int fl) {
   const dim3 grid((unsigned)(((long)a.N * a.GH * a.GW + 255) / 256), 1u, 1u);
-  hipLaunchKernelGGL((k_conv3w<0, 1, true>), grid, dim3(512), 0, st, a, tg, fl, h, nullptr, 1);
+  if (conv3w_strip_ok(a, tg, fl, 1))
+    hipLaunchKernelGGL((k_conv3w<0, 1, true, false, false, false, true>), grid, dim3(512), 0, st, a, tg, fl, h, nullptr, 1);
+  else hipLaunchKernelGGL((k_conv3w<0, 1, true>), grid, dim3(512), 0, st, a, tg, fl, h, nullptr, 1);
 }
 
 }  // namespace zp

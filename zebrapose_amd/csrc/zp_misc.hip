@@ -114,7 +114,7 @@ __global__ void k_pack_split(const PackArgs a, unsigned* rflag) {
     }
     unsigned short q[NPL];
     SplitF32<NPL>::split(v, q);
-    if constexpr (NPL == 2) bad |= h2_overflow(v);
+    if constexpr (NPL == 2) bad |= h2w_overflow(v);
 #pragma unroll
     for (int p = 0; p < NPL; ++p) d[e + p * total] = q[p];
   }
@@ -137,7 +137,7 @@ __device__ __forceinline__ void pack_store(const zp_pack_job& a, int d, float v,
     unsigned short q[2];
     SplitF32<2>::split(v, q);
     for (int p = 0; p < 2; ++p) ((unsigned short*)a.dst)[d + p * ps] = q[p];
-    raise_range_flag(rflag, h2_overflow(v));
+    raise_range_flag(rflag, h2w_overflow(v));
   } else if (a.dtype == ZP_BF16) ((bf16_t*)a.dst)[d] = f2bf(v);
   else if (a.dtype == ZP_F16) ((f16_t*)a.dst)[d] = (f16_t)v;
   else ((float*)a.dst)[d] = v;
