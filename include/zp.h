@@ -68,9 +68,10 @@ extern "C" {
 #define ZP_F32H2 4
 
 /* Range guard of ZP_F32H2.  A finite value at or above 65520 in magnitude has no two-plane form
- * (hi rounds to fp16 infinity).  Every ZP_F32H2 store -- the zp_conv2d epilogues (split-K's
- * included), zp_im2col_split, the f32 stem writing ZP_OUT_NHWC_H2 and zp_pack_weight(_multi) --
- * sets *flag = 1 (a device word) when it meets one; nothing clears it.  The flag is per device
+ * (hi rounds to fp16 infinity); a WEIGHT at or above 32 (65504 / 2^11) has none for the wide-tile
+ * conv, which forms 2^11 * hi in fp16.  Every ZP_F32H2 store -- the zp_conv2d epilogues (split-K's
+ * included), zp_im2col_split, the f32 stem writing ZP_OUT_NHWC_H2 and zp_pack_weight(_multi), the
+ * latter with the weight bound -- sets *flag = 1 (a device word) when it meets one; nothing clears it.  The flag is per device
  * (the calling thread's current device at registration; launches read it at enqueue time, so a
  * captured hipGraph keeps the word of its capture).  NULL unregisters.  The max / average pools and
  * broadcasts of split tensors cannot leave the range of their inputs and do not check.  The Python

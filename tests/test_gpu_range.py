@@ -12,7 +12,10 @@ by 1e5 (the stem's im2col) -- and require:
   * with the guard off, the two-plane forward of the same state is wrong by more than 1% of the
     logit scale -- silently, since a ReLU maps the NaN an infinity becomes to 0 (the guard is what
     fixes it);
-  * values below fp16's normal range (activations ~1e-7) need no fallback and stay within 1e-3.
+  * values below fp16's normal range (activations ~1e-7) need no fallback and stay within 1e-3;
+  * weights at or above 32 in magnitude (k_conv3w forms 2^11 * hi in fp16: zp_common.h
+    h2w_overflow) raise the flag at packing, with the activations kept in range (the next BN's
+    running statistics scaled to match).
 """
 import numpy as np
 import pytest
@@ -142,3 +145,20 @@ def test_tiny_activations_need_no_fallback(golden):
         m, c = net(torch.from_numpy(x).cuda())
     assert net.net.range_fallbacks == 0 and net.net.eval_engine().split == "h2"
     _close((m, c), _oracle(sd, x), "eager tiny x_high")
+
+
+def test_weights_above_32_fall_back(golden):
+    """A decoder 3x3 conv's weights x1000 (max ~146: fine for fp16, not for k_conv3w's 2^11 * hi),
+    its BN's running mean / variance x1000 / x1e6 so that the activations stay as they were."""
+    def mutate(sd):
+        sd["net.aspp.upsample_1.3.weight"].mul_(1e3)
+        sd["net.aspp.upsample_1.4.running_mean"].mul_(1e3)
+        sd["net.aspp.upsample_1.4.running_var"].mul_(1e6)
+    net, sd = _net(golden, mutate)
+    assert float(sd["net.aspp.upsample_1.3.weight"].abs().max()) > 32
+    x = golden("r34_fwd64.npz")["fwd64_x"]
+    with pytest.warns(RuntimeWarning, match="fp16's range"):
+        with torch.no_grad():
+            m, c = net(torch.from_numpy(x).cuda())
+    assert net.net.range_fallbacks == 1 and net.net.f32_split == "x3"
+    _close((m, c), _oracle(sd, x), "eager weights >= 32")

@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--form", default="x3", choices=["x3", "h2"])
     ap.add_argument("--minblocks", default="256", help="zp_conv_tuning key 8 values to A/B (comma list)")
     ap.add_argument("--wide", default="-1", help="zp_conv_tuning key 10 values to A/B (k_conv3w: 0 off, 1 on)")
+    ap.add_argument("--splitk", default="1", help="zp_conv_tuning key 12 values to A/B (k_conv3w split-K: 0, 1, 2)")
     a = ap.parse_args()
     from zebrapose_amd import _lib as L
     from zebrapose_amd.engine import Engine, Unit, Act
@@ -79,18 +80,18 @@ def main():
     mbs = [int(m) for m in a.minblocks.split(",")]
     strips = [int(m) for m in a.strip.split(",")]
     wides = [int(m) for m in a.wide.split(",")]
+    sks = [int(m) for m in a.splitk.split(",")]
     first = {}
+    import itertools
     for r in range(a.rounds):
-        for f0 in flags:
-          for mb in mbs:
-           for sm in strips:
-            for wd in wides:
-             L.lib.zp_conv_tuning(1, f0)
-             L.lib.zp_conv_tuning(8, mb)
-             L.lib.zp_conv_tuning(7, sm)
-             L.lib.zp_conv_tuning(10, wd)
-             f = (f0, mb, sm, wd)
-             for name, eng, unit, x, y, fl in setups:
+        for f0, mb, sm, wd, sk in itertools.product(flags, mbs, strips, wides, sks):
+            L.lib.zp_conv_tuning(1, f0)
+            L.lib.zp_conv_tuning(8, mb)
+            L.lib.zp_conv_tuning(7, sm)
+            L.lib.zp_conv_tuning(10, wd)
+            L.lib.zp_conv_tuning(12, sk)
+            f = (f0, mb, sm, wd, sk)
+            for name, eng, unit, x, y, fl in setups:
                 def run1():
                     if hasattr(unit, "outs"):
                         eng.aspp_branches_fwd(unit.units, x, unit.outs, None)
@@ -123,10 +124,11 @@ def main():
     L.lib.zp_conv_tuning(8, 256)
     L.lib.zp_conv_tuning(7, -1)
     L.lib.zp_conv_tuning(10, -1)
+    L.lib.zp_conv_tuning(12, 1)
     for (name, f), v in sorted(res.items()):
         fl = [s[5] for s in setups if s[0] == name][0]
         us = min(v)
-        print(f"{name:8s} flags {f[0]:6d} minblocks {f[1]:4d} strip {f[2]:2d} wide {f[3]:2d}: {us:9.1f} us  {fl / us * 1e-6:7.1f} TFLOP/s  ({fl / us * 1e-6 / (2516.6 / (6 if a.form == 'x3' else 3)):.3f} of the {a.form} ceiling)")
+        print(f"{name:8s} flags {f[0]:6d} minblocks {f[1]:4d} strip {f[2]:2d} wide {f[3]:2d} splitk {f[4]}: {us:9.1f} us  {fl / us * 1e-6:7.1f} TFLOP/s  ({fl / us * 1e-6 / (2516.6 / (6 if a.form == 'x3' else 3)):.3f} of the {a.form} ceiling)")
 
 
 if __name__ == "__main__":

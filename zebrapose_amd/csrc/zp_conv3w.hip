@@ -72,7 +72,10 @@ __device__ __forceinline__ uint4 scale_hi(const uint4 a) {
 //   shift of txi * dtx pixels.  For a 3x3 conv that is a third of the activation pieces of the
 //   per-step tiles (the part of the staging that costs: tools/conv3_ab.py ablations), and a
 //   strip is issued a step and a half before its first use.
-template <int ABL, int DM, bool HEAD, bool SGB = false, bool PF = false, bool BF = false, bool STR = false>
+// SA: one scaled accumulator per block (see the numerics note above); SA = false: k_conv3's
+//   correction accumulator c2, flushed one cout block later (acc = fma(c2, 2^-11, acc))
+template <int ABL, int DM, bool HEAD, bool SGB = false, bool PF = false, bool BF = false, bool STR = false,
+          bool SA = true>
 __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv_taps TG, const int flags,
                                                 const zp_head_args H, float* __restrict__ ws, const int nsplit) {
   constexpr int NPL = 2;
@@ -109,8 +112,10 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
   const int CB = A.Cin / 32;
   const int ny = TG.ny[tb], nx = TG.nx[tb], dty = TG.dty[tb], dtx = TG.dtx[tb];
   const int nK_all = S.ntaps * CB;
-  const int ks0 = (int)((long)kz * nK_all / nsplit);
-  const int nK = (int)((long)(kz + 1) * nK_all / nsplit) - ks0;  // this slice's K steps
+  // this slice's K steps [ks0, ks0 + nK) (STR: whole groups of nx steps)
+  const int kq = STR ? nx : 1, nq = nK_all / kq;
+  const int ks0 = (int)((long)kz * nq / nsplit) * kq;
+  const int nK = (int)((long)(kz + 1) * nq / nsplit) * kq - ks0;
   const int lr = lane & 15, lk = (lane >> 4) * 8;
   const unsigned psx_b = (unsigned)((long)A.N * A.IH * A.IW * A.ldx * 2);
   const unsigned psw_b = (unsigned)((long)A.w_rows * A.k_pad * 2);
@@ -244,7 +249,7 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
   };
   // STR: the strip walk (next group to issue: chunk g_cb, tap row g_tyi) and its issue into strip
   // stage gst (4 pieces per wave, 6 on the waves with a third piece)
-  int g_cb = ks0 / S.ntaps, g_tyi = 0;
+  int g_cb = ks0 / S.ntaps, g_tyi = (ks0 - (ks0 / S.ntaps) * S.ntaps) / nx;
   auto strip_issue = [&](int gst) {
     const unsigned goff = (unsigned)(g_tyi * step_y + g_cb * 64);
     static_for<3>([&](auto k_c) {
@@ -332,6 +337,7 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
         af[q][p] = ds_read16<(p * APL + q) * 1024>(ab);
       });
     });
+    f32x4 c2p[WP];  // !SA: the previous cout block's correction sums (flushed one block later)
     static_for<WC>([&](auto i_c) {
       constexpr int i = decltype(i_c)::value;
       if constexpr (i + 2 < WC) {
@@ -344,15 +350,28 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
       constexpr int after = (i + 1 < WC ? NPL : 0) + (i + 2 < WC ? NPL : 0);
       asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(after) : "memory");
       __builtin_amdgcn_sched_barrier(0);
-      // the three products of every block into its one accumulator, on the 2^11 scale:
-      // lo'*hi + hi*lo' + (2^11 hi)*hi (the small terms first)
-      const uint4 hs = scale_hi(af[i % 3][0]);
+      // SA: the three products of every block into its one accumulator, on the 2^11 scale:
+      // lo'*hi + hi*lo' + (2^11 hi)*hi (the small terms first).  !SA: the corrections into a fresh
+      // c2 (k_conv3's term order, Terms<2>: hi*lo', then lo'*hi), hi*hi into acc.
+      f32x4 c2[WP];
+      uint4 hs;
+      if constexpr (SA) hs = scale_hi(af[i % 3][0]);
 #pragma unroll
-      for (int j = 0; j < WP; ++j)
-        if constexpr (!abl_mfma) MT::mma(acc[i][j], af[i % 3][1], bf[0][j]);
+      for (int j = 0; j < WP; ++j) {
+        if constexpr (abl_mfma) {
+          // (the fragment reads are asm volatile: they still issue)
+        } else if constexpr (SA) {
+          MT::mma(acc[i][j], af[i % 3][1], bf[0][j]);
+        } else {
+          c2[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+          MT::mma(c2[j], af[i % 3][0], bf[1][j]);
+          MT::mma(c2[j], af[i % 3][1], bf[0][j]);
+        }
+      }
+      if constexpr (SA && !abl_mfma) {
 #pragma unroll
-      for (int j = 0; j < WP; ++j)
-        if constexpr (!abl_mfma) MT::mma(acc[i][j], af[i % 3][0], bf[1][j]);
+        for (int j = 0; j < WP; ++j) MT::mma(acc[i][j], af[i % 3][0], bf[1][j]);
+      }
       if constexpr (i < DM && !abl_dma)  // (no branch: after the last step the pieces are out of range -> no-ops)
         static_for<8 / DM>([&](auto q_c) {
           constexpr int q = i * (8 / DM) + decltype(q_c)::value;
@@ -363,8 +382,25 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
       }
 #pragma unroll
       for (int j = 0; j < WP; ++j) {
-        if constexpr (!abl_mfma) MT::mma(acc[i][j], hs, bf[0][j]);
-        else asm volatile("" ::"v"(hs.x), "v"(hs.y), "v"(hs.z), "v"(hs.w));
+        if constexpr (abl_mfma) {
+          if constexpr (SA) asm volatile("" ::"v"(hs.x), "v"(hs.y), "v"(hs.z), "v"(hs.w));
+        } else if constexpr (SA) {
+          MT::mma(acc[i][j], hs, bf[0][j]);
+        } else {
+          MT::mma(acc[i][j], af[i % 3][0], bf[0][j]);
+        }
+      }
+      if constexpr (!SA && i > 0) {
+#pragma unroll
+        for (int j = 0; j < WP; ++j) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i - 1][j][r] = __builtin_fmaf(c2p[j][r], SplitF32<2>::CS, acc[i - 1][j][r]);
+          asm volatile("" : "+v"(acc[i - 1][j]));  // pinned here: sunk into the next step, every
+        }                                            // block's c2 would stay live (333 spilled VGPRs)
+      }
+      if constexpr (!SA) {
+#pragma unroll
+        for (int j = 0; j < WP; ++j) c2p[j] = c2[j];
       }
       if constexpr (SGB) {
         static_for<4>([&](auto) {
@@ -375,6 +411,12 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
       }
       __builtin_amdgcn_sched_barrier(0);
     });
+    if constexpr (!SA) {
+#pragma unroll
+      for (int j = 0; j < WP; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[WC - 1][j][r] = __builtin_fmaf(c2p[j][r], SplitF32<2>::CS, acc[WC - 1][j][r]);
+    }
   };
 
   // prologue: step 0's DMA into buffer 0 (STR: and group 0's strip into strip stage 0)
@@ -405,11 +447,11 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
   };
   for (int ks = 0; ks < nK; ks += 2) {
     // step ks on buffer 0, issuing the DMA of step ks + 1 into buffer 1
-    const bool sn0 = STR && r_txi == 0 && g_cb < CB;
+    const bool sn0 = STR && r_txi == 0 && ks + nx < nK;
     step(I0{}, ks + 1 < nK, sn0);
     end_step(sn0);
     if (ks + 1 >= nK) break;
-    const bool sn1 = STR && r_txi == 0 && g_cb < CB;
+    const bool sn1 = STR && r_txi == 0 && ks + 1 + nx < nK;
     step(I1{}, ks + 2 < nK, sn1);
     end_step(sn1);
   }
@@ -423,7 +465,7 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
 #pragma unroll
       for (int i = 0; i < WC; ++i) {
         const int cf = c0 + wc * 16 * WC + i * 16 + (lane >> 4) * 4;
-        constexpr float cs = SplitF32<2>::CS;  // (the accumulators are on the 2^11 scale)
+        constexpr float cs = SA ? SplitF32<2>::CS : 1.f;  // (SA: the accumulators are on the 2^11 scale)
         *(float4*)(wsl + (size_t)p * A.Cout + cf) =
             make_float4(acc[i][j][0] * cs, acc[i][j][1] * cs, acc[i][j][2] * cs, acc[i][j][3] * cs);
       }
@@ -512,8 +554,10 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
         sh[0] = s0.x; sh[1] = s0.y; sh[2] = s0.z; sh[3] = s0.w;
         sh[4] = s1.x; sh[5] = s1.y; sh[6] = s1.z; sh[7] = s1.w;
       }
+      if constexpr (SA) {
 #pragma unroll
-      for (int r = 0; r < 8; ++r) sc[r] *= SplitF32<2>::CS;  // the accumulators are on the 2^11 scale (exact)
+        for (int r = 0; r < 8; ++r) sc[r] *= SplitF32<2>::CS;  // the accumulators are on the 2^11 scale (exact)
+      }
     };
     if constexpr (!HEAD) load_bn();
     // HEAD: the head weights of these 32 channels in the lanes' channel order (lane group g holds
@@ -676,7 +720,9 @@ bool conv3w_ok(const zp_conv_args& a) {
 
 // split-K of the wide tile (zp_conv_tuning key 12, default 1): a one-sub NHWC launch under 64 tiles
 // (bs = 1: up2's 3 x 3 at 128 x 128 is 64 tiles, layer5's 512 -> 512 32) is cut along K into up to
-// 8 slices of >= 12 steps, for 256..512 workgroups
+// 8 slices of >= 12 steps, for 256..512 workgroups; mode 2 also cuts grids under g_conv3w_min tiles
+// in two (bs = 32: layer4's 256 -> 256 at 32 x 32 is 128 tiles; measured 137 us vs k_conv3's 128:
+// not the default)
 static int g_conv3w_splitk = 1;
 int conv3w_splitk_mode(int v) {
   const int old = g_conv3w_splitk;
@@ -687,8 +733,12 @@ int conv3w_splitk(const zp_conv_args& a) {
   if (!g_conv3w_splitk || a.nsub != 1 || a.out_mode != ZP_OUT_NHWC || a.dtype != ZP_F32H2 || a.Cout % 256 != 0)
     return 1;
   const long blocks = (((long)a.N * a.GH * a.GW + 255) / 256) * (a.Cout / 256);
-  if (blocks > 64) return 1;
   const int nK = a.sub[0].ntaps * (a.Cin / 32);
+  if (blocks > 64) return (g_conv3w_splitk == 2 && blocks < g_conv3w_min && nK / 2 >= 12) ? 2 : 1;
+  // under 32 tiles even 8 slices leave CUs idle: k_conv3's smaller tiles (and its own split-K) win
+  // (bs = 1, tools/conv3_ab.py --batch 1: layer5's 8 tiles 58.6 us wide vs 45.1 us, up1's 16 tiles
+  // 59.1 vs 45.3; up2's 64 tiles 86.4 vs 87.7)
+  if (blocks < 32) return 1;
   int ns = 1;
   while (ns < 8 && blocks * ns * 2 <= 512 && nK / (ns * 2) >= 12) ns *= 2;
   return ns;
@@ -698,7 +748,7 @@ int conv3w_splitk(const zp_conv_args& a) {
 // rows (GW a multiple of 16 dividing 256, whole tiles per image) and a strip of <= 320 pixels
 // (flag 268435456: off, for A/B)
 static bool conv3w_strip_ok(const zp_conv_args& a, const conv_taps& tg, int fl, int ns) {
-  if ((fl & 268435456) || ns != 1 || a.nsub != 1 || a.sx != 1 || a.sy != 1 || tg.nx[0] < 2 || tg.dtx[0] < 1) return false;
+  if ((fl & 268435456) || a.nsub != 1 || a.sx != 1 || a.sy != 1 || tg.nx[0] < 2 || tg.dtx[0] < 1) return false;
   if (a.GW % 16 != 0 || 256 % a.GW != 0 || ((long)a.GH * a.GW) % 256 != 0) return false;
   if (a.sub[0].ntaps != tg.ny[0] * tg.nx[0]) return false;
   return (256 / a.GW) * (a.GW + (tg.nx[0] - 1) * tg.dtx[0]) <= 320;
@@ -721,7 +771,11 @@ void conv3w_launch(const zp_conv_args& a, const conv_taps& tg, hipStream_t st, i
   else if (fl & 16777216) hipLaunchKernelGGL((k_conv3w<0, 1, false, false, true>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);  // L2 prefetch
   else if (fl & 33554432) hipLaunchKernelGGL((k_conv3w<0, 1, false, false, false, true>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);  // activations first
   else if (fl & 67108864) hipLaunchKernelGGL((k_conv3w<6, 1, false, false, false>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);  // diagnostic: 1/3 of the activation pieces
-  else if (conv3w_strip_ok(a, tg, fl, ns))
+  else if (fl & 536870912) {  // the per-step correction flush (A/B)
+    if (conv3w_strip_ok(a, tg, fl, ns))
+      hipLaunchKernelGGL((k_conv3w<0, 1, false, false, false, false, true, false>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
+    else hipLaunchKernelGGL((k_conv3w<0, 1, false, false, false, false, false, false>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
+  } else if (conv3w_strip_ok(a, tg, fl, ns))
     hipLaunchKernelGGL((k_conv3w<0, 1, false, false, false, false, true>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
   else hipLaunchKernelGGL((k_conv3w<0, 1, false>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
 }

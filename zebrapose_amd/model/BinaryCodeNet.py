@@ -256,7 +256,7 @@ class DeepLabV3(nn.Module):
     def range_fallback(self):
         """Switch the eval forward to the full-range three-plane form after a range-guard hit."""
         warnings.warn("zebrapose_amd: an activation or weight of the fp32 eval forward exceeds fp16's range "
-                      "(|v| >= 65520); the two-plane split engine is replaced by the full-range x3 engine for "
+                      "(activations |v| >= 65520, weights |w| >= 32); the two-plane split engine is replaced by the full-range x3 engine for "
                       "this network", RuntimeWarning, stacklevel=3)
         self.f32_split = "x3"
         self.range_fallbacks += 1
