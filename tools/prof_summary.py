@@ -41,7 +41,7 @@ def bench_label(name):
         return f"k_conv3s<{sp[m.group(1)]},WC={m.group(2)}>"
     if "k_stem_h2" in name:  # the direct two-plane stem (zp_stem_split)
         return "k_stem_h2"
-    m = re.search(r"k_conv3w<(\d+), (\d+), (true|false)(?:, (?:true|false))?>", name)  # the 256 x 256 two-plane tile (+ fused head)
+    m = re.search(r"k_conv3w<(\d+), (\d+), (true|false)(?:, (?:true|false))*>", name)  # the 256 x 256 two-plane tile (+ fused head)
     if m:
         return "k_conv3w_head<h2>" if m.group(3) == "true" else "k_conv3w<h2>"
     m = re.search(r"k_conv3<(\d+), (\d+), (\d+), (\d+), (\d+), (true|false)>", name)

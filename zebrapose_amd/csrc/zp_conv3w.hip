@@ -40,19 +40,6 @@ __device__ __forceinline__ void wbarrier() {
   asm volatile("" ::: "memory");
 }
 
-// 2^11 * x for the 8 fp16 values of a fragment (v_pk_mul_f16; exact: fp16 exponent shift, no
-// overflow for |x| < 32 -- the two-plane weight packs flag larger weights, zp_misc.hip)
-__device__ __forceinline__ uint4 scale_hi(const uint4 a) {
-  typedef _Float16 h2v __attribute__((ext_vector_type(2)));
-  const h2v k = {(_Float16)2048.f, (_Float16)2048.f};
-  uint4 r;
-  r.x = __builtin_bit_cast(unsigned, __builtin_bit_cast(h2v, a.x) * k);
-  r.y = __builtin_bit_cast(unsigned, __builtin_bit_cast(h2v, a.y) * k);
-  r.z = __builtin_bit_cast(unsigned, __builtin_bit_cast(h2v, a.z) * k);
-  r.w = __builtin_bit_cast(unsigned, __builtin_bit_cast(h2v, a.w) * k);
-  return r;
-}
-
 // ABL: diagnostic ablations (timing only, wrong results): 1 no DMA after the prologue, 2 no MFMA, 3 no
 // barrier in the main loop, 4 / 5 no weight / activation DMA after the prologue
 // DM: the next step's 8 DMA pieces are issued over the first DM cout blocks of a step (8 / DM per

@@ -68,6 +68,19 @@ __device__ __forceinline__ uint4 ds_read16(unsigned addr) {
   return r;
 }
 
+// 2^11 * x for the 8 fp16 values of a fragment (v_pk_mul_f16; exact: fp16 exponent shift, no
+// overflow for |x| < 32 -- the two-plane weight packs flag larger weights, zp_misc.hip)
+__device__ __forceinline__ uint4 scale_hi(const uint4 a) {
+  typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+  const h2v k = {(_Float16)2048.f, (_Float16)2048.f};
+  uint4 r;
+  r.x = __builtin_bit_cast(unsigned, __builtin_bit_cast(h2v, a.x) * k);
+  r.y = __builtin_bit_cast(unsigned, __builtin_bit_cast(h2v, a.y) * k);
+  r.z = __builtin_bit_cast(unsigned, __builtin_bit_cast(h2v, a.z) * k);
+  r.w = __builtin_bit_cast(unsigned, __builtin_bit_cast(h2v, a.w) * k);
+  return r;
+}
+
 template <int N, typename F, int I = 0>
 __device__ __forceinline__ void static_for(F&& f) {
   if constexpr (I < N) {
