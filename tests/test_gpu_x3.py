@@ -161,12 +161,14 @@ def test_split_strip_kernel(gpu, geom, mode, form):
     old = L.lib.zp_conv_tuning(7, mode)
     old_mb = L.lib.zp_conv_tuning(8, 0)  # the cout tile by Cout alone
     old_sk = L.lib.zp_conv_tuning(9, 0)  # no split-K (it takes these small grids before the strip kernel)
+    old_wsk = L.lib.zp_conv_tuning(12, 0)  # nor the wide tile's (32 + tiles of 256 channels at bs 2)
     try:
         variant = _check_geom(gpu, geom, form)
     finally:
         L.lib.zp_conv_tuning(7, old)
         L.lib.zp_conv_tuning(8, old_mb)
         L.lib.zp_conv_tuning(9, old_sk)
+        L.lib.zp_conv_tuning(12, old_wsk)
     cout, H = geom[2], geom[8]
     tc = 128 if cout > 64 else 64
     strip = (mode == 2 or (mode == 1 and tc == 64)) and H * H >= 256
@@ -368,5 +370,50 @@ def test_split_k_small_batch(gpu, geom, form):
         out[mode] = joined(oa.buf).permute(0, 3, 1, 2).double().cpu()
     e1, e0 = (out[1] - ref).abs().max().item(), (out[0] - ref).abs().max().item()
     print(f"{geom} {form} bs=1: split-K max|d| {e1:.3g}, unsplit {e0:.3g}")
+    assert not torch.equal(out[1], out[0])
+    assert e1 <= 2.0 * e0 + 2.0 ** -22 * ref.abs().max().item(), (e1, e0)
+
+
+def test_wide_split_k_strip_small_batch(gpu):
+    """bs = 1, up2's 3x3 256 -> 256 at 128 x 128 (64 tiles of 256 x 256): the wide tile runs split
+    along K (zp_conv_tuning key 12, 4 slices of whole (chunk, tap row) groups: its strip staging
+    needs group-aligned slices) and k_splitk_epi finishes it.  Against float64, as accurate as the
+    launch without the wide split-K (k_conv3's tiles), and not bit-identical to it (the wide path
+    ran); the stage log names k_conv3w."""
+    from zebrapose_amd import _lib as L
+    from zebrapose_amd.engine import Engine, Unit, Act, joined
+    from zebrapose_amd.model import layers as LY
+    torch.manual_seed(7)
+    conv = LY.Conv2d(256, 256, 3, 1, 1, 1, bias=False)
+    bn = LY.BatchNorm2d(256)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.normal_(0, 0.1)
+        bn.running_mean.normal_(0, 0.1)
+        bn.running_var.uniform_(0.5, 1.5)
+    conv, bn = conv.to(gpu).eval(), bn.to(gpu).eval()
+    unit = Unit(conv, bn, relu=True)
+    H = 128
+    x = torch.randn(1, 256, H, H)
+    res = torch.randn(1, 256, H, H)
+    ref = _ref64("conv", conv, bn, x, res, True, 1, 1, 1)
+    eng = Engine(torch.nn.Module(), torch.float32, split="h2")
+    xa = Act(_split_act(x.permute(0, 2, 3, 1).contiguous(), gpu, "h2"))
+    ra = Act(_split_act(res.permute(0, 2, 3, 1).contiguous(), gpu, "h2"))
+    out, names = {}, {}
+    for mode in (1, 0):
+        old = L.lib.zp_conv_tuning(12, mode)
+        try:
+            oa = Act(eng._empty((1, H, H, 256), gpu))
+            eng.stage_log = []
+            eng.unit_fwd(unit, xa, oa, None, res=ra)
+            torch.cuda.synchronize()
+            names[mode] = [r[1] for r in eng.stage_log]
+        finally:
+            L.lib.zp_conv_tuning(12, old)
+        out[mode] = joined(oa.buf).permute(0, 3, 1, 2).double().cpu()
+    e1, e0 = (out[1] - ref).abs().max().item(), (out[0] - ref).abs().max().item()
+    print(f"wide split-K bs=1: max|d| {e1:.3g} ({names[1]}), without {e0:.3g} ({names[0]})")
+    assert names[1] == ["k_conv3w<h2>"] and names[0] != names[1]
     assert not torch.equal(out[1], out[0])
     assert e1 <= 2.0 * e0 + 2.0 ** -22 * ref.abs().max().item(), (e1, e0)
