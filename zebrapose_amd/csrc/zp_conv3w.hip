@@ -420,7 +420,7 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
   // STR: a step that issued the next group's strip waits for its own per-step pieces only (issued
   // before the strip's 4 .. 6: vmcnt counts in order); the strip lands by the next step's full wait
   auto end_step = [&](const bool sn) {
-    if (STR && sn) vm_wait<4>();
+    if (STR && sn && nx > 1) vm_wait<4>();  // (one-column groups: the strip is read at the next step)
     else vm_wait<0>();
     asm volatile("" ::"v"(pf_sink));  // the prefetch's (discarded) value: consumed after the wait
     if constexpr (!abl_bar) wbarrier();
@@ -734,14 +734,48 @@ int conv3w_splitk(const zp_conv_args& a) {
 // the strip staging (STR): one sub-problem of stride 1 with >= 2 tap columns, tiles of whole output
 // rows (GW a multiple of 16 dividing 256, whole tiles per image) and a strip of <= 320 pixels
 // (flag 268435456: off, for A/B)
+// (several sub-problems -- the ConvT phases, 1 x 1 / 1 x 2 / 2 x 1 / 2 x 2 taps over the input grid
+// -- each with its own strip geometry; one-column subs stage a halo-free strip per step)
 static bool conv3w_strip_ok(const zp_conv_args& a, const conv_taps& tg, int fl, int ns) {
-  if ((fl & 268435456) || a.nsub != 1 || a.sx != 1 || a.sy != 1 || tg.nx[0] < 2 || tg.dtx[0] < 1) return false;
+  (void)ns;
+  if ((fl & 268435456) || a.sx != 1 || a.sy != 1) return false;
   if (a.GW % 16 != 0 || 256 % a.GW != 0 || ((long)a.GH * a.GW) % 256 != 0) return false;
-  if (a.sub[0].ntaps != tg.ny[0] * tg.nx[0]) return false;
-  return (256 / a.GW) * (a.GW + (tg.nx[0] - 1) * tg.dtx[0]) <= 320;
+  int nxmax = 0;
+  for (int s = 0; s < a.nsub; ++s) {
+    if (a.sub[s].ntaps != tg.ny[s] * tg.nx[s] || (tg.nx[s] > 1 && tg.dtx[s] < 1)) return false;
+    if ((256 / a.GW) * (a.GW + (tg.nx[s] - 1) * tg.dtx[s]) > 320) return false;
+    nxmax = max(nxmax, tg.nx[s]);
+  }
+  return nxmax >= 2;
 }
 
-void conv3w_launch(const zp_conv_args& a, const conv_taps& tg, hipStream_t st, int fl, float* ws, int ns) {
+void conv3w_launch(const zp_conv_args& a0, const conv_taps& tg0, hipStream_t st, int fl, float* ws, int ns) {
+  // several sub-problems (the ConvT phases: 1 / 2 / 2 / 4 taps): dispatched longest first (the
+  // dispatcher walks blockIdx.z slowest, so the 4-tap phase's workgroups start first and the
+  // 1-tap phase's short ones fill the tail); flag 134217728 keeps the caller's order (A/B)
+  zp_conv_args a = a0;
+  conv_taps tg = tg0;
+  if (a.nsub > 1 && !(fl & 134217728)) {
+    int ord[ZP_MAX_SUB];
+    for (int s = 0; s < a.nsub; ++s) ord[s] = s;
+    for (int i = 1; i < a.nsub; ++i)  // stable insertion sort by descending tap count
+      for (int j = i; j > 0 && a0.sub[ord[j]].ntaps > a0.sub[ord[j - 1]].ntaps; --j) {
+        const int t = ord[j];
+        ord[j] = ord[j - 1];
+        ord[j - 1] = t;
+      }
+    for (int s = 0; s < a.nsub; ++s) {
+      const int o = ord[s];
+      a.sub[s] = a0.sub[o];
+      tg.ny[s] = tg0.ny[o];
+      tg.nx[s] = tg0.nx[o];
+      tg.ty0[s] = tg0.ty0[o];
+      tg.dty[s] = tg0.dty[o];
+      tg.tx0[s] = tg0.tx0[o];
+      tg.dtx[s] = tg0.dtx[o];
+      tg.w_bytes[s] = tg0.w_bytes[o];
+    }
+  }
   const dim3 grid((unsigned)(((long)a.N * a.GH * a.GW + 255) / 256), (unsigned)(a.Cout / 256), (unsigned)(a.nsub * ns));
   // flags 262144 / 524288: the DMA pieces over the first 2 / 8 cout blocks (default: the first one);
   // 1048576 / 2097152: DM 1 / 8 with the MFMA / flush interleave (SGB)
