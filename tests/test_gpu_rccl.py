@@ -142,9 +142,10 @@ def test_rccl_world1_grad_exchange(gpu, mode):
     assert nparams == (192 if v3 else 152), nparams
     hp = res["hook_progress"]
     assert len(hp) == nparams
-    if v3:  # ASPP_v3's head runs last in the forward, first in the reverse pass
+    if v3:  # ASPP_v3's head runs last in the forward, first in the reverse pass; its first staged
+        # segment also holds the three-head split and the up blocks (measured: 19 of 71 units)
         done, total = hp["net.aspp_v3.conv_1x1_4.weight"]
-        assert done < total / 4, (done, total)
+        assert done < total / 3, (done, total)
         done, total = hp["net.resnet.resnet.0.weight"]
         assert done == total
     elif mode == "torch_ddp_staged":

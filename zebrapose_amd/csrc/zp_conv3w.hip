@@ -692,15 +692,10 @@ bool conv3w_ok(const zp_conv_args& a) {
   for (int s = 0; s < a.nsub; ++s)
     if (a.sub[s].ldy % 8 != 0 || a.sub[s].cy0 % 8 != 0) return false;
   if (a.res && (a.ldr % 8 != 0 || a.cr0 % 8 != 0)) return false;
-  // several sub-problems in one launch: only with comparable K (the ConvT phases, 1 / 2 / 2 / 4 taps);
-  // the merged ASPP (1 + 9 + 9 + 9 taps) leaves its 1x1 tiles idle early -- measured 612 -> 644 us
-  // (tools/conv3_ab.py aspp): k_conv3's smaller tiles balance it
-  int tmin = 1 << 30, tmax = 0;
-  for (int s = 0; s < a.nsub; ++s) {
-    tmin = min(tmin, a.sub[s].ntaps);
-    tmax = max(tmax, a.sub[s].ntaps);
-  }
-  if (tmax > 4 * tmin) return false;
+  // several sub-problems in one launch (ConvT phases, the merged ASPP's 1 + 9 + 9 + 9 taps): with
+  // the longest-first dispatch (conv3w_launch) the short sub-problems fill the tail -- the merged
+  // ASPP 658 -> 640 us against k_conv3's tiles (tools/conv3_ab.py aspp; in caller order it was
+  // 612 -> 644 us, and k_conv3 kept it)
   const long blocks = (((long)a.N * a.GH * a.GW + 255) / 256) * (a.Cout / 256) * a.nsub;
   return blocks >= g_conv3w_min || conv3w_splitk(a) > 1;
 }
