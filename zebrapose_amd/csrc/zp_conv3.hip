@@ -44,6 +44,88 @@ __device__ __forceinline__ void conv3_epilogue(const zp_conv_args& A, const zp_c
   }
   const long psy = (long)A.N * S.OH * S.OW * S.ldy;
   const long psr = (long)A.N * S.OH * S.OW * A.ldr;
+  // Paired form (k_conv3w's epilogue): v_permlane16_swap pairs the lane groups of cout blocks
+  // (i, i + 1) so that a lane holds 8 consecutive channels of one pixel -- 16-byte stores (and
+  // residual loads) per lane and plane instead of 8.  NHWC output with 8-aligned channel slices and
+  // Cout a multiple of 32 (a block pair is then wholly in or out of range); flag 512: the 8-byte
+  // form (A/B).
+  if constexpr (WC % 2 == 0) {
+    const bool paired = A.out_mode == ZP_OUT_NHWC && S.ldy % 8 == 0 && S.cy0 % 8 == 0 && A.Cout % 32 == 0 &&
+                        (!A.res || (A.ldr % 8 == 0 && A.cr0 % 8 == 0)) && !(flags & 512);
+    if (paired) {
+      const int g = lane >> 4;
+#pragma unroll
+      for (int i = 0; i < WC; i += 2) {
+        const int cs = c0 + wc * 16 * WC + (i + (g & 1)) * 16 + (g >> 1) * 8;  // this lane's 8 channels
+        const bool cok = c0 + wc * 16 * WC + i * 16 < A.Cout;                  // (wave-uniform)
+        float sc[8], sh[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          sc[r] = 1.f;
+          sh[r] = 0.f;
+        }
+        if (cok && S.scale) {
+          const float4 a0 = *(const float4*)(S.scale + cs), a1 = *(const float4*)(S.scale + cs + 4);
+          sc[0] = a0.x; sc[1] = a0.y; sc[2] = a0.z; sc[3] = a0.w; sc[4] = a1.x; sc[5] = a1.y; sc[6] = a1.z; sc[7] = a1.w;
+        }
+        if (cok && S.shift) {
+          const float4 a0 = *(const float4*)(S.shift + cs), a1 = *(const float4*)(S.shift + cs + 4);
+          sh[0] = a0.x; sh[1] = a0.y; sh[2] = a0.z; sh[3] = a0.w; sh[4] = a1.x; sh[5] = a1.y; sh[6] = a1.z; sh[7] = a1.w;
+        }
+#pragma unroll
+        for (int j = 0; j < WP; ++j) {
+          float v[8];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {  // all lanes active (cross-lane op)
+            const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][j][r]), __float_as_uint(acc[i + 1][j][r]),
+                                                             false, false);
+            v[r] = __uint_as_float(sw[0]);
+            v[r + 4] = __uint_as_float(sw[1]);
+          }
+          if (!pok[j] || !cok) continue;
+          const size_t pix = ((size_t)pn[j] * S.OH + poy[j]) * S.OW + pox[j];
+#pragma unroll
+          for (int r = 0; r < 8; ++r) v[r] = v[r] * sc[r] + sh[r];
+          if (A.res) {
+            const unsigned short* R = (const unsigned short*)A.res + pix * A.ldr + A.cr0 + cs;
+            uint4 rq[NPL];
+#pragma unroll
+            for (int p = 0; p < NPL; ++p) rq[p] = *(const uint4*)(R + p * psr);
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+              unsigned short q[NPL];
+#pragma unroll
+              for (int p = 0; p < NPL; ++p) {
+                const uint32_t w4[4] = {rq[p].x, rq[p].y, rq[p].z, rq[p].w};
+                q[p] = (unsigned short)(w4[r >> 1] >> ((r & 1) * 16));
+              }
+              v[r] += SP::join(q);
+            }
+          }
+          if (A.relu) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) v[r] = fmaxf(v[r], 0.f);
+          }
+          uint32_t o[NPL][4];
+#pragma unroll
+          for (int r = 0; r < 8; r += 2) {
+            unsigned short q0[NPL], q1[NPL];
+            SP::split(v[r], q0);
+            SP::split(v[r + 1], q1);
+            if constexpr (NPL == 2) bad |= h2_overflow(v[r]) || h2_overflow(v[r + 1]);
+#pragma unroll
+            for (int p = 0; p < NPL; ++p) o[p][r >> 1] = (uint32_t)q0[p] | ((uint32_t)q1[p] << 16);
+          }
+          if ((flags & 16384) && v[0] != 1.f) continue;  // diagnostic: no stores (unless a value is exactly 1)
+          unsigned short* Y = (unsigned short*)S.y + pix * S.ldy + S.cy0 + cs;
+#pragma unroll
+          for (int p = 0; p < NPL; ++p) *(uint4*)(Y + p * psy) = make_uint4(o[p][0], o[p][1], o[p][2], o[p][3]);
+        }
+      }
+      if constexpr (NPL == 2) raise_range_flag(rflag, bad);
+      return;
+    }
+  }
   const int cbase = c0 + wc * 16 * WC + (lane >> 4) * 4;
 #pragma unroll
   for (int i = 0; i < WC; ++i) {
