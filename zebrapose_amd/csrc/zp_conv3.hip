@@ -252,6 +252,58 @@ __global__ void k_splitk_epi(const zp_conv_args A, const float* __restrict__ ws,
   const int GHW = A.GH * A.GW, M = A.N * GHW, C4 = (A.Cout + 3) / 4;
   const long psy = (long)A.N * S.OH * S.OW * S.ldy;
   const long psr = (long)A.N * S.OH * S.OW * A.ldr;
+  // vector form: a thread per (grid point, 8 channels), 16-byte loads of the slices and of the
+  // residual, 16-byte stores per plane (the scalar form below stored 2 bytes per channel and plane)
+  if (A.Cout % 8 == 0 && S.ldy % 8 == 0 && S.cy0 % 8 == 0 && (!A.res || (A.ldr % 8 == 0 && A.cr0 % 8 == 0))) {
+    const int C8 = A.Cout / 8;
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < (long)M * C8; e += (long)gridDim.x * blockDim.x) {
+      const int p = (int)(e / C8), cf = (int)(e - (long)p * C8) * 8;
+      float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int z = 0; z < nsplit; ++z) {  // slice order: the scalar form's sums, bit for bit
+        const float* w = ws + ((size_t)z * M + p) * A.Cout + cf;
+        const float4 a = *(const float4*)w, b = *(const float4*)(w + 4);
+        v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+        v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+      }
+      const int n = p / GHW, rr = p - n * GHW;
+      const int gy = rr / A.GW, gx = rr - gy * A.GW;
+      const size_t pix = ((size_t)n * S.OH + gy * S.oys + S.oyo) * S.OW + gx * S.oxs + S.oxo;
+      uint4 rq[NPL];
+      if (A.res) {
+        const unsigned short* R = (const unsigned short*)A.res + pix * A.ldr + A.cr0 + cf;
+#pragma unroll
+        for (int pl = 0; pl < NPL; ++pl) rq[pl] = *(const uint4*)(R + pl * psr);
+      }
+      uint32_t o[NPL][4];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        float x = v[r] * (S.scale ? S.scale[cf + r] : 1.f) + (S.shift ? S.shift[cf + r] : 0.f);
+        if (A.res) {
+          unsigned short q[NPL];
+#pragma unroll
+          for (int pl = 0; pl < NPL; ++pl) {
+            const uint32_t w4[4] = {rq[pl].x, rq[pl].y, rq[pl].z, rq[pl].w};
+            q[pl] = (unsigned short)(w4[r >> 1] >> ((r & 1) * 16));
+          }
+          x += SP::join(q);
+        }
+        if (A.relu) x = fmaxf(x, 0.f);
+        unsigned short q[NPL];
+        SP::split(x, q);
+        if constexpr (NPL == 2) bad |= h2_overflow(x);
+#pragma unroll
+        for (int pl = 0; pl < NPL; ++pl) {
+          if (r & 1) o[pl][r >> 1] |= (uint32_t)q[pl] << 16;
+          else o[pl][r >> 1] = q[pl];
+        }
+      }
+      unsigned short* Y = (unsigned short*)S.y + pix * S.ldy + S.cy0 + cf;
+#pragma unroll
+      for (int pl = 0; pl < NPL; ++pl) *(uint4*)(Y + pl * psy) = make_uint4(o[pl][0], o[pl][1], o[pl][2], o[pl][3]);
+    }
+    if constexpr (NPL == 2) raise_range_flag(rflag, bad);
+    return;
+  }
   for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < (long)M * C4; e += (long)gridDim.x * blockDim.x) {
     const int p = (int)(e / C4), cf = (int)(e - (long)p * C4) * 4;
     float v[4] = {0.f, 0.f, 0.f, 0.f};
