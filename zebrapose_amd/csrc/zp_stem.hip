@@ -28,7 +28,7 @@ __global__ void __launch_bounds__(256) k_stem_h2(const float* __restrict__ x, in
   constexpr int NPL = 2, WC = 4, WP = 4;
   using MT = MfmaTraits<f16_t>;
   using SP = SplitF32<NPL>;
-  extern __shared__ float region[];  // [IR][IC][3] f32
+  extern __shared__ float region[];  // [IR][IC][3] f32, then the weights in fragment order
   const int TR = 256 / OW;           // output rows per tile
   const int IR = STEM_S * TR + STEM_K - STEM_S, IC = STEM_S * OW + STEM_K - STEM_S;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -38,15 +38,47 @@ __global__ void __launch_bounds__(256) k_stem_h2(const float* __restrict__ x, in
   const int n = blockIdx.x / tiles_per_img;
   const int oy0 = (blockIdx.x - n * tiles_per_img) * TR;
   const int iy0 = oy0 * STEM_S - STEM_P, ix0 = -STEM_P;
-  // stage the input region (zeros outside the image)
-  for (int e = tid; e < IR * IC; e += 256) {
-    const int r = e / IC, c = e - r * IC;
-    const int iy = iy0 + r, ix = ix0 + c;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) v = *(const float4*)(x + (((size_t)n * H + iy) * W + ix) * ldx);
-    region[e * 3 + 0] = v.x;
-    region[e * 3 + 1] = v.y;
-    region[e * 3 + 2] = v.z;
+  // the packed weights staged once per workgroup (40 KB, fragment order [ks][i][plane][lane] of
+  // uint4: every K step's reads are lane-linear ds_read_b128), loaded together with the input
+  // region; the first form read them from L1 / L2 at every K step
+  uint4* wl = (uint4*)(region + ((IR * IC * 3 + 3) & ~3));
+  // Both stagings issue all of a thread's global loads before its first LDS write (a loop of
+  // load -> write paid one memory latency per iteration: ~10 per workgroup for the region)
+  {
+    constexpr int NU = (STEM_KP / 32) * WC * NPL * 64;  // 2560 uint4 = 10 per thread
+    static_assert(NU % 256 == 0, "weight staging");
+    const long wps_ = (long)w_rows * STEM_KP;
+    uint4 wv[NU / 256];
+#pragma unroll
+    for (int m = 0; m < NU / 256; ++m) {
+      const int u = tid + 256 * m, l = u & 63, r = u >> 6;
+      const int pl = r % NPL, i = (r / NPL) % WC, ks = r / (NPL * WC);
+      wv[m] = *(const uint4*)(w + pl * wps_ + (long)(i * 16 + (l & 15)) * STEM_KP + ks * 32 + (l >> 4) * 8);
+    }
+    // the input region (zeros outside the image), 8 pixels per thread per batch
+    for (int e0 = 0; e0 < IR * IC; e0 += 8 * 256) {
+      float4 v[8];
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const int e = e0 + tid + 256 * m;
+        const int r = e / IC, c = e - r * IC;
+        const int iy = iy0 + r, ix = ix0 + c;
+        v[m] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (e < IR * IC && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+          v[m] = *(const float4*)(x + (((size_t)n * H + iy) * W + ix) * ldx);
+      }
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const int e = e0 + tid + 256 * m;
+        if (e < IR * IC) {
+          region[e * 3 + 0] = v[m].x;
+          region[e * 3 + 1] = v[m].y;
+          region[e * 3 + 2] = v[m].z;
+        }
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < NU / 256; ++m) wl[tid + 256 * m] = wv[m];
   }
   __syncthreads();
   // this lane's pixels: block j -> tile pixel wp * 64 + j * 16 + lr -> (oy - oy0, ox)
@@ -62,17 +94,15 @@ __global__ void __launch_bounds__(256) k_stem_h2(const float* __restrict__ x, in
   for (int i = 0; i < WC; ++i)
 #pragma unroll
     for (int j = 0; j < WP; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  const long wps = (long)w_rows * STEM_KP;  // weight plane stride
   bool bad = false;
-#pragma unroll 1
+#pragma unroll 1  // (fully unrolled: 256 VGPRs, 175 vs 169 us)
   for (int ks = 0; ks < STEM_KP / 32; ++ks) {
     // weight fragments (rows i * 16 + lr, k = ks * 32 + 8 g ..)
     uint4 af[WC][NPL];
 #pragma unroll
     for (int i = 0; i < WC; ++i)
 #pragma unroll
-      for (int pl = 0; pl < NPL; ++pl)
-        af[i][pl] = *(const uint4*)(w + pl * wps + (long)(i * 16 + lr) * STEM_KP + ks * 32 + g * 8);
+      for (int pl = 0; pl < NPL; ++pl) af[i][pl] = wl[((ks * WC + i) * NPL + pl) * 64 + lane];
     // the region offsets of this lane's 8 patch elements kk = ks * 32 + 8 g + e (kk >= 147: zero)
     int eo[8];
 #pragma unroll
@@ -167,8 +197,14 @@ extern "C" int zp_stem_split(const float* x, int B, int H, int W, int ldx, const
   ZP_CHECK_ARG(OW <= 256 && 256 % OW == 0 && (OH * OW) % 256 == 0, "zp_stem_split: OW %d must divide 256", OW);
   ZP_CHECK_ARG(ldy % 8 == 0 && cy0 % 8 == 0 && ldy >= cy0 + 64, "zp_stem_split: ldy / cy0");
   const int TR = 256 / OW;
-  const size_t lds = (size_t)(STEM_S * TR + STEM_K - STEM_S) * (STEM_S * OW + STEM_K - STEM_S) * 3 * sizeof(float);
-  ZP_CHECK_ARG(lds <= 64 * 1024, "zp_stem_split: region %zu B", lds);
+  const size_t reg = (size_t)(STEM_S * TR + STEM_K - STEM_S) * (STEM_S * OW + STEM_K - STEM_S) * 3;  // floats
+  const size_t lds = ((reg + 3) & ~(size_t)3) * sizeof(float) + (size_t)(STEM_KP / 32) * 4 * 2 * 64 * 16;
+  ZP_CHECK_ARG(lds <= 80 * 1024, "zp_stem_split: region + weights %zu B", lds);  // two workgroups per CU
+  static bool attr = false;
+  if (!attr) {  // dynamic LDS beyond 64 KB
+    (void)hipFuncSetAttribute((const void*)k_stem_h2, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+    attr = true;
+  }
   const long psy = (long)B * OH * OW * ldy;
   hipLaunchKernelGGL(k_stem_h2, dim3((unsigned)((long)B * OH * OW / 256)), dim3(256), lds, (hipStream_t)stream, x, H, W,
                      ldx, (const unsigned short*)w, w_rows, scale, shift, (unsigned short*)y, ldy, cy0, OH, OW, psy,
