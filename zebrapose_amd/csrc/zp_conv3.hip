@@ -819,12 +819,15 @@ struct strip3_geo {
 // with in-order vmcnt the wait at the end of a step is a constant: the loads issued after the next
 // step's weights are (WSL - 2) weight events and the strips of the group starts among the last
 // WSL - 1 steps.
-template <int NPL, int WC, int WSL = 2, int SSL = 2>
+// WP = 2 (round 4): 128-pixel tiles (a wave: 2 pixel blocks) with 144-row strips, 53 KB of LDS
+// and ~70 VGPRs, so that three workgroups share a CU: the 64-channel layers' K loops are short
+// (18 - 36 steps) and a lone workgroup's per-step latencies and epilogue stood unhidden.
+template <int NPL, int WC, int WSL = 2, int SSL = 2, int WP = 4>
 __global__ void __launch_bounds__(512) k_conv3s(const zp_conv_args A, const strip3_geo SG, const int flags) {
-  constexpr int WP = 4, NW = 8;
-  constexpr int TC = 32 * WC, TP = 256;
+  constexpr int NW = 8;
+  constexpr int TC = 32 * WC, TP = 64 * WP;
   constexpr int NTW = TC / 16;                  // weight tiles per plane
-  constexpr int SRP = (WSL > 2 || SSL > 2) ? 272 : 288;  // strip rows per plane slot (>= SR, multiple of 16)
+  constexpr int SRP = WP == 2 ? 144 : (WSL > 2 || SSL > 2) ? 272 : 288;  // strip rows per plane slot (>= SR, x16)
   constexpr int SB = SRP / 16;                  // strip row blocks per plane
   constexpr int SU = NPL * SB;                    // strip DMA units per group
   constexpr int SUW = (SU + NW - 1) / NW;       // per wave (padded with no-ops)
@@ -1210,9 +1213,19 @@ static void conv3_dispatch(const zp_conv_args& a, const conv_taps& tg, int tc, h
     if (tc == 128) {
       hipLaunchKernelGGL((k_conv3s<NPL, 4>), sgrid, dim3(512), 0, st, a, s3, fl);
     } else if constexpr (NPL == 2) {
-      if (s3.SR <= 272 && (fl & 1073741824))
+      // 128-pixel tiles (three workgroups per CU) unless flag 32 (A/B)
+      const int tr2 = 128 / s3.W;
+      if (!(fl & 32) && tr2 * s3.SW <= 144 && !(fl & 1073741824)) {
+        strip3_geo h = s3;
+        h.TR = tr2;
+        h.SR = tr2 * s3.SW;
+        const dim3 hgrid((unsigned)(((long)a.N * a.GH * a.GW) / 128), (unsigned)(a.Cout / tc), 1);
+        hipLaunchKernelGGL((k_conv3s<NPL, 2, 2, 2, 2>), hgrid, dim3(512), 0, st, a, h, fl);
+      } else if (s3.SR <= 272 && (fl & 1073741824)) {
         hipLaunchKernelGGL((k_conv3s<NPL, 2, 4, 3>), sgrid, dim3(512), 0, st, a, s3, fl);
-      else hipLaunchKernelGGL((k_conv3s<NPL, 2>), sgrid, dim3(512), 0, st, a, s3, fl);
+      } else {
+        hipLaunchKernelGGL((k_conv3s<NPL, 2>), sgrid, dim3(512), 0, st, a, s3, fl);
+      }
     } else {
       hipLaunchKernelGGL((k_conv3s<NPL, 2>), sgrid, dim3(512), 0, st, a, s3, fl);
     }
