@@ -36,7 +36,7 @@ def bench_label(name):
     if m:
         return f"k_conv_strip2<{tn[m.group(1)]},WC={m.group(2)}>"
     sp = {"3": "x3", "2": "h2"}  # split-fp32 planes -> engine label
-    m = re.search(r"k_conv3s<(\d+), (\d+)(?:, \d+)?>", name)
+    m = re.search(r"k_conv3s<(\d+), (\d+)(?:, \d+)*>", name)
     if m:
         return f"k_conv3s<{sp[m.group(1)]},WC={m.group(2)}>"
     if "k_stem_h2" in name:  # the direct two-plane stem (zp_stem_split)

@@ -1307,7 +1307,7 @@ int conv3_launch(const zp_conv_args& a, hipStream_t st, int fl, const zp_head_ar
     ZP_CHECK_ARG(tc == 256 && a.Cout == 256 && a.nsub == 1 && npl == 2,
                  "zp_conv2d_head: not a fused-head geometry (zp_conv2d_head_ok)");
     ZP_CHECK_ARG(h.w && h.mask && (h.code || h.cout == 1) && h.cout >= 1 && h.cout <= 32, "zp_conv2d_head: bad head");
-    ZP_CHECK_ARG(h.C2 >= 0 && h.C2 % 32 == 0 && h.k_pad % 8 == 0 && h.k_pad >= a.Cout + h.C2,
+    ZP_CHECK_ARG(h.C2 >= 0 && h.C2 % 32 == 0 && h.k_pad % 8 == 0 && h.k_pad >= a.Cout + h.C2 && h.k_pad <= 504,
                  "zp_conv2d_head: C2 %d / k_pad %d", h.C2, h.k_pad);
     ZP_CHECK_ARG(h.C2 == 0 || (h.x2 && h.ldx2 % 8 == 0 && h.cx20 % 8 == 0 && h.ldx2 >= h.cx20 + h.C2),
                  "zp_conv2d_head: x2 layout");

@@ -491,23 +491,45 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
   }
   // HEAD: the 1x1 head's sums (rows hb * 16 + 4 g + q, pixel block j) over this wave's channels
   f32x4 hacc[2][WP];
-  const long hps = (long)32 * H.k_pad;  // head weight plane stride (elements; rows padded to 32)
-  const unsigned short* HW = (const unsigned short*)H.w;
+  // HEAD: the head weights ([NPL][32 rows][k_pad], 40 KB at k_pad 320) staged in LDS -- free after
+  // the main loop's last barrier -- by LDS-DMA in MFMA fragment order: piece (plane, row half hb,
+  // 32-channel chunk q) holds lane l's 8 weights of row hb * 16 + (l & 15) at the channels lane
+  // group l >> 4 carries in the epilogue's paired layout (conv channels: (g & 1) * 16 + (g >> 1) * 8;
+  // the x_128 part: g * 8), so every use is a lane-linear ds_read_b128 (they were global loads, one
+  // L1 round trip each)
+  const int hnq = H.k_pad / 32;  // 32-channel chunks of a head weight row
   if constexpr (HEAD) {
 #pragma unroll
     for (int hb = 0; hb < 2; ++hb)
 #pragma unroll
       for (int j = 0; j < WP; ++j) hacc[hb][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#if defined(__HIP_DEVICE_COMPILE__)
+    const __amdgpu_buffer_rsrc_t hrsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)H.w, (short)0, NPL * 32 * H.k_pad * 2, 0x00020000);
+    const int gq = lane >> 4;
+    for (int pc = wid; pc < NPL * 2 * hnq; pc += 8) {  // (wave-uniform)
+      const int q = pc % hnq, hb = (pc / hnq) & 1, pl = pc / (2 * hnq);
+      const int koff = q * 32 + (q * 32 < A.Cout ? (gq & 1) * 16 + (gq >> 1) * 8 : gq * 8);
+      const unsigned vo = (unsigned)(((pl * 32 + hb * 16 + (lane & 15)) * H.k_pad + koff) * 2);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(hrsrc, (__attribute__((address_space(3))) void*)&lds[pc * 64], 16, vo, 0, 0, 0);
+    }
+#endif
+    vm_wait<0>();
+    __syncthreads();
   }
-  // one 32-channel K slice of the head: weight fragments wf[hb][plane] (k slot g of lane group g),
+  // one 32-channel K slice q of the head: weight fragments wf[hb][plane] (k slot g of lane group g),
   // activation fragment planes (xh, xl) of pixel block j
-  // (wofs: the element offset of this lane's 8 weights in row lr of plane 0; read per use from L1)
-  auto head_mma = [&](const long wofs, const uint4& xh, const uint4& xl, const int j) {
+  auto head_mma = [&](const int q, const uint4& xh, const uint4& xl, const int j) {
 #pragma unroll
     for (int hb = 0; hb < 2; ++hb) {
       uint4 wf[2][NPL];
-#pragma unroll
-      for (int pl = 0; pl < NPL; ++pl) wf[hb][pl] = *(const uint4*)(HW + pl * hps + (long)hb * 16 * H.k_pad + wofs);
+      // (inline-asm reads waited on here: plain LDS loads were hoisted over the pixel blocks and
+      // spilled the accumulators)
+      const unsigned ha = lds_addr(lds) + (unsigned)(((hb * hnq + q) * 64 + lane) * 16);
+      wf[hb][0] = ds_read16<0>(ha);
+      wf[hb][1] = ds_read16<0>(ha + (unsigned)(2 * hnq * 1024));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
       f32x4 c2 = (f32x4){0.f, 0.f, 0.f, 0.f};
       MT::mma(c2, wf[hb][0], xl);
       MT::mma(c2, wf[hb][1], xh);
@@ -549,7 +571,7 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
     if constexpr (!HEAD) load_bn();
     // HEAD: the head weights of these 32 channels in the lanes' channel order (lane group g holds
     // channels (g & 1) * 16 + (g >> 1) * 8 .. + 7 of the slice; the MFMA reads them as k slot g)
-    const long wofs = (long)lr * H.k_pad + cs;
+    const int hq = (wc * 16 * WC + i * 16) / 32;  // the head-weight chunk of this channel pair
 #pragma unroll
     for (int j = 0; j < WP; ++j) {
       float v[8];
@@ -604,7 +626,7 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
         for (int p = 0; p < NPL; ++p) o[p][r >> 1] = (uint32_t)q0[p] | ((uint32_t)q1[p] << 16);
       }
       if constexpr (HEAD) {  // the conv output is not stored: it feeds the head
-        head_mma(wofs, make_uint4(o[0][0], o[0][1], o[0][2], o[0][3]), make_uint4(o[1][0], o[1][1], o[1][2], o[1][3]), j);
+        head_mma(hq, make_uint4(o[0][0], o[0][1], o[0][2], o[0][3]), make_uint4(o[1][0], o[1][1], o[1][2], o[1][3]), j);
         __builtin_amdgcn_sched_barrier(0);  // one pixel block at a time (register pressure)
         continue;
       }
@@ -631,7 +653,7 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
     if (wc == 0) {
       const long psx2 = (long)A.N * S.OH * S.OW * H.ldx2;
       for (int q = 0; q < H.C2 / 32; ++q) {
-        const long wofs = (long)lr * H.k_pad + A.Cout + q * 32 + g * 8;
+        const int hq = A.Cout / 32 + q;
 #pragma unroll
         for (int j = 0; j < WP; ++j) {
           uint4 xq[NPL];
@@ -640,12 +662,12 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
           const unsigned short* X2 = (const unsigned short*)H.x2 + pix * H.ldx2 + H.cx20 + q * 32 + g * 8;
 #pragma unroll
           for (int pl = 0; pl < NPL; ++pl) xq[pl] = q2.ok ? *(const uint4*)(X2 + pl * psx2) : make_uint4(0u, 0u, 0u, 0u);
-          head_mma(wofs, xq[0], xq[1], j);
+          head_mma(hq, xq[0], xq[1], j);
         }
       }
     }
     // the two cout halves' sums meet in LDS (free: every wave passed the main loop's last barrier)
-    f32x4* red = (f32x4*)lds;  // [wp][hb][j][lane]
+    f32x4* red = (f32x4*)(lds + 4096);  // [wp][hb][j][lane], past the staged head weights (64 KB in)
     if (wc == 1) {
 #pragma unroll
       for (int hb = 0; hb < 2; ++hb)
