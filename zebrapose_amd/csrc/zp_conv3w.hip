@@ -134,11 +134,15 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
   // STR: this wave's strip pieces P = wid + 8 k (k < 3, P < nsp; both planes): lane (lr, lk) loads
   // strip pixel s = 16 P + lr = r * SW + c (output row r of the tile, input column c + tx0) at the
   // group's tap row; sym: tap rows whose input row is in the image (0: column / row outside)
-  int nsp = 16, SW = 0;
+  int nsp = 16, SW = 0, sh0 = 0;
   unsigned sbase[3], sym[3];
-  int sj[WP];  // the strip pixel of this lane's pixel block j at tap column 0
+  int sj[WP];  // the strip pixel of this lane's pixel block j at the strip's first column
   if constexpr (STR) {
-    SW = A.GW + (nx - 1) * dtx;
+    // the strip's columns start at the leftmost tap column (the ConvT phases list theirs right to
+    // left: dtx = -1); tap column txi reads at a shift of sh0 + txi * dtx pixels
+    const int sx0 = min(TG.tx0[tb], TG.tx0[tb] + (nx - 1) * dtx);
+    sh0 = TG.tx0[tb] - sx0;
+    SW = A.GW + (nx - 1) * (dtx < 0 ? -dtx : dtx);
     const int TR = TP / A.GW;
     nsp = (TR * SW + 15) >> 4;
     const int n = p0 / GHW, oy0 = (p0 - n * GHW) / A.GW;
@@ -146,7 +150,7 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
     for (int k = 0; k < 3; ++k) {
       const int sp = (wid + 8 * k) * 16 + lr;
       const int r = sp / SW, c = sp - (sp / SW) * SW;
-      const int ix = c + TG.tx0[tb], iyb = oy0 + r + TG.ty0[tb];
+      const int ix = c + sx0, iyb = oy0 + r + TG.ty0[tb];
       unsigned ym = 0;
       for (int q = 0; q < ny; ++q) ym |= (unsigned)((unsigned)(iyb + q * dty) < (unsigned)A.IH) << q;
       sym[k] = (r < TR && (unsigned)ix < (unsigned)A.IW) ? ym : 0u;
@@ -298,7 +302,7 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
     uint4 af[3][NPL];  // weight fragments: a 3-slot ring
     if constexpr (STR) {  // pixel fragments from the strip: 16 consecutive strip pixels, conflict-free
       const unsigned sb = sl0 + (unsigned)r_gs * (unsigned)(NPL * SPMAX * 1024);
-      const int sh = r_txi * dtx;
+      const int sh = sh0 + r_txi * dtx;
       static_for<WP>([&](auto j_c) {
         constexpr int j = decltype(j_c)::value;
         const int sp = sj[j] + sh;
@@ -769,8 +773,8 @@ static bool conv3w_strip_ok(const zp_conv_args& a, const conv_taps& tg, int fl, 
   if (a.GW % 16 != 0 || 256 % a.GW != 0 || ((long)a.GH * a.GW) % 256 != 0) return false;
   int nxmax = 0;
   for (int s = 0; s < a.nsub; ++s) {
-    if (a.sub[s].ntaps != tg.ny[s] * tg.nx[s] || (tg.nx[s] > 1 && tg.dtx[s] < 1)) return false;
-    if ((256 / a.GW) * (a.GW + (tg.nx[s] - 1) * tg.dtx[s]) > 320) return false;
+    if (a.sub[s].ntaps != tg.ny[s] * tg.nx[s] || (tg.nx[s] > 1 && tg.dtx[s] == 0)) return false;
+    if ((256 / a.GW) * (a.GW + (tg.nx[s] - 1) * abs(tg.dtx[s])) > 320) return false;
     nxmax = max(nxmax, tg.nx[s]);
   }
   return nxmax >= 2;
