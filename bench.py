@@ -798,6 +798,8 @@ def run(args):
                            "model": "BinaryCodeNet_Deeplab(34, 16, 2, concat=True)", "global_batch": world * B,
                            "per_gpu_batch": B, "input": f"{S}x{S}", "parallelism": f"replicas{world}",
                            "precision": args.precision, "launch": main["launch"],
+                           "fp32_engine": ("two-plane fp16 split fp32 (ZP_F32H2; range-guarded, full-range "
+                                           "x3 fallback)" if args.precision == "fp32" else None),
                            "correspondences_last_step": n_corr},
                 "roofline": roofline, "bf16": bf16, "bs1": bs1, "cpu_baseline": cpu, "train": train, "pnp": pnp_res,
                 "crop": crop_res, "v3": v3, "multi_object": multi}
