@@ -417,3 +417,64 @@ def test_wide_split_k_strip_small_batch(gpu):
     assert names[1] == ["k_conv3w<h2>"] and names[0] != names[1]
     assert not torch.equal(out[1], out[0])
     assert e1 <= 2.0 * e0 + 2.0 ** -22 * ref.abs().max().item(), (e1, e0)
+
+
+# schedule flags of the two-plane kernels that must not change a single stored bit (zp_conv_tuning
+# key 1 = ZP_CONV_FLAGS; 478 = the default set): 268435456 no strip staging (k_conv3w), 134217728
+# caller's sub-problem order instead of longest first, 1 plain instead of non-temporal stores, 512
+# the 8-byte epilogue (k_conv3 / k_conv3s), 32 the 256-pixel k_conv3s tile
+_BITWISE_FLAGS = [268435456, 134217728, 1, 512, 32]
+
+
+@pytest.mark.parametrize("geom,B,kernel",
+                         [(("conv", 256, 256, 3, 1, 1, 1, False, 64), 16, "k_conv3w<h2>"),    # strips
+                          (("convT", 256, 256, 3, 2, 1, 1, False, 32), 16, "k_conv3w<h2>"),   # 4 phases
+                          (("conv", 64, 64, 3, 1, 1, 1, False, 64), 8, "k_conv3s<h2,WC=2>"),  # WP = 2
+                          (("conv", 256, 256, 3, 1, 2, 2, False, 32), 32, "k_conv3<h2,WC=4,NWP=4>")],
+                         ids=["wide3x3", "wideConvT", "strip64", "conv3_layer4"])
+def test_schedule_flags_are_bit_identical(gpu, geom, B, kernel):
+    """Round-4 schedule choices (strip staging of the wide tile, longest-first phase order, nt
+    stores, the paired 16-byte epilogue, the 128-pixel strip tile) change the data movement only:
+    with each switched back, the stored two-plane outputs are bit-identical (residual on for the
+    convs)."""
+    from zebrapose_amd import _lib as L
+    from zebrapose_amd.engine import Engine, Unit, Act
+    from zebrapose_amd.model import layers as LY
+    kind, cin, cout, k, s, p, d, bias, H = geom
+    torch.manual_seed(11)
+    if kind == "conv":
+        conv = LY.Conv2d(cin, cout, k, s, p, d, bias=bias)
+    else:
+        conv = LY.ConvTranspose2d(cin, cout, k, s, p, output_padding=1, bias=False)
+    bn = LY.BatchNorm2d(cout)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.normal_(0, 0.1)
+        bn.running_mean.normal_(0, 0.1)
+        bn.running_var.uniform_(0.5, 1.5)
+    conv, bn = conv.to(gpu).eval(), bn.to(gpu).eval()
+    unit = Unit(conv, bn, relu=True)
+    OH, OW = unit.out_hw(H, H)
+    x = torch.randn(B, cin, H, H)
+    eng = Engine(torch.nn.Module(), torch.float32, split="h2")
+    xa = Act(_split_act(x.permute(0, 2, 3, 1).contiguous(), gpu, "h2"))
+    ra = None
+    if kind == "conv":
+        res = torch.randn(B, cout, OH, OW)
+        ra = Act(_split_act(res.permute(0, 2, 3, 1).contiguous(), gpu, "h2"))
+    outs = {}
+    for extra in [0] + _BITWISE_FLAGS:
+        old = L.lib.zp_conv_tuning(1, 478 + extra)
+        try:
+            oa = Act(eng._empty((B, OH, OW, cout), gpu))
+            eng.stage_log = []
+            eng.unit_fwd(unit, xa, oa, None, res=ra)
+            torch.cuda.synchronize()
+        finally:
+            L.lib.zp_conv_tuning(1, old)
+        outs[extra] = oa.buf._base.clone()
+    names = [r[1] for r in eng.stage_log]
+    print(geom, names)
+    assert names == [kernel], names
+    for extra in _BITWISE_FLAGS:
+        assert torch.equal(outs[extra], outs[0]), (geom, extra)
