@@ -28,7 +28,10 @@ __global__ void __launch_bounds__(256) k_stem_h2(const float* __restrict__ x, in
   constexpr int NPL = 2, WC = 4, WP = 4;
   using MT = MfmaTraits<f16_t>;
   using SP = SplitF32<NPL>;
-  extern __shared__ float region[];  // [IR][IC][3] f32, then the weights in fragment order
+  // [IR][IC][3] words, each the element split into its two fp16 planes (hi | lo' << 16), then the
+  // weights in fragment order.  Splitting (and the range check) once per staged element instead of
+  // once per use: every input element feeds ~12 overlapping 7 x 7 / s2 patches.
+  extern __shared__ uint32_t region[];
   const int TR = 256 / OW;           // output rows per tile
   const int IR = STEM_S * TR + STEM_K - STEM_S, IC = STEM_S * OW + STEM_K - STEM_S;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -44,6 +47,13 @@ __global__ void __launch_bounds__(256) k_stem_h2(const float* __restrict__ x, in
   uint4* wl = (uint4*)(region + ((IR * IC * 3 + 3) & ~3));
   // Both stagings issue all of a thread's global loads before its first LDS write (a loop of
   // load -> write paid one memory latency per iteration: ~10 per workgroup for the region)
+  bool bad = false;
+  auto split_word = [&](float v) -> uint32_t {
+    unsigned short q[NPL];
+    SP::split(v, q);
+    bad |= h2_overflow(v);
+    return (uint32_t)q[0] | ((uint32_t)q[1] << 16);
+  };
   {
     constexpr int NU = (STEM_KP / 32) * WC * NPL * 64;  // 2560 uint4 = 10 per thread
     static_assert(NU % 256 == 0, "weight staging");
@@ -71,9 +81,9 @@ __global__ void __launch_bounds__(256) k_stem_h2(const float* __restrict__ x, in
       for (int m = 0; m < 8; ++m) {
         const int e = e0 + tid + 256 * m;
         if (e < IR * IC) {
-          region[e * 3 + 0] = v[m].x;
-          region[e * 3 + 1] = v[m].y;
-          region[e * 3 + 2] = v[m].z;
+          region[e * 3 + 0] = split_word(v[m].x);
+          region[e * 3 + 1] = split_word(v[m].y);
+          region[e * 3 + 2] = split_word(v[m].z);
         }
       }
     }
@@ -94,7 +104,6 @@ __global__ void __launch_bounds__(256) k_stem_h2(const float* __restrict__ x, in
   for (int i = 0; i < WC; ++i)
 #pragma unroll
     for (int j = 0; j < WP; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  bool bad = false;
 #pragma unroll 1  // (fully unrolled: 256 VGPRs, 175 vs 169 us)
   for (int ks = 0; ks < STEM_KP / 32; ++ks) {
     // weight fragments (rows i * 16 + lr, k = ks * 32 + 8 g ..)
@@ -117,14 +126,10 @@ __global__ void __launch_bounds__(256) k_stem_h2(const float* __restrict__ x, in
       uint32_t hw[NPL][4];
 #pragma unroll
       for (int e = 0; e < 8; e += 2) {
-        const float v0 = eo[e] >= 0 ? region[pbase[j] + eo[e]] : 0.f;
-        const float v1 = eo[e + 1] >= 0 ? region[pbase[j] + eo[e + 1]] : 0.f;
-        unsigned short q0[NPL], q1[NPL];
-        SP::split(v0, q0);
-        SP::split(v1, q1);
-        bad |= h2_overflow(v0) || h2_overflow(v1);
-#pragma unroll
-        for (int pl = 0; pl < NPL; ++pl) hw[pl][e >> 1] = (uint32_t)q0[pl] | ((uint32_t)q1[pl] << 16);
+        const uint32_t w0 = eo[e] >= 0 ? region[pbase[j] + eo[e]] : 0u;
+        const uint32_t w1 = eo[e + 1] >= 0 ? region[pbase[j] + eo[e + 1]] : 0u;
+        hw[0][e >> 1] = (w0 & 0xffffu) | (w1 << 16);           // the two hi halves
+        hw[1][e >> 1] = (w0 >> 16) | (w1 & 0xffff0000u);       // the two lo' halves
       }
       const uint4 bh = make_uint4(hw[0][0], hw[0][1], hw[0][2], hw[0][3]);
       const uint4 bl = make_uint4(hw[1][0], hw[1][1], hw[1][2], hw[1][3]);
