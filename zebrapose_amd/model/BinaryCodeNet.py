@@ -7,15 +7,17 @@ and loss call signatures as the reference (BinaryCodeNet.py:8-174).  The forward
 backward run in libzp (HIP kernels for gfx950) through ``zebrapose_amd.engine``; there is
 no PyTorch-op fallback.
 
-Precision: ``precision='fp32'`` (default) is the reference's own arithmetic.  Training runs every
-convolution with exact-f32 MFMA (``v_mfma_f32_16x16x4_f32``) and f32 activations; the eval forward
-runs a split-fp32 engine, chosen by ``f32_split`` (``ZP_F32_SPLIT``):
+Precision: ``precision='fp32'`` (default) is the reference's fp32 arithmetic, within its
+tolerance.  Training runs every convolution with exact-f32 MFMA (``v_mfma_f32_16x16x4_f32``) and f32
+activations; the eval forward runs a split-fp32 engine, chosen by ``f32_split`` (``ZP_F32_SPLIT``):
   "h2" / True (default): include/zp.h ZP_F32H2 -- activations and weights as two fp16 planes
       (v = hi + lo * 2^-11, 22 bits), every product from hi*hi + (hi*lo + lo*hi) * 2^-11 on fp16
-      MFMAs with f32 accumulation (3 MFMAs per f32 MAC);
+      MFMAs with f32 accumulation (3 MFMAs per f32 MAC); fp16's range is guarded (activations
+      |v| >= 65520, weights |w| >= 32 raise a device flag and the forward re-runs on "x3");
   "x3": ZP_F32X3 -- three bf16 planes summing exactly to the f32 value, six bf16 MFMA terms;
   False: exact-f32 MFMA.
-Both split forms are closer to a float64 forward than exact-f32 MFMA.  ``precision='bf16'``
+Against a float64 forward "x3" is about 2x closer than exact-f32 MFMA and "h2" about as close
+(its 256 x 256 tile keeps one f32 accumulator per product block).  ``precision='bf16'``
 uses bf16 MFMA with f32 accumulation and bf16 NHWC activations -- the throughput mode
 (configs 2-4); ``precision='fp16'`` is the same with IEEE fp16 (``v_mfma_f32_16x16x32_f16``),
 inference only (configs[4]: R50 multi-object inference).  Set per instance (``net.set_precision``) or with ``ZP_PRECISION``.
