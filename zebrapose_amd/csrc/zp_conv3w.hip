@@ -728,10 +728,13 @@ bool conv3w_ok(const zp_conv_args& a) {
   for (int s = 0; s < a.nsub; ++s)
     if (a.sub[s].ldy % 8 != 0 || a.sub[s].cy0 % 8 != 0) return false;
   if (a.res && (a.ldr % 8 != 0 || a.cr0 % 8 != 0)) return false;
-  // several sub-problems in one launch (ConvT phases, the merged ASPP's 1 + 9 + 9 + 9 taps): with
-  // the longest-first dispatch (conv3w_launch) the short sub-problems fill the tail -- the merged
-  // ASPP 658 -> 640 us against k_conv3's tiles (tools/conv3_ab.py aspp; in caller order it was
-  // 612 -> 644 us, and k_conv3 kept it)
+  // several sub-problems in one launch: the ConvT phases (1..4 taps) run here, longest first
+  // (conv3w_launch).  The merged ASPP's 1 + 9 + 9 + 9 taps stay on k_conv3's tiles: 583-593 us
+  // against 607 us wide at bs 32 (tools/conv3_ab.py aspp, profiles/r04_conv3_ab.txt round-close
+  // sweeps), with the flushed accumulator
+  if (a.nsub > 1)
+    for (int s = 0; s < a.nsub; ++s)
+      if (a.sub[s].ntaps > 4) return false;
   const long blocks = (((long)a.N * a.GH * a.GW + 255) / 256) * (a.Cout / 256) * a.nsub;
   return blocks >= g_conv3w_min || conv3w_splitk(a) > 1;
 }
