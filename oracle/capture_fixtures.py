@@ -393,6 +393,31 @@ def capture_fwd256():
           f"mask {np.abs(om.numpy() - m.numpy()).max():.3g} code {np.abs(oc.numpy() - c.numpy()).max():.3g}")
 
 
+def capture_r50_256(seeds=(0, 1, 2)):
+    """configs[4]'s network at its own geometry (R50 + ASPP_50, 256x256 crops, one network per
+    object as test_vivo.py:99-114 builds them): per object seed, the synthetic weights with BN
+    running stats calibrated on four 256x256 crops by the reference itself (r50_bn256_s<seed>.npz);
+    for seed 0 also the reference's forward of two other 256x256 crops (r50_fwd256.npz) -- the
+    anchor that pins ref_cpu.forward(.., 50) at 256x256 for tests/test_gpu_multi_object.py."""
+    for seed in seeds:
+        net = build_reference(50)
+        net.load_state_dict(ref_cpu.synthetic_state(50, 16, seed=seed))
+        calibrate_bn(net, seeded((4, 3, 256, 256), 51 + seed))
+        bnbuf = canonical_bn_buffers(net, 50)
+        np.savez_compressed(os.path.join(GOLDEN, f"r50_bn256_s{seed}.npz"), **bnbuf)
+        if seed != 0:
+            continue
+        x = seeded((2, 3, 256, 256), 52)
+        with torch.no_grad():
+            m, c = net(x)
+        np.savez_compressed(os.path.join(GOLDEN, "r50_fwd256.npz"), x=x.numpy(), mask=m.numpy(), code=c.numpy())
+        sd2 = ref_cpu.synthetic_state(50, 16, seed=0, bn_buffers=bnbuf)
+        with torch.no_grad():
+            om, oc = ref_cpu.forward(sd2, x, 50)
+        print(f"r50 fwd256 (256-calibrated BN): |logit| max {np.abs(c.numpy()).max():.3g}; oracle vs reference: "
+              f"mask {np.abs(om.numpy() - m.numpy()).max():.3g} code {np.abs(oc.numpy() - c.numpy()).max():.3g}")
+
+
 def capture_gt_codes():
     """GT code planes: the reference's RGB_image_to_class_id_image +
     class_id_image_to_class_code_images (class_id_encoder_decoder.py:6-15, 43-63) on BGR GT crops
@@ -488,6 +513,8 @@ def main():
         capture_add_adi()
     if "--r50" in sys.argv:
         capture_network(50)
+    if only is not None and "r50_256" in only:
+        capture_r50_256()
     if "--v3" in sys.argv:
         capture_v3()
 

@@ -65,3 +65,67 @@ def test_multi_object_rejects_bad_index(gpu, golden):
     x = torch.zeros(2, 3, 64, 64, device="cuda")
     with pytest.raises(ValueError):
         mo(x, [0, 1], np.zeros((2, 4), int))
+
+
+@pytest.mark.parametrize("precision", ["fp16", "fp32"])
+def test_configs4_r50_multi_object_vs_oracle(gpu, golden, precision):
+    """BASELINE.json configs[4] at its own workload: ResNet50 + ASPP_50 networks, one per object
+    (test_vivo.py:99-114 builds one BinaryCodeNet_Deeplab per object and loops over instances,
+    :138-179), fp16 MFMA, batched multi-object inference on 256x256 crops with the code->vertex decode
+    on the device.  Three objects (synthetic weights, BN calibrated at 256x256 by the reference:
+    oracle/capture_fixtures.py capture_r50_256; the oracle's R50 forward is pinned to the reference's
+    at 256x256 by tests/test_oracle.py::test_r50_forward256_matches_reference).  Every crop's logits
+    against ref_cpu.forward(.., 50) of its object in an fp16 band: rel-L2 <= 0.09, >= 97% of the bits
+    outside |logit| <= 0.25 (observed r05 on MI355X: rel-L2 0.048-0.075, every such bit agreeing; the
+    64x64 R50 fixture shows 0.050 -- fp16's 11-bit storage rounded at every one of R50's layers and
+    amplified by the random-weight network, not a kernel error: the same batch in fp32 below is within
+    3.1e-4, and the fp16 kernels are held per op in test_gpu_units.py), and the batched decode exact
+    against ref_cpu.decode_crop on the device's logits with the object's LUT.  The same batch in fp32 (the
+    two-plane split engine) pins the grouping itself: logits within the north-star 1e-3."""
+    from oracle import ref_cpu
+    from zebrapose_amd.model.BinaryCodeNet import BinaryCodeNet_Deeplab
+    from zebrapose_amd.multi_object import MultiObjectPose
+    THR = np.float32(8.940696716308594e-08)
+    rng = np.random.default_rng(7)
+    sds, nets = [], []
+    for seed in (0, 1, 2):
+        sd = ref_cpu.synthetic_state(50, 16, seed, dict(golden(f"r50_bn256_s{seed}.npz")))
+        net = BinaryCodeNet_Deeplab(50, 16, 2, concat=True, output_kernel_size=1)
+        net.load_state_dict(sd)
+        sds.append(sd)
+        nets.append(net.cuda().eval())
+    luts = [rng.uniform(-60, 60, (65536, 3)) for _ in nets]
+    luts[2][::89] = np.nan
+    mo = MultiObjectPose(nets, luts, precision=precision)
+    obj = np.array([2, 0, 1, 0, 2, 1])
+    Bn = len(obj)
+    x = torch.from_numpy(rng.standard_normal((Bn, 3, 256, 256)).astype(np.float32)).cuda()
+    side = rng.integers(64, 401, Bn)
+    bb = np.stack([rng.integers(0, 300, Bn), rng.integers(0, 200, Bn), side, side], 1)
+    out = mo(x, obj, bb, K)
+    torch.cuda.synchronize()
+    assert out["mask"].shape == (Bn, 1, 128, 128) and out["code"].shape == (Bn, 16, 128, 128)
+    mask, code = out["mask"].cpu().numpy(), out["code"].cpu().numpy()
+    counts, xy, xyz = out["counts"].cpu().numpy(), out["xy"].cpu().numpy(), out["xyz"].cpu().numpy()
+    bad = []
+    for b in range(Bn):
+        with torch.no_grad():
+            rm, rc = ref_cpu.forward(sds[obj[b]], x[b:b + 1].cpu(), 50)
+        for got, ref in ((mask[b:b + 1], rm.numpy()), (code[b:b + 1], rc.numpy())):
+            assert np.isfinite(got).all()
+            rel = float(np.linalg.norm(got - ref) / np.linalg.norm(ref))
+            agree = float(((got > THR) == (ref > THR))[np.abs(ref) > 0.25].mean())
+            d = float(np.abs(got - ref).max())
+            print(f"crop {b} (object {obj[b]}): {precision} R50 256x256 rel-L2 {rel:.4f}, max |d| {d:.3g} "
+                  f"(|logit| max {np.abs(ref).max():.3g}), bits agreeing {agree:.4f}")
+            if precision == "fp16" and (rel > 0.09 or agree < 0.97):
+                bad.append((b, rel, agree))
+            if precision == "fp32" and d > 1e-3:
+                bad.append((b, d))
+        n, p2d, p3d, _ = ref_cpu.decode_crop(mask[b, 0], code[b], luts[obj[b]], bb[b])
+        assert int(counts[b]) == n, b
+        np.testing.assert_array_equal(xy[b, :n], p2d)
+        np.testing.assert_array_equal(xyz[b, :n], p3d)
+    assert not bad, bad
+    del mo, nets
+    torch.cuda.empty_cache()

@@ -112,17 +112,45 @@ def test_graph_replay_overflow_recaptures_on_x3(golden):
     x = golden("r34_fwd64.npz")["fwd64_x"]
     gi = GraphedInference(net, batch=x.shape[0], size=x.shape[2])
     assert gi._flag is not None and net.net.eval_engine().split == "h2"
-    m, c = gi(torch.from_numpy(x).cuda())
+    m0, c0 = m, c = gi(torch.from_numpy(x).cuda())
     assert gi.range_fallbacks == 0
     _close((m, c), _oracle(sd, x), "graph h2, in range")
     xs = (x * np.float32(1e5)).astype(np.float32)
     with pytest.warns(RuntimeWarning, match="fp16's range"):
         m, c = gi(torch.from_numpy(xs).cuda())
     assert gi.range_fallbacks == 1 and net.net.f32_split == "x3" and gi._flag is None
+    assert m is m0 and c is c0  # the static outputs keep their identity across the re-capture
     _close((m, c), _oracle(sd, xs), "graph after fallback, scaled input")
     m, c = gi(torch.from_numpy(x).cuda())  # the x3 graph keeps serving in-range crops
-    assert gi.range_fallbacks == 1
+    assert gi.range_fallbacks == 1 and m is m0
     _close((m, c), _oracle(sd, x), "graph x3, in range")
+
+
+def test_unguarded_overflow_does_not_leak(golden):
+    """the range word is per engine and cleared at the start of every two-plane forward.
+    A network with the guard off overflows (its word stays set, unread); a second, guarded,
+    in-range network on the same device must stay on h2, and so must the first one's own next
+    guarded forward once its inputs are in range (its weights are in range)."""
+    bad, _ = _net(golden, _scale_bn("net.resnet.layer5.2.bn2", 1e5))
+    good, sd = _net(golden)
+    x = golden("r34_fwd64.npz")["fwd64_x"]
+    bad.net.range_check = False
+    with torch.no_grad():
+        bad(torch.from_numpy(x).cuda())
+    assert int(bad.net.eval_engine().range_word("cuda").item()) == 1
+    with torch.no_grad():
+        m, c = good(torch.from_numpy(x).cuda())
+    assert good.net.range_fallbacks == 0 and good.net.eval_engine().split == "h2"
+    assert int(good.net.eval_engine().range_word("cuda").item()) == 0
+    _close((m, c), _oracle(sd, x), "guarded in-range net after an unguarded overflow")
+    # the unguarded run packed the weights without a reader: the word is kept until one reads it
+    # (conservative: the packs' |w| >= 32 check runs only at packing); its next guarded forward
+    # therefore reports the kept word and falls back -- never the other network's
+    bad.net.range_check = True
+    with pytest.warns(RuntimeWarning, match="fp16's range"):
+        with torch.no_grad():
+            bad(torch.from_numpy(x).cuda())
+    assert bad.net.range_fallbacks == 1 and good.net.range_fallbacks == 0
 
 
 def test_eager_scaled_input_falls_back(golden):

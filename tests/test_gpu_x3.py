@@ -175,14 +175,13 @@ def test_split_strip_kernel(gpu, geom, mode, form):
     assert variant == (5 if strip else 4), (variant, mode)
 
 
-def _check_geom(gpu, geom, form="x3"):
+def _check_geom(gpu, geom, form="x3", B=2, names_out=None):
     """Split vs exact-f32-MFMA error against float64; returns the launch variant (zp_conv2d_config)."""
     from zebrapose_amd import _lib as L
     from zebrapose_amd.engine import Engine, Unit, Act, joined
     from zebrapose_amd.model import layers as LY
     kind, cin, cout, k, s, p, d, bias, H = geom
     torch.manual_seed(0)
-    B = 2
     if kind == "conv":
         conv = LY.Conv2d(cin, cout, k, s, p, d, bias=bias)
     else:
@@ -221,6 +220,8 @@ def _check_geom(gpu, geom, form="x3"):
         if mode == "x3":
             names = [r[1] for r in eng.stage_log]
             variant = 5 if all(n.startswith("k_conv3s<") for n in names) else 4
+            if names_out is not None:
+                names_out.extend(names)
     scale = ref.abs().max().item()
     e3 = (out["x3"] - ref).abs().max().item()
     e32 = (out["f32"] - ref).abs().max().item()
@@ -419,6 +420,96 @@ def test_wide_split_k_strip_small_batch(gpu):
     assert e1 <= 2.0 * e0 + 2.0 ** -22 * ref.abs().max().item(), (e1, e0)
 
 
+# the geometries the 256 x 128 wide tile takes at the bench's bs = 32 (layer4's 3x3s and its first
+# conv / downsample at 32 x 32, conv_1x1_3): 128 tiles of 256 x 256, 256 of 256 x 128
+TP128_GEOMS = [
+    ("conv", 256, 256, 3, 1, 2, 2, False, 32),
+    ("conv", 128, 256, 3, 1, 2, 2, False, 32),
+    ("conv", 128, 256, 1, 1, 0, 1, False, 32),
+    ("conv", 1280, 256, 1, 1, 0, 1, True, 32),
+]
+
+
+@pytest.mark.parametrize("geom", TP128_GEOMS, ids=[_gid(g) for g in TP128_GEOMS])
+def test_wide_tp128_is_f32_accurate(gpu, geom):
+    """The 256 x 128 two-plane tile (k_conv3w<TP = 128>, zp_conv_tuning key 14; off by default: on
+    layer4 it measured 118.7 us against k_conv3's 114.1) at bs = 32: the dispatch picks it, and its error against float64 is within the two-plane bound of the
+    exact-f32-MFMA kernel's (as every geometry in test_split_conv_is_f32_accurate)."""
+    from zebrapose_amd import _lib as L
+    names = []
+    old = L.lib.zp_conv_tuning(14, 1)
+    try:
+        _check_geom(gpu, geom, "h2", B=32, names_out=names)
+    finally:
+        L.lib.zp_conv_tuning(14, old)
+    assert names == ["k_conv3w<h2,TP=128>"], names
+
+
+@pytest.mark.parametrize("geom", [("conv", 512, 512, 3, 1, 4, 4, False, 32), ("conv", 256, 256, 3, 1, 1, 1, False, 64)],
+                         ids=["l5_d4_K144", "up1_K72"])
+def test_wide_accumulation_forms(gpu, geom):
+    """k_conv3w's accumulation forms (zp_conv_tuning key 13) on long-K launches, ReLU'd positive
+    inputs as in the network, against float64:
+      0 = k_conv3's correction accumulator, flushed per K step by a rounding FMA (the default);
+      1 = round 4's one scaled accumulator: every correction product is added by the MFMA into the
+          large running sum, whose alignment truncates its low bits -- a systematic negative bias;
+      2 = per-step partial sums from zero added by v_add_f32: smaller rms, but the corrections are
+          still truncated against the step's main partial.
+    The default's mean signed error (relative to the mean |output|) must be within 3x the exact-f32
+    MFMA kernel's (+ a 2^-27 floor) and under a tenth of the one-accumulator form's, its rms within
+    the two-plane bound of the f32 kernel's."""
+    from zebrapose_amd import _lib as L
+    from zebrapose_amd.engine import Engine, Unit, Act, joined
+    from zebrapose_amd.model import layers as LY
+    kind, cin, cout, k, s, p, d, bias, H = geom
+    torch.manual_seed(12)
+    B = 8
+    conv = LY.Conv2d(cin, cout, k, s, p, d, bias=False)
+    bn = LY.BatchNorm2d(cout)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.normal_(0, 0.1)
+        bn.running_mean.normal_(0, 0.1)
+        bn.running_var.uniform_(0.5, 1.5)
+    conv, bn = conv.to(gpu).eval(), bn.to(gpu).eval()
+    unit = Unit(conv, bn, relu=False)
+    x = torch.randn(B, cin, H, H).clamp(min=0)
+    ref = _ref64(kind, conv, bn, x, None, False, s, p, d)
+    xh = x.permute(0, 2, 3, 1).contiguous()
+
+    def stats(out):
+        dd = joined(out.buf).permute(0, 3, 1, 2).double().cpu() - ref
+        return dd.mean().item() / ref.abs().mean().item(), dd.pow(2).mean().sqrt().item() / ref.pow(2).mean().sqrt().item()
+    stat = {}
+    f32 = Engine(torch.nn.Module(), torch.float32)
+    oa = Act(torch.empty(B, H, H, cout, device=gpu))
+    f32.unit_fwd(unit, Act(xh.to(gpu)), oa, None)
+    torch.cuda.synchronize()
+    stat["f32"] = stats(oa)
+    xa = Act(_split_act(xh, gpu, "h2"))
+    eng = Engine(torch.nn.Module(), torch.float32, split="h2")
+    old_min, old_acc, old_sk = L.lib.zp_conv_tuning(11, 1), L.lib.zp_conv_tuning(13, -1), L.lib.zp_conv_tuning(12, 0)
+    try:
+        for acc in (-1, 0, 1, 2):
+            L.lib.zp_conv_tuning(13, acc)
+            oa = Act(eng._empty((B, H, H, cout), gpu))
+            eng.stage_log = []
+            eng.unit_fwd(unit, xa, oa, None)
+            torch.cuda.synchronize()
+            assert [r[1] for r in eng.stage_log] == ["k_conv3w<h2>"]
+            stat[acc] = stats(oa)
+    finally:
+        L.lib.zp_conv_tuning(11, old_min)
+        L.lib.zp_conv_tuning(13, old_acc)
+        L.lib.zp_conv_tuning(12, old_sk)
+    print(f"{geom}: (bias, rms) relative -- f32 MFMA {stat['f32']}, flushed {stat[0]}, one accumulator {stat[1]}, "
+          f"per-step partial {stat[2]}")
+    assert stat[-1] == stat[0]  # the default is the flushed form
+    assert abs(stat[0][0]) <= 3.0 * abs(stat["f32"][0]) + 2.0 ** -27, stat
+    assert abs(stat[0][0]) <= abs(stat[1][0]) / 10.0, stat
+    assert stat[0][1] <= BOUND["h2"][0] * stat["f32"][1], stat
+
+
 # schedule flags of the two-plane kernels that must not change a single stored bit (zp_conv_tuning
 # key 1 = ZP_CONV_FLAGS; 478 = the default set): 268435456 no strip staging (k_conv3w), 134217728
 # caller's sub-problem order instead of longest first, 1 plain instead of non-temporal stores, 512
@@ -426,13 +517,14 @@ def test_wide_split_k_strip_small_batch(gpu):
 _BITWISE_FLAGS = [268435456, 134217728, 1, 512, 32]
 
 
-@pytest.mark.parametrize("geom,B,kernel",
-                         [(("conv", 256, 256, 3, 1, 1, 1, False, 64), 16, "k_conv3w<h2>"),    # strips
-                          (("convT", 256, 256, 3, 2, 1, 1, False, 32), 16, "k_conv3w<h2>"),   # 4 phases
-                          (("conv", 64, 64, 3, 1, 1, 1, False, 64), 8, "k_conv3s<h2,WC=2>"),  # WP = 2
-                          (("conv", 256, 256, 3, 1, 2, 2, False, 32), 32, "k_conv3<h2,WC=4,NWP=4>")],
-                         ids=["wide3x3", "wideConvT", "strip64", "conv3_layer4"])
-def test_schedule_flags_are_bit_identical(gpu, geom, B, kernel):
+@pytest.mark.parametrize("geom,B,kernel,tp128",
+                         [(("conv", 256, 256, 3, 1, 1, 1, False, 64), 16, "k_conv3w<h2>", 1),    # strips
+                          (("convT", 256, 256, 3, 2, 1, 1, False, 32), 16, "k_conv3w<h2>", 1),   # 4 phases
+                          (("conv", 64, 64, 3, 1, 1, 1, False, 64), 8, "k_conv3s<h2,WC=2>", 1),  # WP = 2
+                          (("conv", 256, 256, 3, 1, 2, 2, False, 32), 32, "k_conv3<h2,WC=4,NWP=4>", 0),
+                          (("conv", 256, 256, 3, 1, 2, 2, False, 32), 32, "k_conv3w<h2,TP=128>", 1)],
+                         ids=["wide3x3", "wideConvT", "strip64", "conv3_layer4", "wide128_layer4"])
+def test_schedule_flags_are_bit_identical(gpu, geom, B, kernel, tp128):
     """Round-4 schedule choices (strip staging of the wide tile, longest-first phase order, nt
     stores, the paired 16-byte epilogue, the 128-pixel strip tile) change the data movement only:
     with each switched back, the stored two-plane outputs are bit-identical (residual on for the
@@ -463,16 +555,20 @@ def test_schedule_flags_are_bit_identical(gpu, geom, B, kernel):
         res = torch.randn(B, cout, OH, OW)
         ra = Act(_split_act(res.permute(0, 2, 3, 1).contiguous(), gpu, "h2"))
     outs = {}
-    for extra in [0] + _BITWISE_FLAGS:
-        old = L.lib.zp_conv_tuning(1, 478 + extra)
-        try:
-            oa = Act(eng._empty((B, OH, OW, cout), gpu))
-            eng.stage_log = []
-            eng.unit_fwd(unit, xa, oa, None, res=ra)
-            torch.cuda.synchronize()
-        finally:
-            L.lib.zp_conv_tuning(1, old)
-        outs[extra] = oa.buf._base.clone()
+    old14 = L.lib.zp_conv_tuning(14, tp128)
+    try:
+        for extra in [0] + _BITWISE_FLAGS:
+            old = L.lib.zp_conv_tuning(1, 478 + extra)
+            try:
+                oa = Act(eng._empty((B, OH, OW, cout), gpu))
+                eng.stage_log = []
+                eng.unit_fwd(unit, xa, oa, None, res=ra)
+                torch.cuda.synchronize()
+            finally:
+                L.lib.zp_conv_tuning(1, old)
+            outs[extra] = oa.buf._base.clone()
+    finally:
+        L.lib.zp_conv_tuning(14, old14)
     names = [r[1] for r in eng.stage_log]
     print(geom, names)
     assert names == [kernel], names

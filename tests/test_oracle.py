@@ -168,6 +168,17 @@ def test_r50_state_spec_and_forward_match_reference(golden):
     np.testing.assert_allclose(c.numpy(), f["fwd64_code"], atol=1e-5, rtol=0)
 
 
+def test_r50_forward256_matches_reference(golden):
+    """configs[4]'s network at its own 256x256 geometry (BN calibrated at 256x256 by the reference,
+    oracle/capture_fixtures.py capture_r50_256): the oracle's R50 forward equals the reference's."""
+    f = golden("r50_fwd256.npz")
+    sd = ref_cpu.synthetic_state(50, 16, 0, dict(golden("r50_bn256_s0.npz")))
+    with torch.no_grad():
+        m, c = ref_cpu.forward(sd, torch.from_numpy(f["x"]), 50)
+    np.testing.assert_allclose(m.numpy(), f["mask"], atol=1e-5, rtol=0)
+    np.testing.assert_allclose(c.numpy(), f["code"], atol=1e-5, rtol=0)
+
+
 def test_v3_state_spec_and_forward_match_reference(golden):
     """BinaryCodeNet_Deeplab_v3: key layout and the 256x256 three-head forward
     of the oracle against the reference's own outputs (oracle/capture_fixtures.py capture_v3)."""

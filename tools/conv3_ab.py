@@ -21,6 +21,8 @@ LAYERS = {  # name: (kind, cin, cout, k, d, hw)
     "l1": ("conv", 64, 64, 3, 1, 64),
     "l2": ("conv", 128, 128, 3, 1, 32),
     "l4": ("conv", 256, 256, 3, 2, 32),
+    "l4a": ("conv", 128, 256, 3, 2, 32),      # layer4's first conv (128 -> 256)
+    "proj": ("conv", 1280, 256, 1, 1, 32),    # ASPP conv_1x1_3
 }
 
 
@@ -36,6 +38,9 @@ def main():
     ap.add_argument("--minblocks", default="256", help="zp_conv_tuning key 8 values to A/B (comma list)")
     ap.add_argument("--wide", default="-1", help="zp_conv_tuning key 10 values to A/B (k_conv3w: 0 off, 1 on)")
     ap.add_argument("--splitk", default="1", help="zp_conv_tuning key 12 values to A/B (k_conv3w split-K: 0, 1, 2)")
+    ap.add_argument("--acc", default="-1", help="zp_conv_tuning key 13 values to A/B (k_conv3w accumulation: 0 flushed, "
+                    "1 one scaled accumulator, 2 per-step partial)")
+    ap.add_argument("--tp128", default="-1", help="zp_conv_tuning key 14 values to A/B (k_conv3w 256 x 128 tile: 0, 1)")
     a = ap.parse_args()
     from zebrapose_amd import _lib as L
     from zebrapose_amd.engine import Engine, Unit, Act
@@ -75,22 +80,26 @@ def main():
         OH, OW = unit.out_hw(hw, hw)
         y = Act(eng._empty((a.batch, OH, OW, cout), dev))
         taps = 9 if kind == "conv" else 9 / 4 * 4  # convT: 4 phases x 9/4 taps over the input grid
-        fl = 2.0 * a.batch * hw * hw * (9 if kind == "conv" else 9) * cin * cout
+        fl = 2.0 * a.batch * hw * hw * (k * k if kind == "conv" else 9) * cin * cout
         setups.append((name, eng, unit, Act(xs), y, fl))
     mbs = [int(m) for m in a.minblocks.split(",")]
     strips = [int(m) for m in a.strip.split(",")]
     wides = [int(m) for m in a.wide.split(",")]
     sks = [int(m) for m in a.splitk.split(",")]
+    accs = [int(m) for m in a.acc.split(",")]
+    t128 = [int(m) for m in a.tp128.split(",")]
     first = {}
     import itertools
     for r in range(a.rounds):
-        for f0, mb, sm, wd, sk in itertools.product(flags, mbs, strips, wides, sks):
+        for f0, mb, sm, wd, sk, ac, tq in itertools.product(flags, mbs, strips, wides, sks, accs, t128):
             L.lib.zp_conv_tuning(1, f0)
             L.lib.zp_conv_tuning(8, mb)
             L.lib.zp_conv_tuning(7, sm)
             L.lib.zp_conv_tuning(10, wd)
             L.lib.zp_conv_tuning(12, sk)
-            f = (f0, mb, sm, wd, sk)
+            L.lib.zp_conv_tuning(13, ac)
+            L.lib.zp_conv_tuning(14, tq)
+            f = (f0, mb, sm, wd, sk, ac, tq)
             for name, eng, unit, x, y, fl in setups:
                 def run1():
                     if hasattr(unit, "outs"):
@@ -125,10 +134,12 @@ def main():
     L.lib.zp_conv_tuning(7, -1)
     L.lib.zp_conv_tuning(10, -1)
     L.lib.zp_conv_tuning(12, 1)
+    L.lib.zp_conv_tuning(13, -1)
+    L.lib.zp_conv_tuning(14, -1)
     for (name, f), v in sorted(res.items()):
         fl = [s[5] for s in setups if s[0] == name][0]
         us = min(v)
-        print(f"{name:8s} flags {f[0]:6d} minblocks {f[1]:4d} strip {f[2]:2d} wide {f[3]:2d} splitk {f[4]}: {us:9.1f} us  {fl / us * 1e-6:7.1f} TFLOP/s  ({fl / us * 1e-6 / (2516.6 / (6 if a.form == 'x3' else 3)):.3f} of the {a.form} ceiling)")
+        print(f"{name:8s} flags {f[0]:6d} minblocks {f[1]:4d} strip {f[2]:2d} wide {f[3]:2d} splitk {f[4]} acc {f[5]:2d} tp128 {f[6]:2d}: {us:9.1f} us  {fl / us * 1e-6:7.1f} TFLOP/s  ({fl / us * 1e-6 / (2516.6 / (6 if a.form == 'x3' else 3)):.3f} of the {a.form} ceiling)")
 
 
 if __name__ == "__main__":

@@ -41,9 +41,14 @@ def bench_label(name):
         return f"k_conv3s<{sp[m.group(1)]},WC={m.group(2)}>"
     if "k_stem_h2" in name:  # the direct two-plane stem (zp_stem_split)
         return "k_stem_h2"
-    m = re.search(r"k_conv3w<(\d+), (\d+), (true|false)(?:, (?:true|false))*>", name)  # the 256 x 256 two-plane tile (+ fused head)
+    # the 256 x 256 two-plane tile (+ fused head); template <ABL, DM, HEAD, SGB, PF, BF, STR, NUM, TPX>
+    # (TPX 128: the 256 x 128 tile)
+    m = re.search(r"k_conv3w<(\d+), (\d+), (true|false)((?:, (?:true|false|\d+))*)>", name)
     if m:
-        return "k_conv3w_head<h2>" if m.group(3) == "true" else "k_conv3w<h2>"
+        rest = [v.strip() for v in m.group(4).split(",") if v.strip()]
+        if m.group(3) == "true":
+            return "k_conv3w_head<h2>"
+        return "k_conv3w<h2,TP=128>" if len(rest) >= 6 and rest[5] == "128" else "k_conv3w<h2>"
     m = re.search(r"k_conv3<(\d+), (\d+), (\d+), (\d+), (\d+), (true|false)>", name)
     if m:
         return f"k_conv3<{sp[m.group(1)]},WC={m.group(2)},NWP={m.group(4)}>"

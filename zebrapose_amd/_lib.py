@@ -169,21 +169,33 @@ def ptr(t) -> int | None:
     return t.data_ptr()
 
 
-_RANGE_FLAGS = {}
+_RANGE_FLAGS = {}  # device index -> the word registered last (kept alive while registered)
+
+
+def register_range_flag(t: torch.Tensor) -> None:
+    """Register ``t`` (int32 [1] on a HIP device) with zp_split_range_flag (include/zp.h) for its
+    device: every ZP_F32H2 store enqueued from now on raises it for a finite value beyond fp16's
+    range.  The C side reads the pointer at enqueue time, so each Engine registers its own word
+    before its launches (a captured hipGraph keeps the word of its capture).  The tensor is kept
+    alive here while it is the registered one, so the registry never points at freed memory."""
+    idx = t.device.index if t.device.index is not None else torch.cuda.current_device()
+    if _RANGE_FLAGS.get(idx) is t:
+        return
+    with torch.cuda.device(idx):
+        check(lib.zp_split_range_flag(t.data_ptr()), "zp_split_range_flag")
+    _RANGE_FLAGS[idx] = t
 
 
 def range_flag(device) -> torch.Tensor:
-    """The device word registered with zp_split_range_flag (include/zp.h) for ``device``: int32 [1],
-    set to 1 by any ZP_F32H2 store that meets a finite value beyond fp16's range.  Created and
-    registered on first use (outside a graph capture: the engine's eager forward does it)."""
+    """The word currently registered with zp_split_range_flag for ``device`` (int32 [1]); a fresh
+    one is created and registered when there is none.  Engines use their own words
+    (Engine.range_word); this is for direct callers of the C-ABI (tools, tests)."""
     dev = torch.device(device)
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
     t = _RANGE_FLAGS.get(idx)
     if t is None:
         t = torch.zeros(1, dtype=torch.int32, device=f"cuda:{idx}")
-        with torch.cuda.device(idx):
-            check(lib.zp_split_range_flag(t.data_ptr()), "zp_split_range_flag")
-        _RANGE_FLAGS[idx] = t
+        register_range_flag(t)
     return t
 
 

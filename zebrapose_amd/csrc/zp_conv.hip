@@ -2767,7 +2767,7 @@ extern "C" int zp_conv2d_stat_parts(const zp_conv_args* a) {
 
 extern "C" int zp_conv2d_head_ok(const zp_conv_args* a) {
   return a && a->dtype == ZP_F32H2 && a->nsub == 1 && a->Cout == 256 && a->out_mode == ZP_OUT_NHWC &&
-         conv3_tc(*a) == 256 && conv3w_splitk(*a) == 1;
+         conv3_tc(*a) == 256 && conv3w_tp(*a) == 256 && conv3w_splitk(*a) == 1;
 }
 
 extern "C" int zp_conv2d_head(const zp_conv_args* a, const zp_head_args* h, void* stream) {
@@ -2793,7 +2793,10 @@ extern "C" int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* st
  * the older ~1024-workgroup target padded to a multiple of 8); key 6: the fewest workgroups
  * k_conv_quad runs with (default 256); key 7: split-fp32 strip kernel k_conv3s (0 off, 1 the
  * 64-channel tiles, 2 also the 128-channel tiles; -1 = ZP_CONV3_STRIP / default 1); key 8: the
- * fewest workgroups a split-fp32 launch runs 128-channel tiles with (fewer: 64-channel tiles).
+ * fewest workgroups a split-fp32 launch runs 128-channel tiles with (fewer: 64-channel tiles);
+ * keys 10-12: the wide two-plane tile (on / fewest workgroups / split-K); key 13: its accumulation
+ * form (0 flushed correction accumulator, 1 one scaled accumulator, 2 per-step partial sums, the
+ * default; -1 = ZP_CONV3W_ACC); key 14: its 256 x 128 pixel tile (0 off, 1 on; -1 = ZP_CONV3W_TP128).
  * Returns the previous value. */
 /* split-fp32 split-K workspace: bytes of f32 slices zp_conv2d uses for these args when a.stats
  * points to that many (0: the launch is not split) */
@@ -2840,6 +2843,8 @@ extern "C" int zp_conv_tuning(int key, int value) {
   if (key == 10) return conv3w_mode(value);
   if (key == 11) return conv3w_min_blocks(value);
   if (key == 12) return conv3w_splitk_mode(value);
+  if (key == 13) return conv3w_acc_mode(value);
+  if (key == 14) return conv3w_tp128_mode(value);
   if (key == 4) {
     const int old = g_wgrad2_rounds;
     g_wgrad2_rounds = value > 0 ? value : 1;

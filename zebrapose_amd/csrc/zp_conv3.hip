@@ -1109,7 +1109,7 @@ int conv3_tc(const zp_conv_args& a) {
 // (register-pipelined, 3-deep ring) for 64-channel tiles, 32 x 128 for the head.
 int conv3_tp(const zp_conv_args& a, int tc) {
   static const int sched = env_int("ZP_CONV3_SCHED");
-  if (tc == 256) return 256;  // k_conv3w
+  if (tc == 256) return conv3w_tp(a);  // k_conv3w (256, or the 256 x 128 tile)
   if (tc == 128) return sched == 1 ? 128 : 256;  // 8-wave ping-pong 128 x 256, or the pipelined 128 x 128
   return 128;
 }

@@ -9,15 +9,19 @@
 // thirds of the bytes per FLOP, and halves the per-step fixed costs (barrier, first-read latency,
 // DMA issue) per FLOP.
 //
-// Numerics (round 4, "one scaled accumulator"): every product a*b = hi*hi + (hi*lo' + lo'*hi) * 2^-11
-// on v_mfma_f32_16x16x32_f16 (SplitF32<2> operands), but the three products of a 16 x 16 block go
-// into ONE f32 accumulator on the 2^11 scale: (2^11 w_hi)*x_hi + w_hi*x_lo' + w_lo'*x_hi, with
-// 2^11 w_hi formed from the fragment by v_pk_mul_f16 (exact: an exponent shift; weights |w| < 32,
-// flagged at packing otherwise).  The epilogue folds 2^-11 into the BN scale (exact).  k_conv3 keeps
-// a separate correction accumulator flushed per K step (acc = fma(c2, 2^-11, acc): 4 VALU FMAs per
-// block and step); removing that flush took 4x the VALU work off the step and the dependency of
-// every flush on its block's MFMAs (tools/conv3_ab.py: the flush-free ablation ran 6-12% faster).
-// Both are f32 accumulations of exact products: results agree with k_conv3's to f32 rounding.
+// Numerics (template NUM; zp_conv_tuning key 13).  Every product a*b = hi*hi + (hi*lo' + lo'*hi) *
+// 2^-11 of exact fp16 products on v_mfma_f32_16x16x32_f16 (SplitF32<2> operands).  The default
+// (ACC_FLUSH, round 5) is k_conv3's: the two correction products of a 16 x 16 block go into a fresh
+// accumulator c2, hi*hi into acc, and c2 joins acc one cout block later by a rounding FMA
+// (acc = fma(c2, 2^-11, acc)) -- bit-identical to k_conv3<h2>.  Round 4's ACC_SA put all three
+// products into ONE accumulator on the 2^11 scale ((2^11 w_hi)*x_hi + w_hi*x_lo' + w_lo'*x_hi, 2^11
+// w_hi by v_pk_mul_f16; the epilogue folds 2^-11 into the BN scale): 4-6% faster on the big 3x3s, but
+// the MFMA aligns the small correction products to the large running sum and truncates their low
+// bits, a systematic bias of about -1e-7 relative per conv (r05: -1.0e-7 against
+// -1.4e-9 flushed and 9e-10 for exact f32 on a K = 144 conv, tests/test_gpu_x3.py
+// test_wide_accumulation_forms).  ACC_PS (per-step partial sums from zero, added by v_add_f32) has
+// the smallest rms but still truncates the corrections against the step's main partial (-2e-8) and
+// ran slowest; it stays for A/B.
 // Tile: 8 waves = 2 (cout halves of 128) x 4 (pixel quarters of 64); a wave owns 8 x 4 blocks of
 // 16 x 16 (128 accumulator registers).  Its 8 weight fragments are streamed through a 3-deep
 // register ring, the 4 pixel fragments of both planes are held for the step: ~210 VGPRs, no spill
@@ -34,6 +38,11 @@
 #include "zp_conv3.h"
 
 namespace zp {
+
+// accumulation forms of the two-plane products (template NUM; zp_conv_tuning key 13)
+constexpr int ACC_FLUSH = 0;  // k_conv3's: correction accumulator flushed per step by a scaled FMA
+constexpr int ACC_SA = 1;     // one scaled accumulator (round 4): biased, see the numerics note
+constexpr int ACC_PS = 2;     // per-step partial from zero, added by a rounding v_add_f32 (round 5)
 
 __device__ __forceinline__ void wbarrier() {
   __builtin_amdgcn_s_barrier();
@@ -62,16 +71,20 @@ __device__ __forceinline__ void wbarrier() {
 // SA: one scaled accumulator per block (see the numerics note above); SA = false: k_conv3's
 //   correction accumulator c2, flushed one cout block later (acc = fma(c2, 2^-11, acc))
 template <int ABL, int DM, bool HEAD, bool SGB = false, bool PF = false, bool BF = false, bool STR = false,
-          bool SA = true>
+          int NUM = ACC_FLUSH, int TPX = 256>
 __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv_taps TG, const int flags,
                                                 const zp_head_args H, float* __restrict__ ws, const int nsplit) {
   constexpr int NPL = 2;
-  constexpr int TC = 256, TP = 256;
+  constexpr int TC = 256, TP = TPX;
+  static_assert(TP == 256 || TP == 128, "pixel tile");
+  static_assert(TP == 256 || (!HEAD && !BF && DM == 1), "the 256 x 128 tile: plain epilogue, default DMA order");
+  constexpr bool SA = NUM != ACC_FLUSH;              // accumulators on the 2^11 scale (NUM 1, 2)
   constexpr int NTW = TC / 16, NT = (TC + TP) / 16;  // weight tiles / all tiles per plane (16 rows each)
   constexpr int UNITS = NPL * NT;                    // 1 KB DMA units per stage
-  constexpr int WC = 8, WP = 4;                      // per wave: 8 cout blocks x 4 pixel blocks
-  constexpr int TPW = NT / 8;                        // tiles per wave: 2 weight + 2 activation
-  static_assert(2 * TPW == WC, "one DMA piece per cout block");
+  constexpr int WC = 8, WP = TP / 64;                // per wave: 8 cout blocks x 4 (TP 128: 2) pixel blocks
+  constexpr int TPW = NT / 8;                        // tiles per wave: 2 weight + 2 (TP 128: 1) activation
+  constexpr int NPC = 2 * TPW;                       // DMA pieces per wave and step (both planes)
+  static_assert(NPC % DM == 0 && NPC <= 2 * WC, "DMA pieces over the first DM cout blocks");
   using MT = MfmaTraits<f16_t>;
   constexpr int SPMAX = 20;              // STR: strip pieces per plane (320 pixels)
   constexpr int APL = STR ? NTW : NT;    // units per plane of a stage of the per-step ring
@@ -190,7 +203,8 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
   // discarded: nine steps later those rows are L2 hits.
   unsigned pf_sink = 0;
   const bool pf_hi = (lane >> 5) & 1;  // lane groups 0, 1 -> activation tile 2; 2, 3 -> tile 3
-  const unsigned pf_base = pf_hi ? ubase[3] : ubase[2], pf_ym = pf_hi ? uym[3] : uym[2], pf_xm = pf_hi ? uxm[3] : uxm[2];
+  constexpr int PFT = TPW - 1;  // (TP 128: one activation tile)
+  const unsigned pf_base = pf_hi ? ubase[PFT] : ubase[2], pf_ym = pf_hi ? uym[PFT] : uym[2], pf_xm = pf_hi ? uxm[PFT] : uxm[2];
   const unsigned pf_plane = ((lane >> 4) & 1) ? psx_b : 0u;
   auto prep = [&](DmaStep& d) {
 #pragma unroll
@@ -285,6 +299,24 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
   // weight fragments streamed 2 ahead; per block: c2 = hi*lo' + lo'*hi, acc += hi*hi, and the flush
   // acc = fma(c2, 2^-11, acc) one cout block later (its MFMAs have finished by then)
   constexpr bool abl_dma = ABL == 1, abl_mfma = ABL == 2, abl_bar = ABL == 3;
+  // a cout block's per-step sums into its accumulators (NUM 2: one rounding add; NUM 0: the scaled
+  // correction FMA); the asm pins each add here -- sunk into the next step, every block's c2 would
+  // stay live (333 spilled VGPRs)
+  auto flush = [&](f32x4 (&a)[WP], const f32x4 (&c)[WP]) {
+#pragma unroll
+    for (int j = 0; j < WP; ++j) {
+      if constexpr (NUM == ACC_PS) {
+        // (rebuilt as a whole vector: element-wise updates of a[j] spilled 130+ VGPRs, and a vector
+        // add becomes v_pk_add_f32, which costs ~13 cycles more than two v_add_f32 beside MFMAs)
+        const f32x4 t = {a[j].x + c[j].x, a[j].y + c[j].y, a[j].z + c[j].z, a[j].w + c[j].w};
+        a[j] = t;
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) a[j][r] = __builtin_fmaf(c[j][r], SplitF32<2>::CS, a[j][r]);
+      }
+      asm volatile("" : "+v"(a[j]));
+    }
+  };
   auto step = [&](auto s_c, const bool more, const bool strip_now) {
     constexpr int s = decltype(s_c)::value;
     // the next step's DMA (into the other buffer: every wave has passed the barrier that ended the
@@ -328,7 +360,7 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
         af[q][p] = ds_read16<(p * APL + q) * 1024>(ab);
       });
     });
-    f32x4 c2p[WP];  // !SA: the previous cout block's correction sums (flushed one block later)
+    f32x4 c2p[WP];  // NUM 0 / 2: the previous cout block's per-step sums (flushed one block later)
     static_for<WC>([&](auto i_c) {
       constexpr int i = decltype(i_c)::value;
       if constexpr (i + 2 < WC) {
@@ -341,32 +373,39 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
       constexpr int after = (i + 1 < WC ? NPL : 0) + (i + 2 < WC ? NPL : 0);
       asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(after) : "memory");
       __builtin_amdgcn_sched_barrier(0);
-      // SA: the three products of every block into its one accumulator, on the 2^11 scale:
-      // lo'*hi + hi*lo' + (2^11 hi)*hi (the small terms first).  !SA: the corrections into a fresh
-      // c2 (k_conv3's term order, Terms<2>: hi*lo', then lo'*hi), hi*hi into acc.
+      // NUM 2 (ACC_PS): the three products of the block, on the 2^11 scale, into a fresh c2 --
+      // lo'*hi + hi*lo' + (2^11 hi)*hi, the small terms first -- and acc += c2 (v_add_f32, round to
+      // nearest) one cout block later.  NUM 1 (ACC_SA): the same three products straight into acc.
+      // NUM 0 (ACC_FLUSH): the corrections into a fresh c2 (k_conv3's term order, Terms<2>: hi*lo',
+      // then lo'*hi), hi*hi into acc, acc = fma(c2, 2^-11, acc) one block later.
       f32x4 c2[WP];
       uint4 hs;
       if constexpr (SA) hs = scale_hi(af[i % 3][0]);
 #pragma unroll
       for (int j = 0; j < WP; ++j) {
+        if constexpr (NUM != ACC_SA) c2[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
         if constexpr (abl_mfma) {
           // (the fragment reads are asm volatile: they still issue)
-        } else if constexpr (SA) {
+        } else if constexpr (NUM == ACC_SA) {
           MT::mma(acc[i][j], af[i % 3][1], bf[0][j]);
+        } else if constexpr (NUM == ACC_PS) {
+          MT::mma(c2[j], hs, bf[0][j]);
         } else {
-          c2[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
           MT::mma(c2[j], af[i % 3][0], bf[1][j]);
           MT::mma(c2[j], af[i % 3][1], bf[0][j]);
         }
       }
       if constexpr (SA && !abl_mfma) {
 #pragma unroll
-        for (int j = 0; j < WP; ++j) MT::mma(acc[i][j], af[i % 3][0], bf[1][j]);
+        for (int j = 0; j < WP; ++j) {
+          if constexpr (NUM == ACC_SA) MT::mma(acc[i][j], af[i % 3][0], bf[1][j]);
+          else MT::mma(c2[j], af[i % 3][0], bf[1][j]);
+        }
       }
       if constexpr (i < DM && !abl_dma)  // (no branch: after the last step the pieces are out of range -> no-ops)
-        static_for<8 / DM>([&](auto q_c) {
-          constexpr int q = i * (8 / DM) + decltype(q_c)::value;
-          piece(std::integral_constant<int, BF ? (q + 4) % 8 : q>{}, s ^ 1, dn);
+        static_for<NPC / DM>([&](auto q_c) {
+          constexpr int q = i * (NPC / DM) + decltype(q_c)::value;
+          piece(std::integral_constant<int, BF ? (q + NPC / 2) % NPC : q>{}, s ^ 1, dn);
         });
       if constexpr (STR && i == 1 && !abl_dma) {
         if (strip_now) strip_issue(r_gs ^ 1);
@@ -375,21 +414,17 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
       for (int j = 0; j < WP; ++j) {
         if constexpr (abl_mfma) {
           if constexpr (SA) asm volatile("" ::"v"(hs.x), "v"(hs.y), "v"(hs.z), "v"(hs.w));
-        } else if constexpr (SA) {
+        } else if constexpr (NUM == ACC_SA) {
           MT::mma(acc[i][j], hs, bf[0][j]);
+        } else if constexpr (NUM == ACC_PS) {
+          MT::mma(c2[j], af[i % 3][1], bf[0][j]);
         } else {
           MT::mma(acc[i][j], af[i % 3][0], bf[0][j]);
         }
       }
-      if constexpr (!SA && i > 0) {
-#pragma unroll
-        for (int j = 0; j < WP; ++j) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc[i - 1][j][r] = __builtin_fmaf(c2p[j][r], SplitF32<2>::CS, acc[i - 1][j][r]);
-          asm volatile("" : "+v"(acc[i - 1][j]));  // pinned here: sunk into the next step, every
-        }                                            // block's c2 would stay live (333 spilled VGPRs)
-      }
-      if constexpr (!SA) {
+      if constexpr (NUM == ACC_PS) flush(acc[i], c2);  // (the same block: the other wave's MFMAs cover the wait)
+      if constexpr (NUM == ACC_FLUSH && i > 0) flush(acc[i - 1], c2p);
+      if constexpr (NUM == ACC_FLUSH) {
 #pragma unroll
         for (int j = 0; j < WP; ++j) c2p[j] = c2[j];
       }
@@ -402,12 +437,7 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
       }
       __builtin_amdgcn_sched_barrier(0);
     });
-    if constexpr (!SA) {
-#pragma unroll
-      for (int j = 0; j < WP; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[WC - 1][j][r] = __builtin_fmaf(c2p[j][r], SplitF32<2>::CS, acc[WC - 1][j][r]);
-    }
+    if constexpr (NUM == ACC_FLUSH) flush(acc[WC - 1], c2p);
   };
 
   // prologue: step 0's DMA into buffer 0 (STR: and group 0's strip into strip stage 0)
@@ -708,6 +738,28 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
 int conv3w_splitk(const zp_conv_args& a);
 static int g_conv3w = -1;       // zp_conv_tuning key 10 (-1: ZP_CONV3W or the default 1)
 static int g_conv3w_min = 256;  // zp_conv_tuning key 11
+static int g_conv3w_acc = -1;   // zp_conv_tuning key 13: accumulation form (-1: ZP_CONV3W_ACC or ACC_FLUSH)
+static int g_conv3w_tp128 = -1; // zp_conv_tuning key 14: 256 x 128 tiles (-1: ZP_CONV3W_TP128 or 0)
+
+int conv3w_acc_mode(int v) {
+  const int old = g_conv3w_acc;
+  g_conv3w_acc = v;
+  return old;
+}
+int conv3w_tp128_mode(int v) {
+  const int old = g_conv3w_tp128;
+  g_conv3w_tp128 = v;
+  return old;
+}
+static int conv3w_acc() {
+  static const int env = getenv("ZP_CONV3W_ACC") ? atoi(getenv("ZP_CONV3W_ACC")) : ACC_FLUSH;
+  const int v = g_conv3w_acc >= 0 ? g_conv3w_acc : env;
+  return (v == ACC_PS || v == ACC_SA) ? v : ACC_FLUSH;
+}
+static bool conv3w_tp128_on() {
+  static const int env = getenv("ZP_CONV3W_TP128") ? atoi(getenv("ZP_CONV3W_TP128")) : 0;
+  return (g_conv3w_tp128 >= 0 ? g_conv3w_tp128 : env) != 0;
+}
 
 int conv3w_mode(int v) {
   const int old = g_conv3w;
@@ -736,7 +788,18 @@ bool conv3w_ok(const zp_conv_args& a) {
     for (int s = 0; s < a.nsub; ++s)
       if (a.sub[s].ntaps > 4) return false;
   const long blocks = (((long)a.N * a.GH * a.GW + 255) / 256) * (a.Cout / 256) * a.nsub;
-  return blocks >= g_conv3w_min || conv3w_splitk(a) > 1;
+  return blocks >= g_conv3w_min || conv3w_splitk(a) > 1 || conv3w_tp(a) == 128;
+}
+
+// pixel tile of the wide kernel: 256, or 128 for a one-sub launch whose 256 x 256 grid would leave
+// CUs idle (fewer than g_conv3w_min tiles, no split-K) while its 256 x 128 grid fills them (bs 32:
+// layer4's 256 -> 256 3 x 3s at 32 x 32 and conv_1x1_3, 128 -> 256 tiles; they ran on k_conv3's
+// 128 x 256 tile).  k_conv3w<TP = 128>: a wave owns 8 x 2 blocks, 6 DMA pieces per step.
+int conv3w_tp(const zp_conv_args& a) {
+  const long M = (long)a.N * a.GH * a.GW;
+  if (((M + 255) / 256) * (a.Cout / 256) * a.nsub >= g_conv3w_min) return 256;
+  if (!conv3w_tp128_on() || a.nsub != 1 || conv3w_splitk(a) > 1) return 256;
+  return ((M + 127) / 128) * (a.Cout / 256) >= g_conv3w_min ? 128 : 256;
 }
 
 // split-K of the wide tile (zp_conv_tuning key 12, default 1): a one-sub NHWC launch under 64 tiles
@@ -770,14 +833,14 @@ int conv3w_splitk(const zp_conv_args& a) {
 // (flag 268435456: off, for A/B)
 // (several sub-problems -- the ConvT phases, 1 x 1 / 1 x 2 / 2 x 1 / 2 x 2 taps over the input grid
 // -- each with its own strip geometry; one-column subs stage a halo-free strip per step)
-static bool conv3w_strip_ok(const zp_conv_args& a, const conv_taps& tg, int fl, int ns) {
+static bool conv3w_strip_ok(const zp_conv_args& a, const conv_taps& tg, int fl, int ns, int tp = 256) {
   (void)ns;
   if ((fl & 268435456) || a.sx != 1 || a.sy != 1) return false;
-  if (a.GW % 16 != 0 || 256 % a.GW != 0 || ((long)a.GH * a.GW) % 256 != 0) return false;
+  if (a.GW % 16 != 0 || tp % a.GW != 0 || ((long)a.GH * a.GW) % tp != 0) return false;
   int nxmax = 0;
   for (int s = 0; s < a.nsub; ++s) {
     if (a.sub[s].ntaps != tg.ny[s] * tg.nx[s] || (tg.nx[s] > 1 && tg.dtx[s] == 0)) return false;
-    if ((256 / a.GW) * (a.GW + (tg.nx[s] - 1) * abs(tg.dtx[s])) > 320) return false;
+    if ((tp / a.GW) * (a.GW + (tg.nx[s] - 1) * abs(tg.dtx[s])) > 320) return false;
     nxmax = max(nxmax, tg.nx[s]);
   }
   return nxmax >= 2;
@@ -810,10 +873,19 @@ void conv3w_launch(const zp_conv_args& a0, const conv_taps& tg0, hipStream_t st,
       tg.w_bytes[s] = tg0.w_bytes[o];
     }
   }
+  const zp_head_args H{};
+  const int acc = (fl & 536870912) ? ACC_FLUSH : conv3w_acc();  // (flag 536870912: the flushed form, as in round 4)
+  const bool str = conv3w_strip_ok(a, tg, fl, ns);
+  if (ns == 1 && conv3w_tp(a) == 128) {  // the 256 x 128 tile (zp_conv_tuning key 14)
+    const dim3 g128((unsigned)(((long)a.N * a.GH * a.GW + 127) / 128), (unsigned)(a.Cout / 256), (unsigned)a.nsub);
+    if (conv3w_strip_ok(a, tg, fl, ns, 128))
+      hipLaunchKernelGGL((k_conv3w<0, 1, false, false, false, false, true, ACC_FLUSH, 128>), g128, dim3(512), 0, st, a, tg, fl, H, ws, ns);
+    else hipLaunchKernelGGL((k_conv3w<0, 1, false, false, false, false, false, ACC_FLUSH, 128>), g128, dim3(512), 0, st, a, tg, fl, H, ws, ns);
+    return;
+  }
   const dim3 grid((unsigned)(((long)a.N * a.GH * a.GW + 255) / 256), (unsigned)(a.Cout / 256), (unsigned)(a.nsub * ns));
   // flags 262144 / 524288: the DMA pieces over the first 2 / 8 cout blocks (default: the first one);
   // 1048576 / 2097152: DM 1 / 8 with the MFMA / flush interleave (SGB)
-  const zp_head_args H{};
   if (fl & 4096) hipLaunchKernelGGL((k_conv3w<1, 1, false>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);  // diagnostic: no DMA
   else if (fl & 8192) hipLaunchKernelGGL((k_conv3w<2, 1, false>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);  // diagnostic: no MFMA
   else if (fl & 131072) hipLaunchKernelGGL((k_conv3w<3, 1, false>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);  // diagnostic: no barrier
@@ -821,25 +893,39 @@ void conv3w_launch(const zp_conv_args& a0, const conv_taps& tg0, hipStream_t st,
   else if (fl & 8388608) hipLaunchKernelGGL((k_conv3w<5, 1, false>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);  // diagnostic: no activation DMA
   else if (fl & 262144) hipLaunchKernelGGL((k_conv3w<0, 2, false>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
   else if (fl & 524288) hipLaunchKernelGGL((k_conv3w<0, 8, false>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
-  else if (fl & 1048576) hipLaunchKernelGGL((k_conv3w<0, 1, false, true>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
-  else if (fl & 2097152) hipLaunchKernelGGL((k_conv3w<0, 8, false, true>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
+  else if (fl & 1048576) {  // the MFMA / flush interleave (sched_group_barrier), strips as the default
+    if (str) hipLaunchKernelGGL((k_conv3w<0, 1, false, true, false, false, true>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
+    else hipLaunchKernelGGL((k_conv3w<0, 1, false, true>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
+  } else if (fl & 2097152) hipLaunchKernelGGL((k_conv3w<0, 8, false, true>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
   else if (fl & 16777216) hipLaunchKernelGGL((k_conv3w<0, 1, false, false, true>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);  // L2 prefetch
   else if (fl & 33554432) hipLaunchKernelGGL((k_conv3w<0, 1, false, false, false, true>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);  // activations first
   else if (fl & 67108864) hipLaunchKernelGGL((k_conv3w<6, 1, false, false, false>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);  // diagnostic: 1/3 of the activation pieces
-  else if (fl & 536870912) {  // the per-step correction flush (A/B)
-    if (conv3w_strip_ok(a, tg, fl, ns))
-      hipLaunchKernelGGL((k_conv3w<0, 1, false, false, false, false, true, false>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
-    else hipLaunchKernelGGL((k_conv3w<0, 1, false, false, false, false, false, false>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
-  } else if (conv3w_strip_ok(a, tg, fl, ns))
+  else if (acc == ACC_SA) {  // round 4's one scaled accumulator (A/B)
+    if (str) hipLaunchKernelGGL((k_conv3w<0, 1, false, false, false, false, true, ACC_SA>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
+    else hipLaunchKernelGGL((k_conv3w<0, 1, false, false, false, false, false, ACC_SA>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
+  } else if (acc == ACC_PS) {  // per-step partial sums (A/B)
+    if (str) hipLaunchKernelGGL((k_conv3w<0, 1, false, false, false, false, true, ACC_PS>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
+    else hipLaunchKernelGGL((k_conv3w<0, 1, false, false, false, false, false, ACC_PS>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
+  } else if (str)  // the default: k_conv3's flushed correction accumulator (bit-identical to k_conv3<h2>)
     hipLaunchKernelGGL((k_conv3w<0, 1, false, false, false, false, true>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
   else hipLaunchKernelGGL((k_conv3w<0, 1, false>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
 }
 
 void conv3w_head_launch(const zp_conv_args& a, const conv_taps& tg, const zp_head_args& h, hipStream_t st, int fl) {
   const dim3 grid((unsigned)(((long)a.N * a.GH * a.GW + 255) / 256), 1u, 1u);
-  if (conv3w_strip_ok(a, tg, fl, 1))
+  const bool str = conv3w_strip_ok(a, tg, fl, 1);
+  const int acc = (fl & 536870912) ? ACC_FLUSH : conv3w_acc();
+  if (acc == ACC_SA) {  // (A/B)
+    if (str) hipLaunchKernelGGL((k_conv3w<0, 1, true, false, false, false, true, ACC_SA>), grid, dim3(512), 0, st, a, tg, fl, h, nullptr, 1);
+    else hipLaunchKernelGGL((k_conv3w<0, 1, true, false, false, false, false, ACC_SA>), grid, dim3(512), 0, st, a, tg, fl, h, nullptr, 1);
+  } else if (acc == ACC_PS) {  // (A/B)
+    if (str) hipLaunchKernelGGL((k_conv3w<0, 1, true, false, false, false, true, ACC_PS>), grid, dim3(512), 0, st, a, tg, fl, h, nullptr, 1);
+    else hipLaunchKernelGGL((k_conv3w<0, 1, true, false, false, false, false, ACC_PS>), grid, dim3(512), 0, st, a, tg, fl, h, nullptr, 1);
+  } else if (str) {
     hipLaunchKernelGGL((k_conv3w<0, 1, true, false, false, false, true>), grid, dim3(512), 0, st, a, tg, fl, h, nullptr, 1);
-  else hipLaunchKernelGGL((k_conv3w<0, 1, true>), grid, dim3(512), 0, st, a, tg, fl, h, nullptr, 1);
+  } else {
+    hipLaunchKernelGGL((k_conv3w<0, 1, true>), grid, dim3(512), 0, st, a, tg, fl, h, nullptr, 1);
+  }
 }
 
 }  // namespace zp

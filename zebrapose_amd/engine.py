@@ -166,6 +166,21 @@ class Engine:
         # two-plane eval forward: up2's last conv and the head in one launch (zp_conv2d_head);
         # ZP_FUSE_HEAD=0 keeps them apart
         self.fuse_head = os.environ.get("ZP_FUSE_HEAD", "1") != "0"
+        # the two-plane form's range word (range_word) and whether packings were made since its
+        # reader last looked (unread_packs: set by _pack, cleared by the readers)
+        self._rflag = None
+        self.unread_packs = False
+        self.range_probe = None  # optional list (tests): see _probe
+
+    def range_word(self, device):
+        """This engine's zp_split_range_flag word on ``device`` (int32 [1]): raised by any of its
+        two-plane stores or weight packs that meets a value beyond the form's range (include/zp.h)."""
+        dev = torch.device(device)
+        if dev.index is None:
+            dev = torch.device(dev.type, torch.cuda.current_device())
+        if self._rflag is None or self._rflag.device != dev:
+            self._rflag = torch.zeros(1, dtype=torch.int32, device=dev)
+        return self._rflag
 
     # ------------------------------------------------------------------ weight / BN caches
     def invalidate(self):
@@ -202,6 +217,8 @@ class Engine:
                                                       L.ZP_F16: torch.float16}[dt]
             out = torch.empty(shape, dtype=tdt, device=w.device)
             self._cache_gen += 1
+        if dt == L.ZP_F32H2:
+            self.unread_packs = True
         ky = [t[0] for t in sub.taps]
         kx = [t[1] for t in sub.taps]
         L.call("zp_pack_weight", w.data_ptr(), d0, d1, w.shape[2], w.shape[3], transposed, len(sub.taps),
@@ -315,7 +332,7 @@ class Engine:
                 L.check(L.lib.zp_conv2d_head(C.byref(a), C.byref(head[0]), st), "zp_conv2d_head")
             else:
                 L.check(L.lib.zp_conv2d(C.byref(a), st), "zp_conv2d")
-        if self.timing is not None or self.stage_log is not None:
+        if self.timing is not None or self.stage_log is not None or self.range_probe is not None:
             if self.timing is not None:
                 e0 = torch.cuda.Event(enable_timing=True)
                 e1 = torch.cuda.Event(enable_timing=True)
@@ -344,9 +361,16 @@ class Engine:
                 self.timing.append((geo, e0, e1, flops, kname, nbytes))
             if self.stage_log is not None:
                 self.stage_log.append((self.stage, kname, flops, nbytes, geo))
+            self._probe(kname)
         else:
             launch()
         return stats, parts
+
+    def _probe(self, kname):
+        """range_probe (tests): after each launch, a device copy of this engine's range word, so a
+        test can name the first launch that raised it."""
+        if self.range_probe is not None and self._rflag is not None:
+            self.range_probe.append((self.stage, kname, self._rflag.clone()))
 
     def _kname(self, a, plan, x, dt=None):
         """rocprofv3's kernel instantiation of this launch, in the label form tools/prof_summary.py
@@ -355,8 +379,8 @@ class Engine:
         tc, tp, stages, var = C.c_int(), C.c_int(), C.c_int(), C.c_int()
         L.call("zp_conv2d_config", C.byref(a), C.byref(tc), C.byref(tp), C.byref(stages), C.byref(var))
         tn = _TN[dt]
-        if var.value == 6:  # rocprofv3 name: k_conv3w<ABL, DM, HEAD>
-            return f"k_conv3w<{tn}>"
+        if var.value == 6:  # rocprofv3 name: k_conv3w<ABL, DM, HEAD, .., NUM, TPX> (TPX 128: the 256 x 128 tile)
+            return f"k_conv3w<{tn}>" if tp.value == 256 else f"k_conv3w<{tn},TP={tp.value}>"
         if var.value == 5:  # rocprofv3 name: k_conv3s<NPL, WC>
             return f"k_conv3s<{tn},WC={tc.value // 32}>"
         if var.value == 4:  # rocprofv3 name: k_conv3<NPL, WC, WP, NWP, ST, PIPE>
@@ -413,6 +437,7 @@ class Engine:
                     fl = 2.0 * x.B * OH * OW * unit.k * unit.k * cr * unit.cout
                     nb = x.P * x.ld * 4 + x.B * OH * OW * unit.cout * 4 + w.numel() * w.element_size()
                     self.stage_log.append((self.stage, "k_stem_h2", fl, nb, f"{label}:{cr}->{unit.cout} 7x7s2"))
+                self._probe("k_stem_h2")
                 if self.trace is not None:
                     self.trace.append(("conv", unit, x, out, res))
                 return
@@ -776,17 +801,21 @@ class Engine:
         def new(h, w, c):
             return Act(self._empty((B, h, w, c), dev))
 
+        if self.dt == L.ZP_F32H2:
+            # the range guard (include/zp.h zp_split_range_flag): this engine's own word, registered
+            # and cleared at the start of every forward, eager or captured (a captured forward
+            # clears it at the start of each replay), before the weight packing, whose |w| >= 32
+            # check raises it too.  Its readers -- DeepLabV3.forward after an eager forward,
+            # GraphedInference after a replay -- therefore see this forward's stores only: not a
+            # word left set by an unguarded run, nor another network's
+            # (weights packed by a forward whose word nobody read -- an unguarded run -- keep it
+            # set: their |w| >= 32 check runs only at packing time)
+            flag = self.range_word(dev)
+            L.register_range_flag(flag)
+            if not self.unread_packs or torch.cuda.is_current_stream_capturing():
+                flag.zero_()
         self._prepack(dev)
         st = L.stream_ptr()
-        if self.dt == L.ZP_F32H2:
-            # the range guard (include/zp.h zp_split_range_flag): registered before the first
-            # two-plane store; its reader (DeepLabV3.forward) clears it after an eager forward.  A
-            # captured forward clears it at its start, so that each replay starts clean
-            # (GraphedInference reads it after the replay; the weights were packed, and their
-            # range checked, by the eager warm-up)
-            flag = L.range_flag(dev)
-            if torch.cuda.is_current_stream_capturing():
-                flag.zero_()
         self.stage = "stem"
         if self.x3:  # the stem reads f32 (exact-f32 small-Cin kernel) and writes split output
             xin = Act(torch.empty((B, H, W, 8), dtype=torch.float32, device=dev))

@@ -75,26 +75,45 @@ class GraphedInference:
         # may already have switched a network to x3): the captured forward clears the device flag at
         # its start (Engine._forward_main), _replay reads it after each replay
         self._guarded = [m for m in _deeplabs(net) if m.h2_active() and m.range_check]
-        self._flag = L.range_flag(dev) if self._guarded else None
+        # each guarded network's engine word (Engine.range_word): the captured forwards clear and
+        # raise their own words, read together after each replay
+        words = [m.eval_engine().range_word(dev) for m in self._guarded]
+        self._flag = None if not words else words[0] if len(words) == 1 else words
         self.graph = torch.cuda.CUDAGraph()
         # thread_local: under torch.distributed the RCCL watchdog thread may query events meanwhile
         with torch.no_grad(), torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
-            self.out = self._step()
+            out = self._step()
+        # the static outputs keep their identity across a re-capture (the x3 fallback): a new graph's
+        # outputs are copied into the first capture's tensors after each replay (_out_copy)
+        if getattr(self, "out", None) is None:
+            self.out, self._out_copy = out, None
+        else:
+            self._out_copy = out
         self._tensors, self._engs = _state_tensors(net), _engines(net)
         self._stamp = _state_stamp(self._tensors, self._engs)
 
+    def _flag_hit(self):
+        """The guarded networks' range words after a replay: one blocking 4-byte read (the host waits
+        for the replay), or one per network group via a max on the device."""
+        if self._flag is None:
+            return False
+        f = self._flag if torch.is_tensor(self._flag) else torch.cat(self._flag).max()
+        return bool(int(f.item()))
+
     def _replay(self):
         self.graph.replay()
-        if self._flag is not None and int(self._flag.item()):
+        if self._flag_hit():
             # a value beyond fp16's range: the networks switch to the full-range x3 engine, and the
             # step is captured again (the warm-up and capture leave the static inputs alone) and
             # replayed
-            self._flag.zero_()
             for m in self._guarded:
                 m.range_fallback()
             self.range_fallbacks += 1
             self._capture()
             self.graph.replay()
+        if self._out_copy is not None:
+            for d, o in zip(self.out, self._out_copy):
+                d.copy_(o)
 
     def _step(self):
         mask, code = self.net(self.x)
@@ -105,7 +124,9 @@ class GraphedInference:
 
     def __call__(self, x, bboxes=None):
         """x f32 [B, 3, size, size] (device or host); bboxes [B, 4] (x, y, w, h) when a decoder is
-        attached -> (mask, code) or (mask, code, counts, xy, xyz), the graph's static outputs."""
+        attached -> (mask, code) or (mask, code, counts, xy, xyz), the graph's static outputs (the
+        same tensors on every call, a range fallback's re-capture included).  With a two-plane
+        network under the range guard, each call waits for its replay (the 4-byte flag read)."""
         if tuple(x.shape) != tuple(self.x.shape):
             raise ValueError(f"captured for input {tuple(self.x.shape)}, got {tuple(x.shape)}")
         if _state_stamp(self._tensors, self._engs) != self._stamp:

@@ -282,10 +282,12 @@ class DeepLabV3(nn.Module):
         eng = self._engine if self.training else self.eval_engine()
         mask, code, _ = eng.forward(x, train=self.training)
         if eng.split == "h2" and self.range_check and not torch.cuda.is_current_stream_capturing():
-            # (a captured forward is checked by its GraphedInference after each replay)
-            flag = L.range_flag(x.device)
-            if int(flag.item()):
-                flag.zero_()
+            # (a captured forward is checked by its GraphedInference after each replay).  The read
+            # waits for the forward: every guarded eager call synchronises the host with the GPU
+            flag = eng.range_word(x.device)
+            hit = int(flag.item())
+            eng.unread_packs = False
+            if hit:
                 self.range_fallback()
                 mask, code, _ = self.eval_engine().forward(x, train=False)
         return mask, code
