@@ -291,9 +291,11 @@ def test_fp32_matches_reference_fixture_256(golden, split):
 def test_fp32_bench_geometry_fused_head(setup):
     """The benched fp32 forward as benched: two planes, up2's last 3x3 conv and the 1x1 head in one
     launch (zp_conv2d_head: the conv's output is never stored; the head reads x_128 itself).  Logits of
-    the sampled crops within the north-star 1e-3 of the fp32 oracle, and within 2e-4 of the unfused
-    two-plane forward (the fused head multiplies the f32 conv output, the unfused one its stored
-    22-bit form: both are f32-accurate)."""
+    the sampled crops within the north-star 1e-3 of the fp32 oracle, and equal to the unfused two-plane
+    forward up to the head sum's f32 rounding: the fused epilogue splits the conv output into the same
+    two fp16 planes the unfused path stores (zp_conv3w.hip HEAD epilogue), so the two differ only in the
+    order of the head's 320-term sums (a loose bound would hide a channel-mapping error in
+    the fused head's weight layout)."""
     from oracle import ref_cpu
     net, sd, x = setup
     net.set_precision("fp32")
@@ -313,8 +315,9 @@ def test_fp32_bench_geometry_fused_head(setup):
     eng.fuse_head = True
     for a, b in ((m, mu), (c, cu)):
         d = float((a - b).abs().max())
-        print(f"fused vs unfused head: max |d| {d:.3g} (|logit| max {float(b.abs().max()):.3g})")
-        assert d <= 2e-4
+        scale = float(b.abs().max())
+        print(f"fused vs unfused head: max |d| {d:.3g} = {d / scale:.3g} of the logit scale {scale:.3g}")
+        assert d <= 2e-4 and d <= 1e-6 * scale
     xs = x[list(SAMPLE)]
     with torch.no_grad():
         fm, fc = ref_cpu.forward(sd, xs, 34)

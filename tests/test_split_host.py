@@ -56,3 +56,20 @@ def test_im2col_split_argument_checks():
     # not a split dtype
     rc = L.lib.zp_im2col_split(x, 1, 16, 16, 8, 3, 7, 2, 3, 8, 8, 160, L.ZP_BF16, y, None)
     assert rc == 1 and b"split-fp32" in L.lib.zp_last_error()
+
+
+def test_eval_batch_limit():
+    """Engine.eval_batch_limit: the largest eval batch one pass keeps every conv
+    input below 2 GiB -- the widest input is H/2 x W/2 x 384 channels of the engine's storage."""
+    import torch
+    from zebrapose_amd.engine import Engine
+    m = torch.nn.Module()
+    lim = {k: Engine(m, torch.float32, split=k).eval_batch_limit(256, 256) for k in ("h2", "x3")}
+    lim["f32"] = Engine(m, torch.float32).eval_batch_limit(256, 256)
+    lim["bf16"] = Engine(m, torch.bfloat16).eval_batch_limit(256, 256)
+    assert lim == {"h2": 85, "x3": 56, "f32": 85, "bf16": 170}, lim
+    e = Engine(m, torch.float32, split="h2")
+    x = torch.zeros(128, 3, 256, 256)
+    parts = e._chunks(x, train=False)
+    assert [p.shape[0] for p in parts] == [64, 64]
+    assert e._chunks(x, train=True) is None and e._chunks(x[:85], train=False) is None

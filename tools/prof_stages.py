@@ -210,6 +210,25 @@ def md(tab):
     return "\n".join(out) + "\n"
 
 
+def write_leg_csv(tab, path):
+    """One inference leg's last step, per kernel label (the dominant kernel's frac
+    recomputable from one file): launches in the step, us per launch (kernel-trace pass), algorithmic
+    TFLOP/s and its fraction of the leg's ceiling, HBM bytes per launch (PMC passes), MFMA busy %."""
+    form = tab.get("split_form")
+    ceil = PEAK_SPLIT[form] if form else PEAK[tab["precision"]]
+    rows = sorted(tab["kernels"].items(), key=lambda kv: -kv[1]["launches"] * kv[1]["us_per_launch"])
+    with open(path, "w", newline="") as fh:
+        w = csv.writer(fh)
+        w.writerow(["label", "launches_per_step", "us_per_launch", "us_per_step", "tflops", "ceiling_tflops",
+                    "frac_of_ceiling", "hbm_bytes_per_launch", "read_bytes_per_launch", "write_bytes_per_launch",
+                    "mfma_busy_pct", "lib_sha16"])
+        for k, v in rows:
+            w.writerow([k, v["launches"], v["us_per_launch"], round(v["launches"] * v["us_per_launch"], 1), v["tflops"],
+                        round(ceil, 1), round(v["tflops"] / ceil, 3) if v["tflops"] else None,
+                        v["hbm_bytes_per_launch"], v["read_bytes_per_launch"], v["write_bytes_per_launch"],
+                        v["mfma_busy_pct"], tab["lib_sha16"]])
+
+
 def main(tag="r03", precs=("fp32", "bf16")):
     src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
     dst = os.path.join(ROOT, "profiles")
@@ -234,6 +253,7 @@ def main(tag="r03", precs=("fp32", "bf16")):
                 traffic["by_label"][k] = v["hbm_bytes_per_launch"]
         with open(os.path.join(dst, f"{tag}_stages_{p}.json"), "w") as fh:
             json.dump(tab, fh, indent=1)
+        write_leg_csv(tab, os.path.join(dst, f"{tag}_{p}_step_kernels.csv"))
         text.append(md(tab))
         print(md(tab))
     with open(os.path.join(dst, f"{tag}_pmc_traffic.json"), "w") as fh:

@@ -205,10 +205,16 @@ extern "C" int zp_stem_split(const float* x, int B, int H, int W, int ldx, const
   const size_t reg = (size_t)(STEM_S * TR + STEM_K - STEM_S) * (STEM_S * OW + STEM_K - STEM_S) * 3;  // floats
   const size_t lds = ((reg + 3) & ~(size_t)3) * sizeof(float) + (size_t)(STEM_KP / 32) * 4 * 2 * 64 * 16;
   ZP_CHECK_ARG(lds <= 80 * 1024, "zp_stem_split: region + weights %zu B", lds);  // two workgroups per CU
-  static bool attr = false;
-  if (!attr) {  // dynamic LDS beyond 64 KB
-    (void)hipFuncSetAttribute((const void*)k_stem_h2, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
-    attr = true;
+  // dynamic LDS beyond 64 KB: the attribute is set once per device (it may be per device;
+  // a process can drive several GPUs), and a failure is reported as such
+  static bool attr[64] = {};
+  int dev = 0;
+  ZP_CHECK_ARG(hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64, "zp_stem_split: no current device");
+  if (!attr[dev]) {
+    ZP_CHECK_ARG(hipFuncSetAttribute((const void*)k_stem_h2, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024) ==
+                     hipSuccess,
+                 "zp_stem_split: hipFuncSetAttribute(MaxDynamicSharedMemorySize, 80 KB) failed on device %d", dev);
+    attr[dev] = true;
   }
   const long psy = (long)B * OH * OW * ldy;
   hipLaunchKernelGGL(k_stem_h2, dim3((unsigned)((long)B * OH * OW / 256)), dim3(256), lds, (hipStream_t)stream, x, H, W,

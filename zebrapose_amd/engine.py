@@ -766,8 +766,35 @@ class Engine:
             self.bwd_trace.append(tr)
 
     # ------------------------------------------------------------------ network
+    # ------------------------------------------------------------------ batch chunks
+    # Every libzp launch addresses its input and weights with 32-bit buffer offsets, so one launch's
+    # input stays below 2 GiB (zp_conv2d refuses more).  The widest conv input of any network here
+    # sits at half resolution with at most 384 channels (v3's [up_2 | x_128 | mask | 0] concat; the
+    # main network's unfused head input has 320), so an eval forward whose batch would reach that
+    # runs in equal batch chunks: crops are independent in eval mode.  Training keeps
+    # one batch -- its BatchNorm statistics are over the whole batch (train_v6.py:320-321).
+    _CHUNK_BYTES = (1 << 31) - 1
+
+    def eval_batch_limit(self, H, W):
+        """The largest batch one eval forward of this engine runs in a single pass at H x W."""
+        per_crop = (H // 2) * (W // 2) * 384 * _ES[self.dt]
+        return max(1, self._CHUNK_BYTES // per_crop)
+
+    def _chunks(self, x, train):
+        B, _, H, W = x.shape
+        lim = self.eval_batch_limit(H, W)
+        if train or B <= lim:
+            return None
+        n = -(-B // lim)
+        step = -(-B // n)
+        return [x[i:i + step] for i in range(0, B, step)]
+
     def forward(self, x, train):
         """x f32 NCHW [B, 3, H, W] -> (mask [B,1,H/2,W/2], code [B,L,H/2,W/2]) f32, tape (train)."""
+        parts = self._chunks(x, train)
+        if parts is not None:
+            rs = [self._forward_main(c, train, first=i == 0) for i, c in enumerate(parts)]
+            return torch.cat([r["mask"] for r in rs]), torch.cat([r["code"] for r in rs]), None
         r = self._forward_main(x, train)
         return r["mask"], r["code"], r["tape"]
 
@@ -775,11 +802,18 @@ class Engine:
         """BinaryCodeNet_Deeplab_v3 (BinaryCodeNet_v3.py:152-169): the main network, then the
         entire-mask head ASPP_v3 on (mask logits, x_high, x_128, x_64) (aspp_v3.py:78-102)
         -> (mask, entire_mask, code, tape)."""
+        parts = self._chunks(x, train)
+        if parts is not None:
+            outs = []
+            for i, c in enumerate(parts):
+                r = self._forward_main(c, train, first=i == 0)
+                outs.append((r["mask"], self._aspp_v3(r), r["code"]))
+            return tuple(torch.cat(t) for t in zip(*outs)) + (None,)
         r = self._forward_main(x, train)
         entire = self._aspp_v3(r)
         return r["mask"], entire, r["code"], r["tape"]
 
-    def _forward_main(self, x, train):
+    def _forward_main(self, x, train, first=True):
         dl = self._net()
         rn, aspp = dl.resnet, dl.aspp
         if not rn.concat_decoder:
@@ -812,7 +846,8 @@ class Engine:
             # set: their |w| >= 32 check runs only at packing time)
             flag = self.range_word(dev)
             L.register_range_flag(flag)
-            if not self.unread_packs or torch.cuda.is_current_stream_capturing():
+            # (a chunked forward clears it before its first chunk only: the word covers the batch)
+            if first and (not self.unread_packs or torch.cuda.is_current_stream_capturing()):
                 flag.zero_()
         self._prepack(dev)
         st = L.stream_ptr()
