@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define ZP_ABI_VERSION 1
+#define ZP_ABI_VERSION 2
 
 #define ZP_OK 0
 #define ZP_ERR_ARG 1
@@ -163,15 +163,20 @@ long long zp_conv2d_split_ws(const zp_conv_args* a);
  * (default 1, 0 off).  Returns the previous value, -1 for an unknown key. */
 int zp_conv_tuning(int key, int value);
 
-/* Fused 1x1 head (ZP_F32H2 only; the reference's conv_1x1_4 over torch.cat([x, x_128]) and the
- * mask / code split, model/aspp.py:112 + model/BinaryCodeNet.py:172).  The conv of *a (one sub, NHWC,
- * BN scale / shift, bias, residual and ReLU applied as by zp_conv2d) is NOT stored: each output
- * pixel's Cout channels, followed by the C2 channels of x2 at the same pixel (ZP_F32H2 NHWC,
- * [N][OH][OW][ldx2], channels cx20..), feed a 1x1 conv with hcout <= 32 outputs: weights w packed
- * by zp_pack_weight(dtype ZP_F32H2, rows_pad 32, k = channel, k_pad >= Cout + C2), bias (f32 [hcout]
- * or NULL).  Output f32 NCHW: channel 0 -> mask [N][1][OH][OW], channels 1.. -> code
- * [N][hcout-1][OH][OW].  zp_conv2d_head_ok: 1 if *a has a geometry the fused kernel takes (the
- * 256 x 256 split tile with Cout == 256; e.g. not at bs = 1, where the unfused path runs). */
+/* Fused 1x1 head (the reference's conv_1x1_4 over torch.cat([x, x_128]) and the mask / code split,
+ * model/aspp.py:112 + model/BinaryCodeNet.py:172).  The conv of *a (one sub, NHWC, BN scale / shift,
+ * bias, residual and ReLU applied as by zp_conv2d) is NOT stored: each output pixel's Cout channels,
+ * followed by the C2 channels of x2 at the same pixel (NHWC of a's dtype, [N][OH][OW][ldx2], channels
+ * cx20..), feed a 1x1 conv with hcout <= 32 outputs: weights w packed by zp_pack_weight(a's dtype,
+ * rows_pad 32, k = channel, k_pad >= Cout + C2), bias (f32 [hcout] or NULL).  Output f32 NCHW:
+ * channel 0 -> mask [N][1][OH][OW], channels 1.. -> code [N][hcout-1][OH][OW].
+ *   ZP_F32H2: the 256 x 256 two-plane tile runs the conv and the whole head (one launch).
+ *   ZP_BF16 / ZP_F16 (eval, ABI 2): the 3x3 conv runs on the strip tile (two 128-channel cout tiles);
+ *   each tile's head sums over its channels (the first tile's also over x2) go to ws, f32
+ *   [2][32][N*OH*OW] (zp_conv2d_head_ws bytes), and a second launch adds the two in a fixed order,
+ *   plus the bias: deterministic.
+ * zp_conv2d_head_ok: 1 if *a has a geometry the fused kernels take (e.g. not at bs = 1 for
+ * ZP_F32H2, where the unfused path runs). */
 typedef struct zp_head_args {
   const void* w;
   int k_pad;
@@ -181,8 +186,10 @@ typedef struct zp_head_args {
   int ldx2, cx20, C2;
   float* mask;
   float* code;
+  float* ws;  /* ABI 2: the 16-bit path's partial sums (zp_conv2d_head_ws bytes); ignored by ZP_F32H2 */
 } zp_head_args;
 int zp_conv2d_head_ok(const zp_conv_args* a);
+long long zp_conv2d_head_ws(const zp_conv_args* a);
 int zp_conv2d_head(const zp_conv_args* a, const zp_head_args* h, void* stream);
 
 /* Pack an f32 weight tensor src[d0][d1][kh][kw] into dst[rows_pad][k_pad] (dtype), taps

@@ -55,6 +55,7 @@ int main() {
   CHECK(zp_conv2d_config(&up2, &tc, &tp, &st, &var) == ZP_OK);
   CHECK(tc == 256 && tp == 256 && var == 6);                          // the 256 x 256 tile
   CHECK(zp_conv2d_head_ok(&up2) == 1);
+  CHECK(zp_conv2d_head_ws(&up2) == 0);                               // the two-plane head: one launch
   CHECK(zp_conv2d_split_ws(&up2) == 0);                               // big grid: no split-K
   zp_conv_args l5 = conv(ZP_F32H2, 1, 32, 32, 512, 512, 3, 4);        // layer5 at bs 1
   CHECK(zp_conv2d_config(&l5, &tc, &tp, &st, &var) == ZP_OK);
@@ -64,6 +65,9 @@ int main() {
   zp_conv_args bf = conv(ZP_BF16, 32, 64, 64, 256, 256, 3, 1);
   CHECK(zp_conv2d_config(&bf, &tc, &tp, &st, &var) == ZP_OK && tc >= 64 && tp >= 128);
   CHECK(zp_conv2d_grid(&bf) > 0 && zp_conv2d_stat_parts(&bf) > 0);
+  zp_conv_args bf2 = conv(ZP_BF16, 32, 128, 128, 256, 256, 3, 1);   // up2's last 3x3 at bs 32, bf16
+  CHECK(zp_conv2d_head_ok(&bf2) == 1);                               // the fused 16-bit head
+  CHECK(zp_conv2d_head_ws(&bf2) == 2LL * 32 * 32 * 128 * 128 * 4);   // [2 cout tiles][32][M] f32
   zp_wgrad_args wa;
   memset(&wa, 0, sizeof(wa));
   wa.dtype = ZP_BF16; wa.N = 32; wa.IH = wa.GH = 32; wa.IW = wa.GW = 32; wa.sy = wa.sx = 1;

@@ -184,6 +184,40 @@ def test_bf16_bench_geometry_teacher_forced(setup):
           f"{worst_frac:.4f}, worst |d| {worst_ulp:.2f} ulp")
 
 
+@pytest.mark.parametrize("precision", ["bf16", "fp16"])
+def test_16bit_bench_geometry_fused_head(setup, precision):
+    """The 16-bit forward as benched: up2's last 3x3 conv and the 1x1 head fused (zp_conv2d_head,
+    VERDICT r4 #6; reference aspp.py:105-112 + BinaryCodeNet.py:172).  The strip kernel's epilogue
+    feeds its stored-precision outputs (rounded exactly as the unfused path stores them) to the head's
+    MFMAs, per 128-channel cout tile; a second launch adds the two tiles' partials and the bias.  Against
+    the unfused forward (conv stored into the [up2 | x_128] concat, then the separate head launch) the
+    logits differ only by the head sums' f32 summation order: within 1e-6 of the logit scale.  The stage
+    log names the fused kernel and holds no separate head launch."""
+    net, sd, x = setup
+    net.set_precision(precision)
+    net.cuda().eval()
+    eng = net.net.eval_engine()
+    assert eng.head_fusable(x.shape[0], x.shape[2] // 2, x.shape[3] // 2)
+    eng.stage_log = []
+    with torch.no_grad():
+        m, c = net(x.cuda())
+    log, eng.stage_log = eng.stage_log, None
+    tn = {"bf16": "bf16", "fp16": "f16"}[precision]
+    assert any(k == f"k_conv_strip2_head<{tn},WC=4>" for _, k, *_ in log), [k for _, k, *_ in log]
+    assert not any(st == "head" for st, *_ in log)
+    eng.fuse_head = False
+    with torch.no_grad():
+        mu, cu = net(x.cuda())
+    eng.fuse_head = True
+    for a, b in ((m, mu), (c, cu)):
+        assert torch.isfinite(a).all()
+        d = float((a - b).abs().max())
+        scale = float(b.abs().max())
+        print(f"{precision} fused vs unfused head: max |d| {d:.3g} = {d / scale:.3g} of the logit scale {scale:.3g}")
+        assert d <= 1e-6 * scale
+    net.set_precision("bf16")
+
+
 def test_bf16_bench_geometry_end_to_end(setup):
     """bs=32 bf16 logits of crops 0, 13, 31 against the bf16-emulating oracle and the fp32 oracle, in
     norm and bit agreement, plus the exact on-device decode of those logits."""

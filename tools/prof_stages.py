@@ -56,6 +56,8 @@ def nonconv_stage(name):
         return "aspp"
     if "decode" in name or "threshold" in name or "scan" in name:
         return "decode"
+    if "head_combine" in name:  # the fused 16-bit head's second launch
+        return "up2"
     return None
 
 

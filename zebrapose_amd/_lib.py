@@ -57,7 +57,7 @@ class WgradArgs(C.Structure):
 
 class HeadArgs(C.Structure):
     _fields_ = [("w", vp), ("k_pad", i32), ("bias", vp), ("cout", i32), ("x2", vp), ("ldx2", i32), ("cx20", i32),
-                ("C2", i32), ("mask", vp), ("code", vp)]
+                ("C2", i32), ("mask", vp), ("code", vp), ("ws", vp)]
 
 
 class PackJob(C.Structure):
@@ -125,6 +125,7 @@ _SIGS = {
     "zp_stem_split": (i32, [vp, i32, i32, i32, i32, vp, i32, i32, vp, vp, i32, vp, i32, i32, i32, i32, vp]),
     "zp_conv2d_head_ok": (i32, [C.POINTER(ConvArgs)]),
     "zp_conv2d_head": (i32, [C.POINTER(ConvArgs), C.POINTER(HeadArgs), vp]),
+    "zp_conv2d_head_ws": (C.c_longlong, [C.POINTER(ConvArgs)]),
 }
 
 
@@ -141,7 +142,7 @@ def _load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.zp_abi_version() != 1:
+    if lib.zp_abi_version() != 2:
         raise ImportError("libzp.so ABI version mismatch")
     return lib
 

@@ -897,8 +897,16 @@ __global__ void __launch_bounds__(512) k_conv_strip(const zp_conv_args A, const 
 //     row and piece) plus a scalar offset advanced by additions (no divisions);
 //   * one __shared__ array (weights ring, then strip ring).
 // ------------------------------------------------------------------------------------
-template <typename T, int WC, int SPW, int DM>
-__global__ void __launch_bounds__(512) k_conv_strip2(const zp_conv_args A, const strip_geo SG, const int flags) {
+template <typename T, int WC, int WP, int NWP>
+__device__ __forceinline__ void head_epilogue16(const zp_conv_args& A, const zp_conv_sub& S, const zp_head_args& H,
+                                                f32x4 (&acc)[WC][WP], int p0, int c0, int by, int wc, int wp,
+                                                int lane, int M, uint4* lds);
+
+// HEAD (zp_conv2d_head, 16-bit eval): the conv output is not stored; it feeds the fused 1x1 head's
+// partial sums over this tile's channels (head_epilogue16)
+template <typename T, int WC, int SPW, int DM, bool HEAD = false>
+__global__ void __launch_bounds__(512) k_conv_strip2(const zp_conv_args A, const strip_geo SG, const int flags,
+                                                     const zp_head_args H) {
   // DM: where the next group's strip DMA is issued.  0: the read section of tap column 1; 1: spread
   // over the read sections of the group's three steps; 2: between the MFMAs of tap column 0 (the
   // read sections then carry only the weight pieces: the LDS-DMA issue cost, ~60 cycles per piece
@@ -1174,8 +1182,134 @@ __global__ void __launch_bounds__(512) k_conv_strip2(const zp_conv_args A, const
 #pragma unroll
       for (int j = 0; j < WP; ++j) sm += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
     if (sm == 1.f) ((float*)S.y)[tid] = sm;
+  } else if constexpr (HEAD) {
+    head_epilogue16<T, WC, WP, NWP>(A, S, H, acc, p0, c0, by, wc, wp, lane, M, lds);
   } else {
     conv_epilogue<T, WC, WP, NWP>(A, S, acc, p0, c0, wc, wp, lane, M, GHW, bx, blockIdx.z, gridDim.z);
+  }
+}
+
+// The fused head's epilogue for the 16-bit strip tile (ZP_BF16 / ZP_F16 eval; zp_conv2d_head): the
+// tile's TC = 32 WC output channels of 256 pixels, after BN scale / shift, residual and ReLU and
+// rounded to the storage type exactly as the unfused path stores them, are the B operand of the head's
+// 16 x 16 x 32 MFMAs: the paired lane layout (v_permlane16_swap of cout blocks i, i + 1: a lane holds
+// 8 consecutive channels of one pixel) is a B fragment when lane group g is read as k slot g, so the
+// head weights are read with the same channel permutation (k slot g <-> channel (g & 1) * 16 +
+// (g >> 1) * 8 of the 32-channel slice).  The first cout tile also adds x2 (x_128) at k = Cout + c.
+// The two wave rows (wc) of a pixel quarter meet in LDS; the tile's partial sums (rows r < hcout,
+// f32) go to H.ws[by][r][p]; k_head_combine16 adds the cout tiles in order, plus the bias.
+template <typename T, int WC, int WP, int NWP>
+__device__ __forceinline__ void head_epilogue16(const zp_conv_args& A, const zp_conv_sub& S, const zp_head_args& H,
+                                                f32x4 (&acc)[WC][WP], int p0, int c0, int by, int wc, int wp,
+                                                int lane, int M, uint4* lds) {
+  static_assert(WC % 2 == 0, "paired cout blocks");
+  using MT = MfmaTraits<T>;
+  const int g = lane >> 4, lr = lane & 15;
+  const int GHW = S.OH * S.OW;
+  f32x4 hacc[2][WP];
+#pragma unroll
+  for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+    for (int j = 0; j < WP; ++j) hacc[hb][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const T* W = (const T*)H.w;
+  // head weight fragment: rows hb * 16 + lr, the 8 k of lane group g (k = kbase + perm)
+  auto wfrag = [&](int hb, int k) -> uint4 { return *(const uint4*)(W + (size_t)(hb * 16 + lr) * H.k_pad + k); };
+#pragma unroll
+  for (int i = 0; i < WC; i += 2) {
+    const int cs = c0 + wc * 16 * WC + (i + (g & 1)) * 16 + (g >> 1) * 8;  // this lane's 8 channels
+    float sc[8], sh[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      sc[r] = S.scale ? S.scale[cs + r] : 1.f;
+      sh[r] = S.shift ? S.shift[cs + r] : 0.f;
+    }
+    const uint4 w0 = wfrag(0, cs), w1 = wfrag(1, cs);
+#pragma unroll
+    for (int j = 0; j < WP; ++j) {
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {  // all lanes active (cross-lane op)
+        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][j][r]), __float_as_uint(acc[i + 1][j][r]),
+                                                         false, false);
+        v[r] = __uint_as_float(sw[0]);
+        v[r + 4] = __uint_as_float(sw[1]);
+      }
+      const int p = p0 + wp * 16 * WP + j * 16 + lr;
+      const bool ok = p < M;
+      const size_t pix = ok ? (size_t)p : 0;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) v[r] = v[r] * sc[r] + sh[r];
+      if (A.res) {
+        const uint4 rv = *(const uint4*)((const unsigned short*)A.res + pix * A.ldr + A.cr0 + cs);
+        const uint32_t rw[4] = {rv.x, rv.y, rv.z, rv.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[2 * r] += H16<T>::from(rw[r] & 0xffffu);
+          v[2 * r + 1] += H16<T>::from(rw[r] >> 16);
+        }
+      }
+      if (A.relu) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) v[r] = fmaxf(v[r], 0.f);
+      }
+      uint32_t o[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = ok ? (H16<T>::to(v[2 * r]) | (H16<T>::to(v[2 * r + 1]) << 16)) : 0u;
+      const uint4 xb = make_uint4(o[0], o[1], o[2], o[3]);
+      MT::mma(hacc[0][j], w0, xb);
+      MT::mma(hacc[1][j], w1, xb);
+    }
+  }
+  if (by == 0 && wc == 0) {  // x2 (the skip features, NHWC on the output grid), weights at k = Cout + c
+    for (int q = 0; q < H.C2 / 32; ++q) {
+      const uint4 w0 = wfrag(0, A.Cout + q * 32 + g * 8), w1 = wfrag(1, A.Cout + q * 32 + g * 8);
+#pragma unroll
+      for (int j = 0; j < WP; ++j) {
+        const int p = p0 + wp * 16 * WP + j * 16 + lr;
+        const uint4 xq = p < M ? *(const uint4*)((const unsigned short*)H.x2 + (size_t)p * H.ldx2 + H.cx20 + q * 32 + g * 8)
+                               : make_uint4(0u, 0u, 0u, 0u);
+        MT::mma(hacc[0][j], w0, xq);
+        MT::mma(hacc[1][j], w1, xq);
+      }
+    }
+  }
+  // the wave rows' sums meet in LDS (free: every wave passed the main loop's last barrier)
+  f32x4* red = (f32x4*)lds;  // [wp][hb][j][lane]
+  if (wc != 0) {
+#pragma unroll
+    for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+      for (int j = 0; j < WP; ++j) red[((wp * 2 + hb) * WP + j) * 64 + lane] = hacc[hb][j];
+  }
+  __syncthreads();
+  if (wc != 0) return;
+#pragma unroll
+  for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+    for (int j = 0; j < WP; ++j) {
+      const f32x4 o = red[((wp * 2 + hb) * WP + j) * 64 + lane];
+      const int p = p0 + wp * 16 * WP + j * 16 + lr;
+      if (p >= M) continue;
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const int r = hb * 16 + g * 4 + qq;
+        if (r < H.cout) H.ws[((size_t)by * 32 + r) * M + p] = hacc[hb][j][qq] + o[qq];
+      }
+    }
+  (void)GHW;
+}
+
+// the fused 16-bit head's second launch: mask / code = ws[0] + ws[1] (the two cout tiles, in that
+// order) + bias, f32 NCHW (one thread per output pixel)
+__global__ void k_head_combine16(const float* __restrict__ ws, int M, int GHW, int hcout, const float* __restrict__ bias,
+                                 float* __restrict__ mask, float* __restrict__ code) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= M) return;
+  const int n = p / GHW, sp = p - n * GHW;
+  for (int r = 0; r < hcout; ++r) {
+    const float v = (ws[(size_t)r * M + p] + ws[((size_t)32 + r) * M + p]) + (bias ? bias[r] : 0.f);
+    if (r == 0) mask[(size_t)n * GHW + sp] = v;
+    else code[((size_t)n * (hcout - 1) + (r - 1)) * GHW + sp] = v;
   }
 }
 
@@ -2514,10 +2648,11 @@ extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
                  zp_conv2d_stat_parts(&a));
     const int fl = conv_flags();
     if (fl & 64) {  // k_conv_strip2 (lean main loop); flags & 32: strip DMA spread over the group
-#define ZP_STRIP2(T, WC)                                                                           \
-  if (fl & 256) hipLaunchKernelGGL((k_conv_strip2<T, WC, 5, 2>), grid, dim3(512), 0, st, a, sg, fl); \
-  else if (fl & 32) hipLaunchKernelGGL((k_conv_strip2<T, WC, 5, 1>), grid, dim3(512), 0, st, a, sg, fl); \
-  else hipLaunchKernelGGL((k_conv_strip2<T, WC, 5, 0>), grid, dim3(512), 0, st, a, sg, fl);
+      const zp_head_args H0{};
+#define ZP_STRIP2(T, WC)                                                                               \
+  if (fl & 256) hipLaunchKernelGGL((k_conv_strip2<T, WC, 5, 2>), grid, dim3(512), 0, st, a, sg, fl, H0); \
+  else if (fl & 32) hipLaunchKernelGGL((k_conv_strip2<T, WC, 5, 1>), grid, dim3(512), 0, st, a, sg, fl, H0); \
+  else hipLaunchKernelGGL((k_conv_strip2<T, WC, 5, 0>), grid, dim3(512), 0, st, a, sg, fl, H0);
       if (a.dtype == ZP_F16) {
         if (tc == 64) { ZP_STRIP2(f16_t, 2) } else { ZP_STRIP2(f16_t, 4) }
       } else {
@@ -2765,15 +2900,61 @@ extern "C" int zp_conv2d_stat_parts(const zp_conv_args* a) {
   return (conv_tp(*a) / 64) * zp_conv2d_grid(a) * a->nsub;
 }
 
+// the 16-bit fused head: a 3x3 stride-1 conv on the 128-channel strip tile (k_conv_strip2, two cout
+// tiles for Cout 256)
+static bool head16_ok(const zp_conv_args& a) {
+  if ((a.dtype != ZP_BF16 && a.dtype != ZP_F16) || a.nsub != 1 || a.Cout != 256 || a.out_mode != ZP_OUT_NHWC ||
+      a.stats || !(conv_flags() & 64))
+    return false;
+  if (a.res && (a.ldr % 8 != 0 || a.cr0 % 8 != 0)) return false;
+  return strip_eligible(a, nullptr) && conv_tc(a) == 128;
+}
+
 extern "C" int zp_conv2d_head_ok(const zp_conv_args* a) {
-  return a && a->dtype == ZP_F32H2 && a->nsub == 1 && a->Cout == 256 && a->out_mode == ZP_OUT_NHWC &&
+  if (!a) return 0;
+  if (a->dtype == ZP_BF16 || a->dtype == ZP_F16) return head16_ok(*a);
+  return a->dtype == ZP_F32H2 && a->nsub == 1 && a->Cout == 256 && a->out_mode == ZP_OUT_NHWC &&
          conv3_tc(*a) == 256 && conv3w_tp(*a) == 256 && conv3w_splitk(*a) == 1;
+}
+
+extern "C" long long zp_conv2d_head_ws(const zp_conv_args* a) {
+  if (!a || !(a->dtype == ZP_BF16 || a->dtype == ZP_F16)) return 0;
+  return 2LL * 32 * (long long)a->N * a->GH * a->GW * 4;
 }
 
 extern "C" int zp_conv2d_head(const zp_conv_args* a, const zp_head_args* h, void* stream) {
   ZP_CHECK_ARG(a && h, "zp_conv2d_head: null args");
   ZP_CHECK_ARG(zp_conv2d_head_ok(a), "zp_conv2d_head: not a fused-head geometry (zp_conv2d_head_ok)");
-  return conv3_launch(*a, (hipStream_t)stream, conv_flags(), h);
+  if (a->dtype == ZP_F32H2) return conv3_launch(*a, (hipStream_t)stream, conv_flags(), h);
+  // ZP_BF16 / ZP_F16: the strip kernel with the head epilogue, then the cout tiles' combine
+  const zp_conv_args& A = *a;
+  ZP_CHECK_ARG(h->w && h->mask && (h->code || h->cout == 1) && h->cout >= 1 && h->cout <= 32 && h->ws,
+               "zp_conv2d_head: bad head (16-bit: needs ws, zp_conv2d_head_ws bytes)");
+  ZP_CHECK_ARG(h->C2 >= 0 && h->C2 % 32 == 0 && h->k_pad % 8 == 0 && h->k_pad >= A.Cout + h->C2,
+               "zp_conv2d_head: C2 %d / k_pad %d", h->C2, h->k_pad);
+  ZP_CHECK_ARG(h->C2 == 0 || (h->x2 && h->ldx2 % 8 == 0 && h->cx20 % 8 == 0 && h->ldx2 >= h->cx20 + h->C2),
+               "zp_conv2d_head: x2 layout");
+  ZP_CHECK_ARG(A.Cin > 0 && A.Cin % 64 == 0 && A.ldx >= A.cx0 + A.Cin && A.cx0 % 8 == 0 && A.ldx % 8 == 0 &&
+                   A.k_pad % 64 == 0 && A.w_rows % 128 == 0 && A.w_rows >= A.Cout && A.sub[0].w && A.sub[0].ntaps == 9,
+               "zp_conv2d_head: conv operands");
+  ZP_CHECK_ARG(A.sub[0].OH == A.GH && A.sub[0].OW == A.GW, "zp_conv2d_head: output grid");
+  const long long xb = (long long)A.N * A.IH * A.IW * A.ldx * 2, wb = (long long)A.w_rows * A.k_pad * 2;
+  ZP_CHECK_ARG(xb < (1ll << 31) && wb < (1ll << 31), "zp_conv2d_head: input / weights must stay below 2 GiB");
+  strip_geo sg{};
+  ZP_CHECK_ARG(strip_eligible(A, &sg), "zp_conv2d_head: not a strip geometry");
+  sg.x_bytes = (unsigned)xb;
+  sg.w_bytes = (unsigned)wb;
+  hipStream_t st = (hipStream_t)stream;
+  const int fl = conv_flags();
+  const dim3 grid((unsigned)(((long)A.N * A.GH * A.GW) / 256), 2u, 1u);
+  if (A.dtype == ZP_F16) hipLaunchKernelGGL((k_conv_strip2<f16_t, 4, 5, 2, true>), grid, dim3(512), 0, st, A, sg, fl, *h);
+  else hipLaunchKernelGGL((k_conv_strip2<bf16_t, 4, 5, 2, true>), grid, dim3(512), 0, st, A, sg, fl, *h);
+  ZP_LAUNCH_CHECK("zp_conv2d_head (16-bit conv + head partials)");
+  const int M = A.N * A.GH * A.GW;
+  hipLaunchKernelGGL(k_head_combine16, dim3((M + 255) / 256), dim3(256), 0, st, h->ws, M, A.GH * A.GW, h->cout, h->bias,
+                     h->mask, h->code);
+  ZP_LAUNCH_CHECK("zp_conv2d_head (combine)");
+  return ZP_OK;
 }
 
 /* launch configuration zp_conv2d picks for these args (for kernel labels in reports) */

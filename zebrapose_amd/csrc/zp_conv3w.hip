@@ -43,6 +43,7 @@ namespace zp {
 constexpr int ACC_FLUSH = 0;  // k_conv3's: correction accumulator flushed per step by a scaled FMA
 constexpr int ACC_SA = 1;     // one scaled accumulator (round 4): biased, see the numerics note
 constexpr int ACC_PS = 2;     // per-step partial from zero, added by a rounding v_add_f32 (round 5)
+constexpr int ACC_FS = 3;     // ACC_FLUSH with acc on the 2^11 scale: the flush is a plain v_add_f32
 
 __device__ __forceinline__ void wbarrier() {
   __builtin_amdgcn_s_barrier();
@@ -78,7 +79,7 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
   constexpr int TC = 256, TP = TPX;
   static_assert(TP == 256 || TP == 128, "pixel tile");
   static_assert(TP == 256 || (!HEAD && !BF && DM == 1), "the 256 x 128 tile: plain epilogue, default DMA order");
-  constexpr bool SA = NUM != ACC_FLUSH;              // accumulators on the 2^11 scale (NUM 1, 2)
+  constexpr bool SA = NUM != ACC_FLUSH;              // accumulators on the 2^11 scale (NUM 1, 2, 3)
   constexpr int NTW = TC / 16, NT = (TC + TP) / 16;  // weight tiles / all tiles per plane (16 rows each)
   constexpr int UNITS = NPL * NT;                    // 1 KB DMA units per stage
   constexpr int WC = 8, WP = TP / 64;                // per wave: 8 cout blocks x 4 (TP 128: 2) pixel blocks
@@ -305,7 +306,7 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
   auto flush = [&](f32x4 (&a)[WP], const f32x4 (&c)[WP]) {
 #pragma unroll
     for (int j = 0; j < WP; ++j) {
-      if constexpr (NUM == ACC_PS) {
+      if constexpr (NUM == ACC_PS || NUM == ACC_FS) {
         // (rebuilt as a whole vector: element-wise updates of a[j] spilled 130+ VGPRs, and a vector
         // add becomes v_pk_add_f32, which costs ~13 cycles more than two v_add_f32 beside MFMAs)
         const f32x4 t = {a[j].x + c[j].x, a[j].y + c[j].y, a[j].z + c[j].z, a[j].w + c[j].w};
@@ -395,7 +396,7 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
           MT::mma(c2[j], af[i % 3][1], bf[0][j]);
         }
       }
-      if constexpr (SA && !abl_mfma) {
+      if constexpr ((NUM == ACC_SA || NUM == ACC_PS) && !abl_mfma) {
 #pragma unroll
         for (int j = 0; j < WP; ++j) {
           if constexpr (NUM == ACC_SA) MT::mma(acc[i][j], af[i % 3][0], bf[1][j]);
@@ -418,13 +419,15 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
           MT::mma(acc[i][j], hs, bf[0][j]);
         } else if constexpr (NUM == ACC_PS) {
           MT::mma(c2[j], af[i % 3][1], bf[0][j]);
+        } else if constexpr (NUM == ACC_FS) {
+          MT::mma(acc[i][j], hs, bf[0][j]);
         } else {
           MT::mma(acc[i][j], af[i % 3][0], bf[0][j]);
         }
       }
       if constexpr (NUM == ACC_PS) flush(acc[i], c2);  // (the same block: the other wave's MFMAs cover the wait)
-      if constexpr (NUM == ACC_FLUSH && i > 0) flush(acc[i - 1], c2p);
-      if constexpr (NUM == ACC_FLUSH) {
+      if constexpr ((NUM == ACC_FLUSH || NUM == ACC_FS) && i > 0) flush(acc[i - 1], c2p);
+      if constexpr (NUM == ACC_FLUSH || NUM == ACC_FS) {
 #pragma unroll
         for (int j = 0; j < WP; ++j) c2p[j] = c2[j];
       }
@@ -437,7 +440,7 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
       }
       __builtin_amdgcn_sched_barrier(0);
     });
-    if constexpr (NUM == ACC_FLUSH) flush(acc[WC - 1], c2p);
+    if constexpr (NUM == ACC_FLUSH || NUM == ACC_FS) flush(acc[WC - 1], c2p);
   };
 
   // prologue: step 0's DMA into buffer 0 (STR: and group 0's strip into strip stage 0)
@@ -754,7 +757,7 @@ int conv3w_tp128_mode(int v) {
 static int conv3w_acc() {
   static const int env = getenv("ZP_CONV3W_ACC") ? atoi(getenv("ZP_CONV3W_ACC")) : ACC_FLUSH;
   const int v = g_conv3w_acc >= 0 ? g_conv3w_acc : env;
-  return (v == ACC_PS || v == ACC_SA) ? v : ACC_FLUSH;
+  return (v == ACC_PS || v == ACC_SA || v == ACC_FS) ? v : ACC_FLUSH;
 }
 static bool conv3w_tp128_on() {
   static const int env = getenv("ZP_CONV3W_TP128") ? atoi(getenv("ZP_CONV3W_TP128")) : 0;
@@ -906,6 +909,9 @@ void conv3w_launch(const zp_conv_args& a0, const conv_taps& tg0, hipStream_t st,
   } else if (acc == ACC_PS) {  // per-step partial sums (A/B)
     if (str) hipLaunchKernelGGL((k_conv3w<0, 1, false, false, false, false, true, ACC_PS>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
     else hipLaunchKernelGGL((k_conv3w<0, 1, false, false, false, false, false, ACC_PS>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
+  } else if (acc == ACC_FS) {  // the flushed form on the 2^11 scale
+    if (str) hipLaunchKernelGGL((k_conv3w<0, 1, false, false, false, false, true, ACC_FS>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
+    else hipLaunchKernelGGL((k_conv3w<0, 1, false, false, false, false, false, ACC_FS>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
   } else if (str)  // the default: k_conv3's flushed correction accumulator (bit-identical to k_conv3<h2>)
     hipLaunchKernelGGL((k_conv3w<0, 1, false, false, false, false, true>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
   else hipLaunchKernelGGL((k_conv3w<0, 1, false>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
@@ -918,9 +924,9 @@ void conv3w_head_launch(const zp_conv_args& a, const conv_taps& tg, const zp_hea
   if (acc == ACC_SA) {  // (A/B)
     if (str) hipLaunchKernelGGL((k_conv3w<0, 1, true, false, false, false, true, ACC_SA>), grid, dim3(512), 0, st, a, tg, fl, h, nullptr, 1);
     else hipLaunchKernelGGL((k_conv3w<0, 1, true, false, false, false, false, ACC_SA>), grid, dim3(512), 0, st, a, tg, fl, h, nullptr, 1);
-  } else if (acc == ACC_PS) {  // (A/B)
-    if (str) hipLaunchKernelGGL((k_conv3w<0, 1, true, false, false, false, true, ACC_PS>), grid, dim3(512), 0, st, a, tg, fl, h, nullptr, 1);
-    else hipLaunchKernelGGL((k_conv3w<0, 1, true, false, false, false, false, ACC_PS>), grid, dim3(512), 0, st, a, tg, fl, h, nullptr, 1);
+  } else if (acc == ACC_FS) {
+    if (str) hipLaunchKernelGGL((k_conv3w<0, 1, true, false, false, false, true, ACC_FS>), grid, dim3(512), 0, st, a, tg, fl, h, nullptr, 1);
+    else hipLaunchKernelGGL((k_conv3w<0, 1, true, false, false, false, false, ACC_FS>), grid, dim3(512), 0, st, a, tg, fl, h, nullptr, 1);
   } else if (str) {
     hipLaunchKernelGGL((k_conv3w<0, 1, true, false, false, false, true>), grid, dim3(512), 0, st, a, tg, fl, h, nullptr, 1);
   } else {

@@ -344,7 +344,7 @@ class Engine:
             kname = self._kname(a, plan, x, dt)
             if head is not None:
                 flops += head[1]
-                kname = kname.replace("k_conv3w<", "k_conv3w_head<")
+                kname = kname.replace("k_conv3w<", "k_conv3w_head<").replace("k_conv_strip2<", "k_conv_strip2_head<")
             geo = (f"{label}:{x.C}->{cout} taps{max(len(sb.taps) for sb in plan.subs)} "
                    f"{x.H}x{x.W}->{plan.GH}x{plan.GW}x{a.nsub}")
             # algorithmic HBM bytes: the input slice and every output read / written once, the
@@ -539,14 +539,20 @@ class Engine:
             self.trace.append(("head", unit, x, (mask, code), None))
 
     def head_fusable(self, B, H, W):
-        """True when the two-plane engine runs up2's last conv and the 1x1 head as one launch
-        (zp_conv2d_head): eval forward, no trace, and the 256 x 256 tile eligible at this grid."""
-        if self.dt != L.ZP_F32H2 or not self.fuse_head or self.trace is not None:
+        """True when up2's last conv (3x3, 256 -> 256) and the 1x1 head run fused (zp_conv2d_head):
+        eval forward, no trace, and -- two-plane engine -- the 256 x 256 tile eligible at this grid, or
+        -- bf16 / fp16 -- the strip tile (conv + per-cout-tile head partials, then their combine)."""
+        if self.dt not in (L.ZP_F32H2, L.ZP_BF16, L.ZP_F16) or not self.fuse_head or self.trace is not None:
             return False
         a = L.ConvArgs()
-        a.dtype, a.Cin, a.Cout, a.w_rows, a.N, a.GH, a.GW = L.ZP_F32H2, 256, 256, 256, B, H, W
+        a.dtype, a.Cin, a.Cout, a.N, a.GH, a.GW, a.IH, a.IW = self.dt, 256, 256, B, H, W, H, W
+        a.w_rows = int(L.lib.zp_conv_rows_pad(256))
+        a.ldx, a.cx0, a.sy, a.sx, a.k_pad = 256, 0, 1, 1, 9 * 256
         a.out_mode, a.nsub = L.ZP_OUT_NHWC, 1
-        a.sub[0].ldy, a.sub[0].cy0 = 256, 0
+        s = a.sub[0]
+        s.ldy, s.cy0, s.OH, s.OW, s.oys, s.oxs, s.ntaps = 256, 0, H, W, 1, 1, 9
+        for t in range(9):
+            s.ty[t], s.tx[t] = t // 3 - 1, t % 3 - 1
         return bool(L.lib.zp_conv2d_head_ok(C.byref(a)))
 
     def unit_fwd_head(self, unit, x: Act, head_unit, x2: Act, mask, code):
@@ -565,11 +571,16 @@ class Engine:
         h.x2, h.ldx2, h.cx20, h.C2 = x2.ptr, x2.ld, x2.c0, x2.C
         h.mask, h.code = mask.data_ptr(), L.ptr(code)
         B = x.B
+        hws = None
+        if self.dt in (L.ZP_BF16, L.ZP_F16):  # the cout tiles' head partials (zp_conv2d_head_ws)
+            hws = torch.empty(2 * 32 * B * OH * OW, dtype=torch.float32, device=x.buf.device)
+            h.ws = hws.data_ptr()
         hflops = 2.0 * B * OH * OW * head_unit.cin * head_unit.cout
         hbytes = B * OH * OW * (x2.C * _ES[self.dt] + head_unit.cout * 4) + hw.numel() * hw.element_size()
         outs = [(mask.data_ptr(), 256, 0, OH, OW, scale, shift, None)]  # (y: never written by the fused launch)
         self._conv(x, plan, unit.cout, ws, kp, rows, outs, None, unit.relu, label="upconv+head",
                    head=(h, hflops, hbytes))
+        del hws  # (the partials buffer's block returns to the stream's pool: the launches are enqueued)
 
     # ------------------------------------------------------------------ backward pieces
     def _grad_buf(self, gmap, act: Act):
