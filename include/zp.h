@@ -160,7 +160,11 @@ long long zp_conv2d_split_ws(const zp_conv_args* a);
  * split-fp32 strip kernel k_conv3s (0 off, 1 64-channel tiles, 2 also 128-channel tiles; -1 =
  * ZP_CONV3_STRIP or the default 1); key 8 = the fewest workgroups a split-fp32 launch runs
  * 128-channel tiles with (fewer: 64-channel tiles); key 9 = split-K of small split-fp32 launches
- * (default 1, 0 off).  Returns the previous value, -1 for an unknown key. */
+ * (default 1, 0 off); keys 10-12 = the 256 x 256 two-plane tile (on / fewest workgroups / split-K);
+ * key 13 = its accumulation form (0 the flushed correction accumulator, default; 1 one scaled
+ * accumulator; 2 per-step partial sums; 3 flushed on the 2^11 scale); key 14 = its 256 x 128 tile
+ * (default 0); key 15 = zp_bn_train_finalize's merge in one launch (1, default) or two (0).  Returns
+ * the previous value, -1 for an unknown key. */
 int zp_conv_tuning(int key, int value);
 
 /* Fused 1x1 head (the reference's conv_1x1_4 over torch.cat([x, x_128]) and the mask / code split,
@@ -288,10 +292,12 @@ int zp_im2col_split(const float* x, int B, int H, int W, int ldx, int C, int k, 
                     int kpad, int dtype, void* y, void* stream);
 /* The stem conv of the two-plane engine in one launch (ZP_F32H2 only): torchvision conv1 (7x7,
  * stride 2, pad 3, 3 -> 64 channels; reference model/resnet.py:195) + folded BN (scale, shift) +
- * ReLU, from the f32 NHWC image x [B][H][W][ldx] (channels 0..2; ldx a multiple of 4) to a ZP_F32H2
- * NHWC slice y [2][B][OH][OW][ldy] at channel cy0.  Weights: zp_pack_weight of the 7x7 kernel in
- * the zp_im2col_split order (taps row-major, cstride 3, k_pad 160, dtype ZP_F32H2, w_rows >= 64).
- * Replaces zp_im2col_split + the 1x1 split GEMM (no patch tensor).  OW must divide 256. */
+ * ReLU, from the f32 image x -- ldx == 0: NCHW [B][3][H][W], the reference's input tensor
+ * (bop_dataset_pytorch.py:345; no zp_nchw_to_nhwc copy); else NHWC [B][H][W][ldx] (channels 0..2, ldx a
+ * multiple of 4) -- to a ZP_F32H2 NHWC slice y [2][B][OH][OW][ldy] at channel cy0.  Weights:
+ * zp_pack_weight of the 7x7 kernel in the zp_im2col_split order (taps row-major, cstride 3, k_pad 160,
+ * dtype ZP_F32H2, w_rows >= 64).  Replaces zp_im2col_split + the 1x1 split GEMM (no patch tensor).
+ * OW must divide 256 and be <= 128. */
 int zp_stem_split(const float* x, int B, int H, int W, int ldx, const void* w, int w_rows, int k_pad,
                   const float* scale, const float* shift, int dtype, void* y, int ldy, int cy0, int OH, int OW,
                   void* stream);

@@ -65,3 +65,48 @@ def test_bn_backward_mask_from_raw_matches_stored_mask(dt, P, Cc):
     yk = y.float().cpu() > 0
     mk = (torch.addcmul(shift, rf, scale) > 0).cpu()  # fma form
     assert float((yk != mk).float().mean()) < 1e-3
+
+
+@pytest.mark.parametrize("parts,C", [(8192, 64), (4100, 256), (200, 96), (1024, 2048)])
+def test_bn_stat_merge_one_launch_equals_two(gpu, parts, C):
+    """zp_bn_train_finalize's level-1 + level-2 statistics merge in ONE launch (zp_conv_tuning key 15;
+    the last-arriving block of each channel group runs level 2 after an agent-scope counter hand-off)
+    stores exactly the bits of the two-launch form (same parts, same fixed merge order), re-arms its
+    counters (three calls in a row agree), and matches a float64 merge of the same partials (Chan's
+    formula: the train-mode batch mean / biased variance, train_v6.py's BatchNorm2d in training)."""
+    from zebrapose_amd import _lib as L
+    g = torch.Generator().manual_seed(parts + C)
+    cnt = torch.randint(1, 33, (parts, C), generator=g).float()
+    mean = torch.randn(parts, C, generator=g) * 3 + 1
+    m2 = torch.rand(parts, C, generator=g) * cnt * 2
+    base = torch.cat([cnt, mean, m2]).contiguous()
+    gamma, beta = torch.rand(C, generator=g) + 0.5, torch.randn(C, generator=g)
+
+    def run(mode):
+        old = L.lib.zp_conv_tuning(15, mode)
+        try:
+            part = base.clone().to(gpu)
+            rm, rv = torch.zeros(C, device=gpu), torch.ones(C, device=gpu)
+            nbt = torch.zeros(1, dtype=torch.int64, device=gpu)
+            sc, sh = torch.empty(C, device=gpu), torch.empty(C, device=gpu)
+            save = torch.empty(4 * C, device=gpu)
+            L.call("zp_bn_train_finalize", part.data_ptr(), parts, C, int(cnt.sum()), 1e-5, 0.1,
+                   gamma.to(gpu).data_ptr(), beta.to(gpu).data_ptr(), None, rm.data_ptr(), rv.data_ptr(), nbt.data_ptr(),
+                   sc.data_ptr(), sh.data_ptr(), save.data_ptr(), L.stream_ptr())
+            torch.cuda.synchronize()
+            return [t.cpu() for t in (sc, sh, save, rm, rv, nbt)]
+        finally:
+            L.lib.zp_conv_tuning(15, old)
+    two = run(0)
+    ones = [run(1) for _ in range(3)]
+    for one in ones:
+        for a, b in zip(one, two):
+            assert torch.equal(a, b)
+    c64, m64, q64 = cnt.double(), mean.double(), m2.double()
+    n = c64.sum(0)
+    mu = (c64 * m64).sum(0) / n
+    var = (q64.sum(0) + (c64 * (m64 - mu) ** 2).sum(0)) / n
+    got_mean, got_inv = two[2][:C].double(), two[2][C:2 * C].double()
+    assert torch.allclose(got_mean, mu, rtol=1e-6, atol=1e-6)
+    assert torch.allclose(got_inv, 1.0 / torch.sqrt(var + 1e-5), rtol=1e-6)
+    assert int(two[5][0]) == 1

@@ -103,6 +103,8 @@ __device__ __forceinline__ void raise_range_flag(unsigned* flag, bool bad) {
 // the word registered for the calling thread's current device (NULL: no guard); read by the host
 // launch code of every split store (a captured hipGraph keeps the pointer of its capture)
 unsigned* range_flag();
+// zp_conv_tuning key 15 (zp_misc.hip): the train-mode BN statistics merge in one launch (1) or two (0)
+int bn_fused_mode(int v);
 
 template <typename T> struct Elem;
 template <> struct Elem<float> {

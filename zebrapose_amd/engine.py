@@ -58,6 +58,12 @@ class Act:
     ptr = property(lambda s: s.buf.data_ptr())
 
 
+class NchwInput(Act):
+    """The f32 NCHW input [B, 3, H, W] seen as the stem's (8-channel) NHWC input: ld 0 tells
+    zp_stem_split to read the NCHW tensor itself (include/zp.h)."""
+    ld = property(lambda s: 0)
+
+
 def joined(buf):
     """The f32 values of an activation buffer: itself, or -- for a split engine's plane-0 view --
     (hi + mid) + lo of a [3, ...] bf16 tensor (exact, include/zp.h ZP_F32X3), or hi + lo * 2^-11 of a
@@ -424,7 +430,7 @@ class Engine:
             cr = unit.conv.weight.shape[1]
             kp = G.ceil_to(unit.k * unit.k * cr, 32)
             if (self.dt == L.ZP_F32H2 and self.stem_direct and (unit.k, unit.s, unit.p, cr, unit.cout) == (7, 2, 3, 3, 64)
-                    and OW <= 256 and 256 % OW == 0 and (OH * OW) % 256 == 0 and out.ld % 8 == 0 and out.c0 % 8 == 0
+                    and OW <= 128 and 256 % OW == 0 and (OH * OW) % 256 == 0 and out.ld % 8 == 0 and out.c0 % 8 == 0
                     and x.ld % 4 == 0):
                 # one launch from the f32 image (zp_stem_split): no patch tensor
                 taps = [(ky, kx) for ky in range(unit.k) for kx in range(unit.k)]
@@ -435,7 +441,7 @@ class Engine:
                        shift.data_ptr(), self.dt, out.ptr, out.ld, out.c0, OH, OW, L.stream_ptr())
                 if self.stage_log is not None:
                     fl = 2.0 * x.B * OH * OW * unit.k * unit.k * cr * unit.cout
-                    nb = x.P * x.ld * 4 + x.B * OH * OW * unit.cout * 4 + w.numel() * w.element_size()
+                    nb = x.P * (x.ld or 3) * 4 + x.B * OH * OW * unit.cout * 4 + w.numel() * w.element_size()
                     self.stage_log.append((self.stage, "k_stem_h2", fl, nb, f"{label}:{cr}->{unit.cout} 7x7s2"))
                 self._probe("k_stem_h2")
                 if self.trace is not None:
@@ -537,6 +543,12 @@ class Engine:
             tape.recs.append(("head", unit, x, key, None, None, None))
         elif self.trace is not None:
             self.trace.append(("head", unit, x, (mask, code), None))
+
+    def nchw_stem(self, B, H, W, tape):
+        """True when the two-plane stem (zp_stem_split) reads the f32 NCHW input directly: eval, no
+        trace (the teacher-forced replays start from the NHWC copy), output width <= 128."""
+        return (self.dt == L.ZP_F32H2 and self.stem_direct and tape is None and self.trace is None
+                and W // 2 <= 128 and 256 % (W // 2) == 0 and ((H // 2) * (W // 2)) % 256 == 0)
 
     def head_fusable(self, B, H, W):
         """True when up2's last conv (3x3, 256 -> 256) and the 1x1 head run fused (zp_conv2d_head):
@@ -863,7 +875,9 @@ class Engine:
         self._prepack(dev)
         st = L.stream_ptr()
         self.stage = "stem"
-        if self.x3:  # the stem reads f32 (exact-f32 small-Cin kernel) and writes split output
+        if self.nchw_stem(B, H, W, tape):  # zp_stem_split reads the NCHW input itself (ldx 0)
+            xin = NchwInput(x.permute(0, 2, 3, 1), 0, 8)
+        elif self.x3:  # the stem reads f32 (exact-f32 small-Cin kernel) and writes split output
             xin = Act(torch.empty((B, H, W, 8), dtype=torch.float32, device=dev))
             L.call("zp_nchw_to_nhwc", x.data_ptr(), B, 3, H, W, 8, L.ZP_F32, xin.ptr, st)
         else:
