@@ -412,21 +412,33 @@ __global__ void __launch_bounds__(128 * NWP) k_conv3(const zp_conv_args A, const
   static_assert(((NPL - 1) * NT + WC + 3) * 1024 < 65536, "ds_read immediate range");
   // split-K (nsplit > 1): blockIdx.z = sub * nsplit + K slice; the slice's raw f32 sums go to ws
   // [nsub][nsplit][M][Cout] and k_splitk_epi finishes them
-  const int tb = (int)blockIdx.z / nsplit, kz = (int)blockIdx.z - tb * nsplit;
-  const zp_conv_sub& S = A.sub[tb];
+  int tb = (int)blockIdx.z / nsplit;
+  const int kz = (int)blockIdx.z - tb * nsplit;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wc = wid / NWP, wp = wid % NWP;
   const int GHW = A.GH * A.GW;
   const int M = A.N * GHW;
   int bx = blockIdx.x, by = blockIdx.y;
-  if (flags & 2) {  // XCD-aware order (k_conv): the cout tiles of a pixel tile meet in one L2
-    const int total = gridDim.x * gridDim.y;
+  const int total = gridDim.x * gridDim.y;
+  if ((flags & 1048576) && nsplit == 1 && A.nsub > 1 && (total & 7) == 0) {
+    // several sub-problems over one input (the merged ASPP's four branches, zp_conv_tuning key 16,
+    // off by default: see g_subint): the subs of a tile are dispatched next to each other on one
+    // XCD (dispatch id % 8 picks the XCD), so the input rows they all read meet in that XCD's L2
+    const int gid = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const int q = gid >> 3;
+    tb = q % A.nsub;
+    const int tile = (gid & 7) * (total >> 3) + q / A.nsub;
+    bx = tile / gridDim.y;
+    by = tile - bx * gridDim.y;
+  } else if (flags & 2) {  // XCD-aware order (k_conv): the cout tiles of a pixel tile meet in one L2
     const int bid = blockIdx.x + gridDim.x * blockIdx.y;
     const int lin = (total & 7) ? bid : (bid & 7) * (total >> 3) + (bid >> 3);
     bx = lin / gridDim.y;
     by = lin - bx * gridDim.y;
   }
+  tb = __builtin_amdgcn_readfirstlane(tb);
+  const zp_conv_sub& S = A.sub[tb];
   const int p0 = bx * TP, c0 = by * TC;
   const int CB = A.Cin / 32;
   const int ny = TG.ny[tb], nx = TG.nx[tb], dty = TG.dty[tb], dtx = TG.dtx[tb];
@@ -1163,6 +1175,16 @@ static bool conv3_strip(const zp_conv_args& a, int tc, strip3_geo* sg) {
 }
 
 static int g_splitk = 1;  // zp_conv_tuning key 9: split-K of small split-fp32 launches (0 off)
+// zp_conv_tuning key 16: interleave the subs of a multi-sub k_conv3 launch (-1: ZP_CONV3_SUBINT or 0).
+// Measured (merged ASPP, bs 32): 585 -> 734 us with it on.  Each 3 x 3 branch's two-plane weights
+// are 4.7 MB, an XCD's whole L2: branch after branch keeps one branch's weights hot, interleaving
+// makes every XCD cycle through all four (x_high, 67 MB, is re-read from the Infinity Cache either way)
+static int g_subint = -1;
+int conv3_subint_mode(int v) {
+  const int old = g_subint;
+  g_subint = v;
+  return old;
+}
 
 int conv3_splitk_mode(int v) {
   const int old = g_splitk;
@@ -1234,6 +1256,8 @@ static void conv3_dispatch(const zp_conv_args& a, const conv_taps& tg, int tc, h
   const int tp = conv3_tp(a, tc);
   const int gx = ceil_div((long)a.N * a.GH * a.GW, tp), gy = ceil_div(a.Cout, tc);
   const dim3 grid(gx, gy, ns * a.nsub);
+  static const int subint_env = getenv("ZP_CONV3_SUBINT") ? atoi(getenv("ZP_CONV3_SUBINT")) : 0;
+  if ((g_subint >= 0 ? g_subint : subint_env) && a.nsub > 1) fl |= 1048576;
   // 128-channel layers: 8 waves, 128 x 256, 2-deep ring (two planes: 3-deep, the same LDS);
   // smaller tiles: register-pipelined one wave per SIMD over 128 pixels (ZP_CONV3_SCHED=1: the
   // 128-channel tile that way too)
