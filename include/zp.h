@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define ZP_ABI_VERSION 2
+#define ZP_ABI_VERSION 3
 
 #define ZP_OK 0
 #define ZP_ERR_ARG 1
@@ -125,6 +125,19 @@ typedef struct zp_conv_args {
                                   (count, mean, centred M2), parts = zp_conv2d_stat_parts() */
   int nsub;
   zp_conv_sub sub[ZP_MAX_SUB];
+  /* ABI 3.  Data-gradient launches (ZP_F32 / ZP_BF16, NHWC, no scale / shift / residual / ReLU / stats):
+   * if bnr_part is non-NULL the launch also takes the reduce of zp_bn_bwd_reduce (relu mode 2) for the
+   * train-mode BatchNorm whose OUTPUT gradient it writes -- g = the stored value, masked by
+   * fma(x, save scale, save shift) > 0, xhat = (x - mean) * invstd -- per stat part:
+   * partials[0][k][c] = sum g, partials[1][k][c] = sum g * xhat over stat part k, in the
+   * [2][parts + 1][Cout] layout of zp_bn_bwd_reduce with parts = zp_conv2d_bnr_parts(); finish with
+   * zp_bn_bwd_totals.
+   * Valid only when this launch is the gradient's only writer (it overwrites every pixel).
+   * Replaces the separate reduce pass of the BN backward (reference model/resnet.py:41-51, autograd
+   * of nn.BatchNorm2d + ReLU) */
+  const void* bnr_x;       /* that BN's raw conv output x [P][Cout] (dtype) */
+  const float* bnr_save;   /* its zp_bn_train_finalize save: mean, invstd, scale, shift ([4][Cout]) */
+  float* bnr_part;
 } zp_conv_args;
 
 int zp_abi_version(void);
@@ -138,6 +151,9 @@ int zp_conv_rows_pad(int Cout);
 int zp_conv2d_grid(const zp_conv_args* a);
 /* number of partial-sum slots `stats` needs: (pixel tile / 64) * grid_x * nsub (one per wave half) */
 int zp_conv2d_stat_parts(const zp_conv_args* a);
+/* number of partial-sum slots a launch with bnr_part emits: zp_conv2d_stat_parts, or one per
+ * 256-pixel tile where the strip kernel sums its wave halves first (ABI 3) */
+int zp_conv2d_bnr_parts(const zp_conv_args* a);
 /* launch configuration zp_conv2d picks: cout tile, pixel tile, LDS ring depth, kernel variant
  * (0 = k_conv, 1 = k_conv_strip: 3x3 stride-1 convs with activation-strip reuse, 2 = k_conv_strip2:
  * the same with the lean main loop, 3 = k_conv_quad: the four phases of a stride-2 transposed
@@ -271,6 +287,12 @@ int zp_bn_bwd_parts(int P, int C);
 int zp_bn_bwd_reduce(const void* dy, int lddy, int cdy0, const void* y, int ldy, int cy0,
                      const void* x, int P, int C, const float* save, int relu, int dtype,
                      float* partials, float* dgamma, float* dbeta, int accumulate, void* stream);
+/* totals of partials [2][parts + 1][C] filled by a zp_conv2d launch with bnr_part (parts =
+ * zp_conv2d_bnr_parts) -> partials[0][out_parts][c], partials[1][out_parts][c] of the [2][out_parts
+ * + 1][C] layout zp_bn_bwd_apply reads (out_parts = zp_bn_bwd_parts(P, C); the buffer holds
+ * [2][max(parts, out_parts) + 1][C]); dgamma / dbeta as zp_bn_bwd_reduce */
+int zp_bn_bwd_totals(float* partials, int parts, int C, int out_parts, float* dgamma, float* dbeta,
+                     int accumulate, void* stream);
 /* dx[p][c] = gamma*invstd*(g - sum_g/P - xhat*sum_gx/P)  (dx dtype, [P][C]); relu as for the
  * reduce (mode 2 needs dx);
  * dres (optional) [p, cdres0+c] = g, or += g if res_accumulate */

@@ -84,6 +84,20 @@ int main() {
   CHECK(zp_mask_loss_ws_bytes(32LL * 128 * 128) > 0);
   CHECK(zp_pose_error_ws_bytes(32, 1000, ZP_METRIC_ADI) >= 0);
   CHECK(zp_bn_bwd_parts(32 * 64 * 64, 64) > 0);
+  // the fused BN backward reduce (ABI 3): refused without its inputs, with a residual or a split dtype
+  zp_conv_args bnr = conv(ZP_BF16, 32, 32, 32, 256, 256, 3, 1);
+  bnr.x = (void*)16; bnr.sub[0].w = (void*)16; bnr.sub[0].y = (void*)16;
+  bnr.bnr_part = (float*)16;
+  CHECK(zp_conv2d(&bnr, NULL) == ZP_ERR_ARG);                        // no bnr_x / bnr_save
+  bnr.bnr_x = (void*)16; bnr.bnr_save = (const float*)16; bnr.res = (void*)16; bnr.ldr = 256;
+  CHECK(zp_conv2d(&bnr, NULL) == ZP_ERR_ARG);                        // residual epilogue
+  zp_conv_args bnr3 = up2;
+  bnr3.bnr_part = (float*)16; bnr3.bnr_x = (void*)16; bnr3.bnr_save = (const float*)16;
+  CHECK(zp_conv2d(&bnr3, NULL) == ZP_ERR_ARG);                       // split-fp32 forms: eval only
+  CHECK(zp_bn_bwd_totals(NULL, 4, 64, 4, NULL, NULL, 0, NULL) == ZP_ERR_ARG);
+  zp_conv_args bnr2 = conv(ZP_BF16, 32, 128, 128, 256, 256, 3, 1);  // strip tile: one part per 256 pixels
+  CHECK(zp_conv2d_bnr_parts(&bnr2) == 32 * 128 * 128 / 256);
+  CHECK(zp_conv2d_bnr_parts(&bnr2) * 4 == zp_conv2d_stat_parts(&bnr2));
   // tuning knobs round-trip; unknown keys answer -1
   const int old = zp_conv_tuning(10, 0);
   CHECK(zp_conv_tuning(10, old) == 0);

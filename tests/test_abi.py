@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
 def test_python_binding_covers_header():
     from zebrapose_amd import _lib
     assert set(_declared()) <= set(_lib._SIGS), set(_declared()) - set(_lib._SIGS)
-    assert _lib.lib.zp_abi_version() == 2
+    assert _lib.lib.zp_abi_version() == 3
 
 
 def test_struct_layout():
@@ -37,7 +37,9 @@ def test_struct_layout():
     # offsets the kernels rely on: sub[] array right after nsub, 8-byte aligned pointers
     assert ctypes.sizeof(_lib.ConvSub) % 8 == 0
     assert _lib.ConvArgs.sub.offset % 8 == 0
-    assert ctypes.sizeof(_lib.ConvArgs) == _lib.ConvArgs.sub.offset + 4 * ctypes.sizeof(_lib.ConvSub)
+    # ABI 3: the fused BN backward reduce's three pointers follow sub[]
+    assert _lib.ConvArgs.bnr_x.offset == _lib.ConvArgs.sub.offset + 4 * ctypes.sizeof(_lib.ConvSub)
+    assert ctypes.sizeof(_lib.ConvArgs) == _lib.ConvArgs.bnr_x.offset + 3 * 8
     assert ctypes.sizeof(_lib.PackJob) == 16 + 10 * 4 + 2 * 64  # zp_pack_job (include/zp.h)
 
 

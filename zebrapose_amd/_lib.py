@@ -38,7 +38,8 @@ class ConvArgs(C.Structure):
                 ("N", i32), ("GH", i32), ("GW", i32), ("sy", i32), ("sx", i32),
                 ("Cout", i32), ("k_pad", i32), ("w_rows", i32),
                 ("res", vp), ("ldr", i32), ("cr0", i32), ("relu", i32), ("out_mode", i32),
-                ("stats", vp), ("nsub", i32), ("sub", ConvSub * MAX_SUB)]
+                ("stats", vp), ("nsub", i32), ("sub", ConvSub * MAX_SUB),
+                ("bnr_x", vp), ("bnr_save", vp), ("bnr_part", vp)]
 
 
 class WgradSub(C.Structure):
@@ -74,6 +75,7 @@ _SIGS = {
     "zp_conv_rows_pad": (i32, [i32]),
     "zp_conv2d_grid": (i32, [C.POINTER(ConvArgs)]),
     "zp_conv2d_stat_parts": (i32, [C.POINTER(ConvArgs)]),
+    "zp_conv2d_bnr_parts": (i32, [C.POINTER(ConvArgs)]),
     "zp_conv2d_split_ws": (C.c_longlong, [C.POINTER(ConvArgs)]),
     "zp_pack_weight": (i32, [vp, i32, i32, i32, i32, i32, i32, C.POINTER(i32), C.POINTER(i32), i32, i32, vp, i32,
                              i32, vp]),
@@ -84,6 +86,7 @@ _SIGS = {
     "zp_bn_apply": (i32, [vp, i32, i32, vp, vp, vp, i32, i32, i32, i32, vp, i32, i32, vp]),
     "zp_bn_bwd_parts": (i32, [i32, i32]),
     "zp_bn_bwd_reduce": (i32, [vp, i32, i32, vp, i32, i32, vp, i32, i32, vp, i32, i32, vp, vp, vp, i32, vp]),
+    "zp_bn_bwd_totals": (i32, [vp, i32, i32, i32, vp, vp, i32, vp]),
     "zp_bn_bwd_apply": (i32, [vp, i32, i32, vp, i32, i32, vp, i32, i32, vp, vp, vp, i32, i32, vp, vp, i32, i32, i32,
                               vp]),
     "zp_nchw_to_nhwc": (i32, [vp, i32, i32, i32, i32, i32, i32, vp, vp]),
@@ -142,7 +145,7 @@ def _load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.zp_abi_version() != 2:
+    if lib.zp_abi_version() != 3:
         raise ImportError("libzp.so ABI version mismatch")
     return lib
 

@@ -33,11 +33,11 @@ __device__ uint4 g_zero_page[8];
 
 // Conv epilogue shared by k_conv and k_conv_strip: BN scale/shift (+bias), residual, ReLU,
 // NHWC (channel slice) / NCHW-head / f32 stores, or train-mode BN partial statistics.
-template <typename T, int WC, int WP, int NWP>
+template <typename T, int WC, int WP, int NWP, bool BNR = false>
 __device__ __forceinline__ void conv_epilogue(const zp_conv_args& A, const zp_conv_sub& S, f32x4 (&acc)[WC][WP],
                                               const int p0, const int c0, const int wc, const int wp, const int lane,
                                               const int M, const int GHW, const int bx, const int zi,
-                                              const int nz, unsigned* rflag = nullptr) {
+                                              const int nz, unsigned* rflag = nullptr, float* red = nullptr) {
   // ---------------- epilogue ----------------
   // (zi, nz): this tile's sub-problem and the sub-problem count, for the statistics part index
   // (blockIdx.z / gridDim.z, except in k_conv_quad, whose tiles hold all four sub-pixel phases)
@@ -75,6 +75,13 @@ __device__ __forceinline__ void conv_epilogue(const zp_conv_args& A, const zp_co
       pox[j] = gx * S.oxs + S.oxo;
     }
   }
+  // BNR (k_conv_strip2's bnr instance): the fused BN backward sums (zp.h bnr_*) are taken in the
+  // paired store loop below, on its 8-channel lanes (16-byte raw loads, issued before the pixel loop)
+  constexpr bool BPAIR = BNR && sizeof(T) == 2 && WC % 2 == 0;
+  bool bdone = false;  // the paired loop took them
+  if constexpr (BPAIR) {
+    if (A.bnr_part) __syncthreads();  // red (the kernel's LDS): every wave's main loop has finished reading it
+  }
   bool stored = false;
   if constexpr (sizeof(T) == 2 && WC % 2 == 0) {
     // bf16 NHWC fast path: v_permlane16_swap pairs lane groups (g, g + 1) so that each lane
@@ -106,6 +113,33 @@ __device__ __forceinline__ void conv_epilogue(const zp_conv_args& A, const zp_co
           sh[0] = s0.x; sh[1] = s0.y; sh[2] = s0.z; sh[3] = s0.w;
           sh[4] = s1.x; sh[5] = s1.y; sh[6] = s1.z; sh[7] = s1.w;
         }
+        // BPAIR: this lane's 8 channels' BN terms and the raw x of its WP pixels, loaded up front
+        uint4 bx8[BPAIR ? WP : 1];
+        float bm[8], bi[8], bsc[8], bsh[8], bs0[8], bs1[8];
+        if constexpr (BPAIR) {
+          if (A.bnr_part) {
+#pragma unroll
+            for (int j = 0; j < WP; ++j) {
+              const size_t pix = ((size_t)pn[j] * S.OH + poy[j]) * S.OW + pox[j];
+              bx8[j] = (pok[j] && cok) ? *(const uint4*)((const unsigned short*)A.bnr_x + pix * A.Cout + cs)
+                                       : make_uint4(0u, 0u, 0u, 0u);
+            }
+            float4 q[8];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+              q[2 * t] = cok ? *(const float4*)(A.bnr_save + t * A.Cout + cs) : make_float4(0.f, 0.f, 0.f, 0.f);
+              q[2 * t + 1] = cok ? *(const float4*)(A.bnr_save + t * A.Cout + cs + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+            float* dst[4] = {bm, bi, bsc, bsh};
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+              dst[t][0] = q[2 * t].x; dst[t][1] = q[2 * t].y; dst[t][2] = q[2 * t].z; dst[t][3] = q[2 * t].w;
+              dst[t][4] = q[2 * t + 1].x; dst[t][5] = q[2 * t + 1].y; dst[t][6] = q[2 * t + 1].z; dst[t][7] = q[2 * t + 1].w;
+            }
+#pragma unroll
+            for (int r = 0; r < 8; ++r) bs0[r] = bs1[r] = 0.f;
+          }
+        }
 #pragma unroll
         for (int j = 0; j < WP; ++j) {
           float v[8];
@@ -136,6 +170,19 @@ __device__ __forceinline__ void conv_epilogue(const zp_conv_args& A, const zp_co
           uint32_t o[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) o[r] = H16<T>::to(v[2 * r]) | (H16<T>::to(v[2 * r + 1]) << 16);
+          if constexpr (BPAIR) {
+            if (A.bnr_part) {  // g = the stored gradient; mask and xhat from the raw x (relu mode 2)
+              const uint32_t xw[4] = {bx8[j].x, bx8[j].y, bx8[j].z, bx8[j].w};
+#pragma unroll
+              for (int r = 0; r < 8; ++r) {
+                const float xx = H16<T>::from((r & 1) ? (xw[r >> 1] >> 16) : (xw[r >> 1] & 0xffffu));
+                float g = H16<T>::from((r & 1) ? (o[r >> 1] >> 16) : (o[r >> 1] & 0xffffu));
+                g = __builtin_fmaf(xx, bsc[r], bsh[r]) > 0.f ? g : 0.f;
+                bs0[r] += g;
+                bs1[r] += g * (xx - bm[r]) * bi[r];
+              }
+            }
+          }
           if (ZP_ABL == 6 && o[0] != 0x3f803f80u) continue;  // diagnostic: no stores (unless a value pair is exactly 1, 1)
           if constexpr (ZP_ABL == 8) {  // diagnostic: non-temporal stores
             typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -143,6 +190,26 @@ __device__ __forceinline__ void conv_epilogue(const zp_conv_args& A, const zp_co
             __builtin_nontemporal_store((u32x4){o[0], o[1], o[2], o[3]}, yp);
           } else {
             *(uint4*)((unsigned short*)S.y + pix * S.ldy + S.cy0 + cs) = make_uint4(o[0], o[1], o[2], o[3]);
+          }
+        }
+        if constexpr (BPAIR) {
+          if (A.bnr_part) {
+            bdone = true;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {  // over the 16 pixel lanes of this lane row (all lanes active)
+              bs0[r] = row16_sum(bs0[r]);
+              bs1[r] = row16_sum(bs1[r]);
+            }
+            if ((lane & 15) == 0) {  // red: [wp][sum][channel of the tile] (k_conv_strip2 passes it)
+              const int ct = cs - c0;
+              constexpr int TCB = 32 * WC;
+              float* r0 = red + (wp * 2 + 0) * TCB + ct;
+              float* r1 = red + (wp * 2 + 1) * TCB + ct;
+              *(float4*)r0 = make_float4(bs0[0], bs0[1], bs0[2], bs0[3]);
+              *(float4*)(r0 + 4) = make_float4(bs0[4], bs0[5], bs0[6], bs0[7]);
+              *(float4*)r1 = make_float4(bs1[0], bs1[1], bs1[2], bs1[3]);
+              *(float4*)(r1 + 4) = make_float4(bs1[4], bs1[5], bs1[6], bs1[7]);
+            }
           }
         }
       }
@@ -297,6 +364,102 @@ __device__ __forceinline__ void conv_epilogue(const zp_conv_args& A, const zp_co
           A.stats[((size_t)2 * parts + part) * A.Cout + c] = m2;
         }
       }
+  }
+  if (A.bnr_part) {
+    // Data gradient feeding a train-mode BN + ReLU backward (zp.h bnr_*): per wave half, the sums
+    // zp_bn_bwd_reduce (relu mode 2) takes over the stored gradient g -- masked where the forward's
+    // fma(x, scale, shift) was <= 0 -- and g * xhat, xhat = (x - mean) * invstd of the BN's raw
+    // input x at the same pixel.  The zp_conv2d checks leave no scale / shift / residual / ReLU here:
+    // the stored value is the accumulator (rounded to T).  BPAIR (bdone): the paired store loop
+    // took them into red already; otherwise (k_conv / k_conv_quad dgrads, the f32 parity mode) this
+    // pass, 4 channels per lane, loads issued per channel block before their use.
+    // red (k_conv_strip2: its LDS, free after the main loop): the NWP wave halves of a cout block meet
+    // there and the tile writes one part (zp_conv2d_bnr_parts) -- a quarter of the partials for the
+    // totals pass to read
+    const int parts = red ? gridDim.x * nz : gridDim.x * nz * NWP;
+    const int part = red ? zi * gridDim.x + bx : (zi * gridDim.x + bx) * NWP + wp;
+    constexpr int TCB = 32 * WC;  // channels of the tile's cout block (2 wave rows of 16 * WC)
+    if (!bdone) {
+      if (red) __syncthreads();  // every wave's last main-loop LDS read precedes the writes below
+      const float* sv = A.bnr_save;
+      using XV = typename std::conditional<sizeof(T) == 2, uint2, float4>::type;
+#pragma unroll
+      for (int i = 0; i < WC; ++i) {
+        const int cf = cbase + i * 16;
+        const bool cok = cf < A.Cout;  // (Cout % 4 == 0: all four channels or none)
+        XV xr[WP];
+#pragma unroll
+        for (int j = 0; j < WP; ++j) {
+          const size_t pix = ((size_t)pn[j] * S.OH + poy[j]) * S.OW + pox[j];
+          xr[j] = (pok[j] && cok) ? *(const XV*)((const T*)A.bnr_x + pix * A.Cout + cf) : XV{};
+        }
+        float4 pm[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) pm[q] = cok ? *(const float4*)(sv + q * A.Cout + cf) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float mean[4] = {pm[0].x, pm[0].y, pm[0].z, pm[0].w}, inv[4] = {pm[1].x, pm[1].y, pm[1].z, pm[1].w};
+        const float msc[4] = {pm[2].x, pm[2].y, pm[2].z, pm[2].w}, msh[4] = {pm[3].x, pm[3].y, pm[3].z, pm[3].w};
+        float sg[4] = {0.f, 0.f, 0.f, 0.f}, sgx[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < WP; ++j) {
+          float xx[4];
+          if constexpr (sizeof(T) == 2) {
+            xx[0] = H16<T>::from(xr[j].x & 0xffffu);
+            xx[1] = H16<T>::from(xr[j].x >> 16);
+            xx[2] = H16<T>::from(xr[j].y & 0xffffu);
+            xx[3] = H16<T>::from(xr[j].y >> 16);
+          } else {
+            xx[0] = xr[j].x; xx[1] = xr[j].y; xx[2] = xr[j].z; xx[3] = xr[j].w;
+          }
+          const bool ok = pok[j] && cok;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float g = acc[i][j][r];
+            if (sizeof(T) == 2 && A.out_mode != ZP_OUT_NHWC_F32) g = H16<T>::from(H16<T>::to(g));  // stored value
+            g = (ok && __builtin_fmaf(xx[r], msc[r], msh[r]) > 0.f) ? g : 0.f;
+            sg[r] += g;
+            sgx[r] += g * (xx[r] - mean[r]) * inv[r];
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if constexpr (sizeof(T) == 2) {
+            sg[r] = row16_sum(sg[r]);
+            sgx[r] = row16_sum(sgx[r]);
+          } else {
+#pragma unroll
+            for (int off = 1; off < 16; off <<= 1) {
+              sg[r] += __shfl_xor(sg[r], off);
+              sgx[r] += __shfl_xor(sgx[r], off);
+            }
+          }
+        }
+        if (red) {
+          if ((lane & 15) == 0) {  // [wp][sum][channel of the tile]
+            const int ct = cf - c0;
+            *(float4*)(red + (wp * 2 + 0) * TCB + ct) = make_float4(sg[0], sg[1], sg[2], sg[3]);
+            *(float4*)(red + (wp * 2 + 1) * TCB + ct) = make_float4(sgx[0], sgx[1], sgx[2], sgx[3]);
+          }
+        } else if ((lane & 15) == 0 && cok) {
+          *(float4*)(A.bnr_part + (size_t)part * A.Cout + cf) = make_float4(sg[0], sg[1], sg[2], sg[3]);
+          *(float4*)(A.bnr_part + ((size_t)parts + 1 + part) * A.Cout + cf) = make_float4(sgx[0], sgx[1], sgx[2], sgx[3]);
+        }
+      }
+    }
+    if (red) {
+      __syncthreads();
+      // the tile's sums over its NWP wave halves, in wave order: thread t < TCB sums channel t
+      const int t = wc * NWP * 64 + wp * 64 + lane;  // flat thread id (wave = wc * NWP + wp)
+      if (t < TCB && c0 + t < A.Cout) {
+        float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+        for (int w = 0; w < NWP; ++w) {
+          s0 += red[(w * 2 + 0) * TCB + t];
+          s1 += red[(w * 2 + 1) * TCB + t];
+        }
+        A.bnr_part[(size_t)part * A.Cout + c0 + t] = s0;
+        A.bnr_part[((size_t)parts + 1 + part) * A.Cout + c0 + t] = s1;
+      }
+    }
   }
 }
 
@@ -904,7 +1067,7 @@ __device__ __forceinline__ void head_epilogue16(const zp_conv_args& A, const zp_
 
 // HEAD (zp_conv2d_head, 16-bit eval): the conv output is not stored; it feeds the fused 1x1 head's
 // partial sums over this tile's channels (head_epilogue16)
-template <typename T, int WC, int SPW, int DM, bool HEAD = false>
+template <typename T, int WC, int SPW, int DM, bool HEAD = false, bool BNR = false>
 __global__ void __launch_bounds__(512) k_conv_strip2(const zp_conv_args A, const strip_geo SG, const int flags,
                                                      const zp_head_args H) {
   // DM: where the next group's strip DMA is issued.  0: the read section of tap column 1; 1: spread
@@ -1185,7 +1348,8 @@ __global__ void __launch_bounds__(512) k_conv_strip2(const zp_conv_args A, const
   } else if constexpr (HEAD) {
     head_epilogue16<T, WC, WP, NWP>(A, S, H, acc, p0, c0, by, wc, wp, lane, M, lds);
   } else {
-    conv_epilogue<T, WC, WP, NWP>(A, S, acc, p0, c0, wc, wp, lane, M, GHW, bx, blockIdx.z, gridDim.z);
+    conv_epilogue<T, WC, WP, NWP, BNR>(A, S, acc, p0, c0, wc, wp, lane, M, GHW, bx, blockIdx.z, gridDim.z, nullptr,
+                                       (float*)lds);
   }
 }
 
@@ -2562,6 +2726,10 @@ extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
   ZP_CHECK_ARG(a.nsub >= 1 && a.nsub <= ZP_MAX_SUB, "zp_conv2d: nsub %d", a.nsub);
   ZP_CHECK_ARG(a.x && a.N > 0 && a.GH > 0 && a.GW > 0 && a.IH > 0 && a.IW > 0 && a.Cout > 0,
                "zp_conv2d: bad geometry");
+  ZP_CHECK_ARG(!a.bnr_part || (a.bnr_x && a.bnr_save && (a.dtype == ZP_F32 || a.dtype == ZP_BF16) && !a.stats &&
+                                !a.res && !a.relu && a.out_mode == ZP_OUT_NHWC && a.Cout % 4 == 0),
+               "zp_conv2d: bnr_* (fused BN backward reduce) needs a plain f32 / bf16 NHWC store (no stats, "
+               "residual, ReLU), bnr_x and bnr_save, Cout %% 4 == 0");
   if (a.dtype == ZP_F32X3 || a.dtype == ZP_F32H2) return conv3_launch(a, (hipStream_t)stream, conv_flags());
   const int E = a.dtype == ZP_F32 ? 4 : 8, KE = 8 * E;
   const bool smallc = a.Cin < KE;
@@ -2572,12 +2740,13 @@ extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
   ZP_CHECK_ARG(a.w_rows % conv_tc(a) == 0 && a.w_rows >= a.Cout, "zp_conv2d: w_rows %d", a.w_rows);
   ZP_CHECK_ARG((a.out_mode >= 0 && a.out_mode <= 2) || ((a.out_mode == ZP_OUT_NHWC_X3 || a.out_mode == ZP_OUT_NHWC_H2) && a.dtype == ZP_F32 && !a.stats),
                "zp_conv2d: out_mode %d", a.out_mode);
-  ZP_CHECK_ARG(!a.stats || (!a.res && !a.relu && a.out_mode != ZP_OUT_HEAD_NCHW && !a.sub[0].scale &&
+  ZP_CHECK_ARG(!(a.stats || a.bnr_part) || (!a.res && !a.relu && a.out_mode != ZP_OUT_HEAD_NCHW && !a.sub[0].scale &&
                             !a.sub[0].shift),
                "zp_conv2d: stats are taken on the raw conv output (no scale/shift/residual/relu/head)");
   for (int s = 0; s < a.nsub; ++s) {
     const zp_conv_sub& S = a.sub[s];
     ZP_CHECK_ARG(S.w && S.y, "zp_conv2d: sub %d null w/y", s);
+    ZP_CHECK_ARG(!a.bnr_part || (!S.scale && !S.shift), "zp_conv2d: bnr_* with a scale / shift epilogue");
     ZP_CHECK_ARG(S.ntaps >= 1 && S.ntaps <= ZP_MAX_TAPS, "zp_conv2d: ntaps %d", S.ntaps);
     if (smallc) {
       ZP_CHECK_ARG(S.kw > 0 && (long)S.ntaps * a.Cin <= a.k_pad, "zp_conv2d: small-Cin taps/k_pad");
@@ -2623,7 +2792,7 @@ extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
   {
     const long mpix = (long)a.N * a.GH * a.GW;
     const zp_conv_sub& S = a.sub[0];
-    if (E == 8 && !smallc && mpix <= 64 && a.nsub == 1 && S.ntaps == 1 && !a.stats && !a.res &&
+    if (E == 8 && !smallc && mpix <= 64 && a.nsub == 1 && S.ntaps == 1 && !a.stats && !a.bnr_part && !a.res &&
         a.out_mode == ZP_OUT_NHWC && a.w_rows >= ((a.Cout + 63) / 64) * 64 && (conv_flags() & 1024) != 0) {
       const dim3 grid((a.Cout + 63) / 64, (unsigned)mpix);
       if (a.dtype == ZP_F16) hipLaunchKernelGGL(k_conv_smallm<f16_t>, grid, dim3(256), 0, (hipStream_t)stream, a);
@@ -2641,8 +2810,10 @@ extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
     sg.w_bytes = tg.w_bytes[0];
     const int sgx = (int)(((long)a.N * a.GH * a.GW) / 256);
     const dim3 grid(sgx, gy, 1);
+    const int fl0 = conv_flags();
     // train-mode statistics: the caller sized the partials buffer with zp_conv2d_stat_parts; the
     // launch must emit exactly that many parts (NWP = 4 wave-halves per 256-pixel tile)
+    ZP_CHECK_ARG(!a.bnr_part || (fl0 & 64) || 4 * sgx == zp_conv2d_stat_parts(&a), "zp_conv2d: strip bnr parts");
     ZP_CHECK_ARG(!a.stats || 4 * sgx == zp_conv2d_stat_parts(&a),
                  "zp_conv2d: strip launch emits %d stat parts, zp_conv2d_stat_parts says %d", 4 * sgx,
                  zp_conv2d_stat_parts(&a));
@@ -2653,12 +2824,19 @@ extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
   if (fl & 256) hipLaunchKernelGGL((k_conv_strip2<T, WC, 5, 2>), grid, dim3(512), 0, st, a, sg, fl, H0); \
   else if (fl & 32) hipLaunchKernelGGL((k_conv_strip2<T, WC, 5, 1>), grid, dim3(512), 0, st, a, sg, fl, H0); \
   else hipLaunchKernelGGL((k_conv_strip2<T, WC, 5, 0>), grid, dim3(512), 0, st, a, sg, fl, H0);
-      if (a.dtype == ZP_F16) {
+#define ZP_STRIP2B(T, WC)                                                                              \
+  if (fl & 256) hipLaunchKernelGGL((k_conv_strip2<T, WC, 5, 2, false, true>), grid, dim3(512), 0, st, a, sg, fl, H0); \
+  else if (fl & 32) hipLaunchKernelGGL((k_conv_strip2<T, WC, 5, 1, false, true>), grid, dim3(512), 0, st, a, sg, fl, H0); \
+  else hipLaunchKernelGGL((k_conv_strip2<T, WC, 5, 0, false, true>), grid, dim3(512), 0, st, a, sg, fl, H0);
+      if (a.bnr_part) {  // (bf16 only: zp_conv2d's bnr check)
+        if (tc == 64) { ZP_STRIP2B(bf16_t, 2) } else { ZP_STRIP2B(bf16_t, 4) }
+      } else if (a.dtype == ZP_F16) {
         if (tc == 64) { ZP_STRIP2(f16_t, 2) } else { ZP_STRIP2(f16_t, 4) }
       } else {
         if (tc == 64) { ZP_STRIP2(bf16_t, 2) } else { ZP_STRIP2(bf16_t, 4) }
       }
 #undef ZP_STRIP2
+#undef ZP_STRIP2B
     } else if (a.dtype == ZP_F16) {
       if (tc == 64) hipLaunchKernelGGL((k_conv_strip<f16_t, 2, 3, 5>), grid, dim3(512), 0, st, a, sg, fl);
       else hipLaunchKernelGGL((k_conv_strip<f16_t, 4, 3, 5>), grid, dim3(512), 0, st, a, sg, fl);
@@ -2675,7 +2853,7 @@ extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
     qg.w_bytes = tg.w_bytes[0];
     const int qgx = (int)(((long)a.N * a.GH * a.GW) / 256);
     const dim3 grid(qgx, gy, 1);
-    ZP_CHECK_ARG(!a.stats || 4 * 4 * qgx == zp_conv2d_stat_parts(&a),
+    ZP_CHECK_ARG(!(a.stats || a.bnr_part) || 4 * 4 * qgx == zp_conv2d_stat_parts(&a),
                  "zp_conv2d: quad launch emits %d stat parts, zp_conv2d_stat_parts says %d", 16 * qgx,
                  zp_conv2d_stat_parts(&a));
     const int fl = conv_flags();
@@ -2693,7 +2871,7 @@ extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
   const int stages = conv_stages(a, tc);
   {
     const int launched_nwp = tc == 256 ? 4 : nwp;  // launch_conv_tc256 is always the 256-pixel tile
-    ZP_CHECK_ARG(!a.stats || launched_nwp * gx * a.nsub == zp_conv2d_stat_parts(&a),
+    ZP_CHECK_ARG(!(a.stats || a.bnr_part) || launched_nwp * gx * a.nsub == zp_conv2d_stat_parts(&a),
                  "zp_conv2d: launch emits %d stat parts, zp_conv2d_stat_parts says %d", launched_nwp * gx * a.nsub,
                  zp_conv2d_stat_parts(&a));
   }
@@ -2898,6 +3076,14 @@ extern "C" int zp_conv2d_wgrad(const zp_wgrad_args* ap, void* ws, void* stream) 
 extern "C" int zp_conv2d_stat_parts(const zp_conv_args* a) {
   if (!a) return 0;
   return (conv_tp(*a) / 64) * zp_conv2d_grid(a) * a->nsub;
+}
+
+extern "C" int zp_conv2d_bnr_parts(const zp_conv_args* a) {
+  if (!a) return 0;
+  // k_conv_strip2 sums its wave halves in LDS: one part per 256-pixel tile
+  if (a->dtype != ZP_F32 && conv_tc(*a) <= 128 && strip_eligible(*a, nullptr) && (conv_flags() & 64))
+    return (int)(((long)a->N * a->GH * a->GW) / 256);
+  return zp_conv2d_stat_parts(a);
 }
 
 // the 16-bit fused head: a 3x3 stride-1 conv on the 128-channel strip tile (k_conv_strip2, two cout

@@ -592,8 +592,11 @@ __global__ void __launch_bounds__(256) k_bn_bwd_reduce(const T* __restrict__ dy,
 // block = 8 channels x 128 part lanes (1024 threads; C / 8 blocks: 8 for a 64-channel BN, where the
 // former 32 x 32 layout ran 2 blocks for the whole GPU); each lane sums its parts (4 loads per
 // stream in flight), then a fixed pairwise tree over the 128 lanes (deterministic)
+// oparts: the totals go to rows oparts of both halves (the [2][oparts + 1][C] layout zp_bn_bwd_apply
+// reads; oparts != parts after a zp_conv2d launch with bnr_part) -- only this block touches channel c,
+// and it writes after every read of its parts
 __global__ void __launch_bounds__(1024) k_bn_bwd_totals(float* __restrict__ part, int parts, int C, float* dgamma,
-                                                        float* dbeta, int accumulate) {
+                                                        float* dbeta, int accumulate, int oparts) {
   __shared__ double sh[2][128][9];
   const int cl = threadIdx.x & 7, pl = threadIdx.x >> 3;
   const int c = blockIdx.x * 8 + cl;
@@ -628,8 +631,8 @@ __global__ void __launch_bounds__(1024) k_bn_bwd_totals(float* __restrict__ part
   if (pl != 0 || c >= C) return;
   s = sh[0][0][cl];
   q = sh[1][0][cl];
-  part[(size_t)parts * C + c] = (float)s;
-  part[((size_t)parts + 1 + parts) * C + c] = (float)q;
+  part[(size_t)oparts * C + c] = (float)s;
+  part[((size_t)oparts + 1 + oparts) * C + c] = (float)q;
   if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)q : (float)q;
   if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)s : (float)s;
 }
@@ -1582,8 +1585,17 @@ extern "C" int zp_bn_bwd_reduce(const void* dy, int lddy, int cdy0, const void* 
 #undef ZP_BNR
   ZP_LAUNCH_CHECK("zp_bn_bwd_reduce");
   hipLaunchKernelGGL(k_bn_bwd_totals, dim3((C + 7) / 8), dim3(1024), 0, st, partials, parts, C, dgamma, dbeta,
-                     accumulate);
+                     accumulate, parts);
   ZP_LAUNCH_CHECK("zp_bn_bwd_reduce totals");
+  return ZP_OK;
+}
+
+extern "C" int zp_bn_bwd_totals(float* partials, int parts, int C, int out_parts, float* dgamma, float* dbeta,
+                                int accumulate, void* stream) {
+  ZP_CHECK_ARG(partials && parts > 0 && out_parts > 0 && C > 0, "zp_bn_bwd_totals: bad args");
+  hipLaunchKernelGGL(k_bn_bwd_totals, dim3((C + 7) / 8), dim3(1024), 0, (hipStream_t)stream, partials, parts, C,
+                     dgamma, dbeta, accumulate, out_parts);
+  ZP_LAUNCH_CHECK("zp_bn_bwd_totals");
   return ZP_OK;
 }
 

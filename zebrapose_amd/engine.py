@@ -169,6 +169,8 @@ class Engine:
         self._side = None
         self._side_used = False
         self.bn_mask_from_raw = True  # BN+ReLU backward without residual: mask from raw (A/B knob)
+        # the reduce of a BN + ReLU backward taken by its reader's dgrad launch (_bnr_fusable)
+        self.bn_bwd_fused = os.environ.get("ZP_BN_BWD_FUSED", "1") != "0"
         # two-plane eval forward: up2's last conv and the head in one launch (zp_conv2d_head);
         # ZP_FUSE_HEAD=0 keeps them apart
         self.fuse_head = os.environ.get("ZP_FUSE_HEAD", "1") != "0"
@@ -292,10 +294,13 @@ class Engine:
 
     # ------------------------------------------------------------------ conv launch
     def _conv(self, x: Act, plan, cout, weights, k_pad, rows, outs, res=None, relu=False,
-              out_mode=L.ZP_OUT_NHWC, stats=None, small=None, label=None, dt=None, head=None):
+              out_mode=L.ZP_OUT_NHWC, stats=None, small=None, label=None, dt=None, head=None, bnr=None):
         """weights / outs: per sub.  outs[i] = (y_ptr, ldy, cy0, OH, OW, scale, shift, y2).  dt
         overrides the engine's dtype code (the x3 engine's f32 stem).  head: (L.HeadArgs, head FLOPs,
-        head bytes) -- the conv feeds the fused 1x1 head (zp_conv2d_head) instead of storing."""
+        head bytes) -- the conv feeds the fused 1x1 head (zp_conv2d_head) instead of storing.
+        bnr: (raw, save, P) of the train-mode BN whose output gradient this data-gradient launch
+        writes: the launch also takes that BN backward's reduce (zp.h bnr_*); returns (partials,
+        parts) in place of (stats, parts)."""
         dt = self.dt if dt is None else dt
         a = L.ConvArgs()
         a.dtype = dt
@@ -321,10 +326,18 @@ class Engine:
             if small is not None:
                 s.kw, s.dil, s.pad = small
         parts = 0
-        if stats == "alloc":
+        if bnr is not None:
+            raw, save, P = bnr
+            parts = L.lib.zp_conv2d_bnr_parts(C.byref(a))
+            rows_ = max(parts, L.lib.zp_bn_bwd_parts(P, cout)) + 1
+            stats = torch.empty(2 * rows_ * cout, dtype=torch.float32, device=x.buf.device)
+            a.bnr_x, a.bnr_save, a.bnr_part = raw.data_ptr(), save.data_ptr(), stats.data_ptr()
+        elif stats == "alloc":
             parts = L.lib.zp_conv2d_stat_parts(C.byref(a))
             stats = torch.empty(3 * parts * cout, dtype=torch.float32, device=x.buf.device)
-        if stats is not None:
+        if bnr is not None:
+            pass
+        elif stats is not None:
             a.stats = stats.data_ptr()
         elif dt in SPLIT:  # split-K workspace of a small split-fp32 launch (zp_conv2d_split_ws)
             nb = L.lib.zp_conv2d_split_ws(C.byref(a))
@@ -673,9 +686,10 @@ class Engine:
             torch.cuda.current_stream(dev).wait_stream(self._side)
         self._side_used = False
 
-    def _dgrad(self, unit, gy: Act, gx: Act, accumulate=True):
+    def _dgrad(self, unit, gy: Act, gx: Act, accumulate=True, bnr=None):
         """gx (+)= dgrad(gy): accumulate into the input gradient slice (residual = itself), or
-        overwrite it (accumulate False: its first writer, see _grad_out)."""
+        overwrite it (accumulate False: its first writer, see _grad_out).  bnr: see _conv (the
+        overwrite form only); returns _conv's (partials, parts)."""
         plan = unit.dgrad_plan(gx.H, gx.W)
         cin_l = gy.C  # = cout (padded for the head)
         kp = max(self._kpad(len(sb.taps), cin_l) for sb in plan.subs)
@@ -686,8 +700,9 @@ class Engine:
         small = self._small(cin_l, unit.k, -unit.d, -unit.p) if unit.kind == "conv" and unit.s == 1 else None
         if cin_l < _KE[self.dt]:
             assert small is not None, "small-channel dgrad only for stride-1 convs"
-        self._conv(gy, plan, unit.cin, ws, kp, rows, outs, res=gx if accumulate else None, relu=False, small=small,
-                   label="dgrad")
+        assert bnr is None or not accumulate
+        return self._conv(gy, plan, unit.cin, ws, kp, rows, outs, res=gx if accumulate else None, relu=False,
+                          small=small, label="dgrad", bnr=bnr)
 
     @staticmethod
     def _snap(a: Act):
@@ -718,14 +733,22 @@ class Engine:
             if kind == "bn":
                 P = out.P
                 parts = L.lib.zp_bn_bwd_parts(P, unit.cout)
-                partials = torch.empty(2 * (parts + 1) * unit.cout, dtype=torch.float32, device=dev)
+                if out.buf.data_ptr() not in gmap.get("__bnr__", {}):
+                    partials = torch.empty(2 * (parts + 1) * unit.cout, dtype=torch.float32, device=dev)
                 dgamma = torch.empty_like(bn.weight)
                 dbeta = torch.empty_like(bn.bias)
                 # ReLU without a residual: the mask is recomputed from raw (mode 2), out is not read
                 rm = (2 if res is None and self.bn_mask_from_raw else 1) if unit.relu else 0
-                L.call("zp_bn_bwd_reduce", gout.ptr, gout.ld, gout.c0, out.ptr, out.ld, out.c0, raw.data_ptr(), P,
-                       unit.cout, save.data_ptr(), rm, self.dt, partials.data_ptr(), dgamma.data_ptr(),
-                       dbeta.data_ptr(), 0, st)
+                fused = gmap.get("__bnr__", {}).pop(out.buf.data_ptr(), None)
+                if fused is not None:  # the consumer's dgrad launch took the reduce (_bnr_fusable)
+                    assert rm == 2
+                    partials, fparts = fused
+                    L.call("zp_bn_bwd_totals", partials.data_ptr(), fparts, unit.cout, parts, dgamma.data_ptr(),
+                           dbeta.data_ptr(), 0, st)
+                else:
+                    L.call("zp_bn_bwd_reduce", gout.ptr, gout.ld, gout.c0, out.ptr, out.ld, out.c0, raw.data_ptr(),
+                           P, unit.cout, save.data_ptr(), rm, self.dt, partials.data_ptr(), dgamma.data_ptr(),
+                           dbeta.data_ptr(), 0, st)
                 graw = torch.empty_like(raw)
                 gres, racc = self._grad_out(gmap, res, True) if res is not None else (None, True)
                 gres_before = self._snap(gres) if tr is not None and gres is not None and racc else None
@@ -782,7 +805,15 @@ class Engine:
         if need_dx:
             gx, acc = self._grad_out(gmap, x, self._dgrad_whole(unit, x))
             before = self._snap(gx) if tr is not None and acc else None
-            self._dgrad(unit, gy, gx, accumulate=acc)
+            prod = None if acc else gmap.get("__bnr_prod__", {}).get(x.buf.data_ptr())
+            if prod is not None:
+                # x is the output of a BN + ReLU (mode 2) whose only reader is this unit: the dgrad
+                # launch that writes its whole gradient also takes that BN backward's reduce
+                _, praw, psave = prod
+                fused = self._dgrad(unit, gy, gx, accumulate=False, bnr=(praw, psave, x.P))
+                gmap.setdefault("__bnr__", {})[x.buf.data_ptr()] = fused
+            else:
+                self._dgrad(unit, gy, gx, accumulate=acc)
             if tr is not None:
                 tr["gx"] = (before, self._snap(gx))
         if tr is not None:
@@ -1091,6 +1122,45 @@ class Engine:
             torch.cuda.current_stream(self._side.device).wait_stream(self._side)
             self._side_used = False
 
+    def _bnr_fusable(self, tape):
+        """{activation buffer: (unit, raw, save)} of the train-mode BN + ReLU outputs whose backward
+        reduce can run inside the data-gradient launch of their reader (zp.h bnr_*): relu mask from
+        the raw conv output (mode 2: no residual), the output is a whole buffer (no channel slice of a
+        concat), and exactly one taped op reads that buffer -- a conv unit with its own BN or none,
+        not the head -- so that reader's dgrad, which writes every pixel of the gradient (overwrite,
+        _grad_out), is its only writer.  f32 / bf16 engines (the kernels' epilogue), ZP_BN_BWD_FUSED=0
+        turns it off."""
+        if not self.bn_bwd_fused or self.dt not in (L.ZP_F32, L.ZP_BF16):
+            return {}
+        readers = {}
+
+        def read(act):
+            if act is not None:
+                k = act.buf.data_ptr()
+                readers[k] = readers.get(k, 0) + 1
+        kinds = {}
+        for rec in tape.recs:
+            kind = rec[0]
+            if kind in ("plain", "bn", "head"):
+                read(rec[2])
+                read(rec[4])
+                kinds.setdefault(rec[2].buf.data_ptr(), []).append((kind, rec[1], rec[2]))
+            elif kind in ("maxpool", "broadcast", "copy", "avgpool"):
+                read(rec[1])
+        out = {}
+        for rec in tape.recs:
+            if rec[0] != "bn":
+                continue
+            _, unit, _x, o, res, raw, save = rec
+            k = o.buf.data_ptr()
+            if not unit.relu or res is not None or not self.bn_mask_from_raw or o.c0 != 0 or o.C != o.ld:
+                continue
+            rd = kinds.get(k)
+            if readers.get(k) != 1 or not rd or rd[0][0] == "head" or not self._dgrad_whole(rd[0][1], rd[0][2]):
+                continue
+            out[k] = (unit, raw, save)
+        return out
+
     def backward_iter(self, tape, dmask, dcode, dentire=None, grads=None):
         """Engine.backward as a generator: yields after each taped op's backward has been enqueued
         (the staged autograd chain of zebrapose_amd.staged advances it stage by stage)."""
@@ -1130,6 +1200,7 @@ class Engine:
 
         if not v3:
             main_head_grad()
+        gmap["__bnr_prod__"] = self._bnr_fusable(tape)
         for rec in reversed(tape.recs):
             kind = rec[0]
             if kind == "head" and rec[3] == "head" and v3:
