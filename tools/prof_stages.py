@@ -6,7 +6,8 @@ the kernel-trace stats (profiles/<tag>_infer_kernel_stats.csv, <tag>_train1s_ker
 
 Attribution: every pass runs the same tools/prof_driver.py --mode infer program, whose dispatch
 sequence is identical from step 2 on.  The last step is the window from its k_nchw_to_nhwc (the
-input conversion, first kernel of a step) to the end of the run (the decode kernels end it).  Its
+input conversion, first kernel of a step; the two-plane engine's k_stem_h2, which reads the NCHW
+input itself since round 5) to the end of the run (the decode kernels end it).  Its
 conv dispatches are matched one by one, in order, to the driver's stage log (engine.stage_log:
 stage, kernel label, FLOPs); the label of every pair is checked.  Non-conv kernels are attributed
 by name (nchw_to_nhwc, im2col -> stem, maxpool -> layer1, global avgpool / broadcast -> aspp, decode).
@@ -68,8 +69,10 @@ def is_conv(name):
 def last_step(rows):
     """rows: dispatches in order [(name, ...)] -> the slice of the last step."""
     starts = [i for i, r in enumerate(rows) if "nchw_to_nhwc" in r[0]]
+    if not starts:  # round 5: the two-plane stem reads the NCHW input itself (no conversion kernel)
+        starts = [i for i, r in enumerate(rows) if "k_stem_h2" in r[0]]
     if not starts:
-        raise SystemExit("no k_nchw_to_nhwc dispatch found")
+        raise SystemExit("no k_nchw_to_nhwc / k_stem_h2 dispatch found")
     return rows[starts[-1]:]
 
 

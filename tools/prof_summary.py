@@ -32,8 +32,10 @@ def bench_label(name):
     m = re.search(r"k_conv_strip<(unsigned short|_Float16), (\d+), (\d+), (\d+)>", name)
     if m:
         return f"k_conv_strip<{tn[m.group(1)]},WC={m.group(2)},ST={m.group(3)}>"
-    m = re.search(r"k_conv_strip2<(unsigned short|_Float16), (\d+), (\d+), (true|false|\d+)(, (true|false))?>", name)
-    if m:  # (the 5th parameter, HEAD: the fused 16-bit head's conv, zp_conv2d_head)
+    m = re.search(r"k_conv_strip2<(unsigned short|_Float16), (\d+), (\d+), (true|false|\d+)(, (true|false))?(, (true|false))?>",
+                  name)
+    if m:  # (the 5th parameter, HEAD: the fused 16-bit head's conv, zp_conv2d_head; the 6th, BNR: a data
+        # gradient taking the BN backward reduce -- same label, as the engine's)
         head = "_head" if m.group(6) == "true" else ""
         return f"k_conv_strip2{head}<{tn[m.group(1)]},WC={m.group(2)}>"
     sp = {"3": "x3", "2": "h2"}  # split-fp32 planes -> engine label
