@@ -67,13 +67,14 @@ def test_bn_backward_mask_from_raw_matches_stored_mask(dt, P, Cc):
     assert float((yk != mk).float().mean()) < 1e-3
 
 
-@pytest.mark.parametrize("parts,C", [(8192, 64), (4100, 256), (200, 96), (1024, 2048)])
+@pytest.mark.parametrize("parts,C", [(8192, 64), (4100, 256), (200, 96), (512, 256), (1024, 2048)])
 def test_bn_stat_merge_one_launch_equals_two(gpu, parts, C):
     """zp_bn_train_finalize's level-1 + level-2 statistics merge in ONE launch (zp_conv_tuning key 15;
     the last-arriving block of each channel group runs level 2 after an agent-scope counter hand-off)
     stores exactly the bits of the two-launch form (same parts, same fixed merge order), re-arms its
     counters (three calls in a row agree), and matches a float64 merge of the same partials (Chan's
-    formula: the train-mode batch mean / biased variance, train_v6.py's BatchNorm2d in training)."""
+    formula: the train-mode batch mean / biased variance, train_v6.py's BatchNorm2d in training).
+    129 .. 512 parts (200, 512) run the one-level merge (k_bn_stat_merge1) in both modes."""
     from zebrapose_amd import _lib as L
     g = torch.Generator().manual_seed(parts + C)
     cnt = torch.randint(1, 33, (parts, C), generator=g).float()

@@ -406,6 +406,79 @@ __global__ void __launch_bounds__(256) k_bn_stat_merge_fin(float* __restrict__ p
   bn_finalize_block(part, parts, BN_MERGE_R, C, blockIdx.x, f, sh);
 }
 
+// One level for up to BN_MERGE1_MAX parts (round 5; most layers of the bs 32 training step have
+// 512): block = 8 channels x 128 part lanes, a lane's (at most 4) parts loaded once; the two passes of
+// Chan's merge (n, sum n_k mean_k -> mean; sum M2_k + n_k (mean_k - mean)^2) read registers, each
+// followed by a fixed pairwise tree over the 128 lanes in f64 (deterministic); then the finalize of
+// bn_finalize_block.  One launch without the two-level form's counter hand-off, whose release /
+// acquire fences and two dependent global passes per level held every merge near 10 us.
+constexpr int BN_MERGE1_MAX = 512;
+__global__ void __launch_bounds__(1024) k_bn_stat_merge1(const float* __restrict__ part, int parts, int C, const BnFin f) {
+  __shared__ double sh[2][128][9];
+  const int cl = threadIdx.x & 7, pl = threadIdx.x >> 3;
+  const int c = blockIdx.x * 8 + cl;
+  constexpr int U = BN_MERGE1_MAX / 128;
+  float pn[U], pm[U], pq[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int k = pl + 128 * u;
+    const bool in = c < C && k < parts;
+    pn[u] = in ? part[(size_t)k * C + c] : 0.f;
+    pm[u] = in ? part[((size_t)parts + k) * C + c] : 0.f;
+    pq[u] = in ? part[((size_t)2 * parts + k) * C + c] : 0.f;
+  }
+  double n = 0, s = 0;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    n += (double)pn[u];
+    s += (double)pn[u] * (double)pm[u];
+  }
+  sh[0][pl][cl] = n;
+  sh[1][pl][cl] = s;
+  __syncthreads();
+  for (int w = 64; w > 0; w >>= 1) {
+    if (pl < w) {
+      sh[0][pl][cl] += sh[0][pl + w][cl];
+      sh[1][pl][cl] += sh[1][pl + w][cl];
+    }
+    __syncthreads();
+  }
+  const double ntot = sh[0][0][cl], stot = sh[1][0][cl];
+  const double mean = ntot > 0 ? stot / ntot : 0.0;
+  double q = 0;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const double dm = (double)pm[u] - mean;
+    q += (double)pq[u] + (double)pn[u] * dm * dm;  // (parts past the end: all three zero)
+  }
+  __syncthreads();  // every lane has read the pass-1 totals
+  sh[0][pl][cl] = q;
+  __syncthreads();
+  for (int w = 64; w > 0; w >>= 1) {
+    if (pl < w) sh[0][pl][cl] += sh[0][pl + w][cl];
+    __syncthreads();
+  }
+  if (pl != 0 || c >= C) return;
+  q = sh[0][0][cl];
+  const double cntd = ntot;
+  double var = cntd > 0 ? q / cntd : 0.0;
+  if (var < 0) var = 0;
+  float invstd = (float)(1.0 / sqrt(var + (double)f.eps));
+  float sc = f.gamma[c] * invstd;
+  const float shv = __builtin_fmaf(-(float)mean, sc, f.beta[c]);
+  f.scale[c] = sc;
+  f.shift[c] = shv;
+  f.save[c] = (float)mean;
+  f.save[C + c] = invstd;
+  f.save[2 * C + c] = sc;
+  f.save[3 * C + c] = shv;
+  double mt = mean + (f.bias ? (double)f.bias[c] : 0.0);
+  double unb = cntd > 1 ? var * cntd / (cntd - 1.0) : var;
+  f.rm[c] = (float)((1.0 - f.mom) * f.rm[c] + f.mom * mt);
+  f.rv[c] = (float)((1.0 - f.mom) * f.rv[c] + f.mom * unb);
+  if (c == 0 && f.nbt) f.nbt[0] += 1;
+}
+
 // the fused merge's per-device counters (one per channel group, zero between launches: each launch's
 // last block re-arms its own); allocated and zeroed on first use outside a stream capture
 static unsigned* g_bn_cnt[64];
@@ -1488,6 +1561,11 @@ extern "C" int zp_bn_train_finalize(float* partials, int parts, int C, long long
   hipStream_t st = (hipStream_t)stream;
   // the partials buffer is the caller's scratch (zp_conv2d stats): level 1 merges in place
   int stride = 1;
+  if (parts > 2 * BN_MERGE_R && parts <= BN_MERGE1_MAX) {  // (both key-15 modes: one level, one launch)
+    hipLaunchKernelGGL(k_bn_stat_merge1, dim3((C + 7) / 8), dim3(1024), 0, st, partials, parts, C, f);
+    ZP_LAUNCH_CHECK("zp_bn_train_finalize (one level)");
+    return ZP_OK;
+  }
   if (parts > 2 * BN_MERGE_R) {
     const int groups = (C + 31) / 32;
     static const int env = getenv("ZP_BN_FUSED") ? atoi(getenv("ZP_BN_FUSED")) : 1;
