@@ -2934,18 +2934,38 @@ static bool wgrad_lds(const zp_wgrad_args& a) {
   return a.dtype == ZP_BF16 && v != 0;
 }
 // tile: 0 = 64 co x 512 col (Cout <= 64), 1 = 128 x 256, 2 = 256 x 256 (Cout >= 256: fewer staged
-// bytes per FLOP -- the L2 -> LDS stream, not the MFMA, bounds this kernel)
+// bytes per FLOP -- the L2 -> LDS stream, not the MFMA, bounds this kernel).  Round 5: a k_wgrad2
+// launch whose 256 x 256 plan would give each split under 2048 pixels takes 128 x 256 instead --
+// few tiles (a 3x3 256 -> 256 at 32 x 32 has 9) mean ~28 splits, and each split writes a 256 KB f32
+// partial slab (64 MB per launch, re-read by k_wgrad_reduce) for 1216 pixels of MFMA work:
+// measured 739 -> 679 us over layer4's 11 wgrads, the 1 x 1 convs 43 -> 32 us; the 128 x 128
+// decoder / layer5 wgrads (18724 / 4681 pixels per split) stay on 256 x 256 (1116 vs 1328 us).
+// ZP_WGRAD_BIG=0: always 128 x 256; 2: always 256 x 256 (A/B)
+static bool wgrad2_eligible(const zp_wgrad_args& a);
+static int num_cus();
+extern int g_wgrad2_rounds_v;
 static int wgrad_cfg(const zp_wgrad_args& a) {
   static const int big = getenv("ZP_WGRAD_BIG") ? env_int("ZP_WGRAD_BIG") : 1;
   if (a.Cout <= 64) return 0;
-  if (a.Cout >= 256 && big) return 2;
-  return 1;
+  if (a.Cout < 256 || !big) return 1;
+  if (big == 1 && wgrad2_eligible(a)) {
+    long M = (long)a.N * a.GH * a.GW;
+    int cm = 0;
+    for (int s = 0; s < a.nsub; ++s) cm = cm > a.sub[s].ntaps * a.Cin ? cm : a.sub[s].ntaps * a.Cin;
+    const long tiles = (long)ceil_div(cm, 256) * ceil_div(a.Cout, 256);
+    long sp = (long)g_wgrad2_rounds_v * num_cus() / tiles;
+    const long maxsp = M / (16 * 64) > 0 ? M / (16 * 64) : 1;
+    sp = sp < 1 ? 1 : (sp > maxsp ? maxsp : sp);
+    if (M / sp < 2048) return 1;
+  }
+  return 2;
 }
 // k_wgrad2 (lean issue path) for the common geometry -- see the kernel's header comment.
 // zp_conv_tuning key 3: 0 disables it; key 4: its workgroup rounds over the CUs (default 1: fewer,
 // longer workgroups than k_wgrad_lds's 1024 -- the split-K partial slabs are written and re-read
 // in full -- and never a partial extra round; one round measured fastest).
 static int g_wgrad2 = 1, g_wgrad2_rounds = 1, g_wgrad_lds_rounds = 1;
+int g_wgrad2_rounds_v = 1;  // (g_wgrad2_rounds, read by wgrad_cfg above)
 static int num_cus() {
   static int n = 0;
   if (!n) {
@@ -3220,6 +3240,7 @@ extern "C" int zp_conv_tuning(int key, int value) {
   if (key == 4) {
     const int old = g_wgrad2_rounds;
     g_wgrad2_rounds = value > 0 ? value : 1;
+    g_wgrad2_rounds_v = g_wgrad2_rounds;
     return old;
   }
   return -1;
