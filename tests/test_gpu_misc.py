@@ -54,7 +54,8 @@ def test_nchw_to_nhwc(gpu, prec, cpad):
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32, torch.float16])
 def test_pack_weight_multi_matches_single_packs(gpu, dt):
     """The batched repack of training (one grid row per job) against zp_pack_weight job by job:
-    plain 3x3, a tap subset (ConvT phase), transposed (dgrad / ConvT layout), a padded-channel stem
+    plain 3x3, a tap subset (ConvT phase), transposed (dgrad / ConvT layout), the reversed tap order
+    of a data-gradient packing (the compile-time 3x3 forms of k_pack_multi), a padded-channel stem
     (cstride 8 > 3 channels, k_pad tail) and a 1x1 with padded rows."""
     import ctypes as C
     from zebrapose_amd import _lib as L
@@ -64,6 +65,8 @@ def test_pack_weight_multi_matches_single_packs(gpu, dt):
         (128, 64, 3, 0, [(i // 3, i % 3) for i in range(9)], 64, 128, 576),
         (64, 96, 3, 0, [(0, 0), (0, 2), (2, 0), (2, 2)], 96, 64, 384),
         (96, 64, 3, 1, [(i // 3, i % 3) for i in range(9)], 96, 64, 896),
+        (96, 64, 3, 1, [(2 - i // 3, 2 - i % 3) for i in range(9)], 96, 64, 896),  # dgrad: taps reversed
+        (64, 128, 3, 0, [(2 - i // 3, 2 - i % 3) for i in range(9)], 128, 64, 1152),
         (64, 3, 7, 0, [(i // 7, i % 7) for i in range(49)], 8, 64, 448),
         (17, 320, 1, 0, [(0, 0)], 320, 32, 320),
     ]

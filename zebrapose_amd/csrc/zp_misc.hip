@@ -150,7 +150,72 @@ __device__ __forceinline__ void pack_store(const zp_pack_job& a, int d, float v,
 // below it read the transposed layouts one scattered 36-byte run per lane (r02 PMC: 1.3 GB moved per
 // 116 MB of weights).
 constexpr int PK_R = 8, PK_C = 64, PK_ROW = PK_C * 9 + 1;  // +1: the transposed fill hits distinct banks
-__global__ void __launch_bounds__(256) k_pack_multi(const zp_pack_job* __restrict__ jobs, unsigned* rflag) {
+// KHW / NT: the job's kh * kw and tap count as compile-time constants (9 / 9: a full 3x3 forward packing;
+// 9 / -9: the reversed taps of a 3x3 data-gradient packing; 1 / 1: the 1x1s), or 0 for the runtime
+// values (ConvT phase sub-problems); with them a tile's loads are all issued before its LDS writes
+// (one memory round trip per tile instead of one per element batch)
+template <int KHW, int NT>
+__device__ __forceinline__ void pack_tiled(const zp_pack_job& a, const int* toff, float* tile, unsigned* rflag) {
+  const int rows = a.transposed ? a.d1 : a.d0;
+  const int chans = a.transposed ? a.d0 : a.d1;
+  const int khw = KHW ? KHW : a.kh * a.kw;
+  const int ntaps = NT > 0 ? NT : (NT < 0 ? -NT : a.ntaps);
+  const int ct = (a.cstride + PK_C - 1) / PK_C, rt = (a.rows_pad + PK_R - 1) / PK_R;
+  const int kt = ntaps * a.cstride, nld = PK_R * PK_C * khw;
+  for (int tl = blockIdx.x; tl < rt * ct; tl += gridDim.x) {
+    const int r0 = (tl / ct) * PK_R, c0 = (tl % ct) * PK_C;
+    auto elem = [&](int e, int& li) -> float {  // source element e of the tile -> its value, LDS index
+      const int k = e % khw, q = e / khw;
+      int rl, cl;
+      if (a.transposed) {  // src[c][r][tap]: runs of consecutive r per channel
+        rl = q % PK_R;
+        cl = q / PK_R;
+      } else {  // src[r][c][tap]: runs of consecutive c per row
+        cl = q % PK_C;
+        rl = q / PK_C;
+      }
+      const int r = r0 + rl, c = c0 + cl;
+      li = rl * PK_ROW + cl * 9 + k;
+      return (r < rows && c < chans) ? a.src[(a.transposed ? ((size_t)c * a.d1 + r) : ((size_t)r * a.d1 + c)) * khw + k]
+                                     : 0.f;
+    };
+    if constexpr (KHW > 0) {
+      constexpr int PER = (PK_R * PK_C * KHW + 255) / 256;
+      float v[PER];
+      int li[PER];
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int e = threadIdx.x + 256 * u;
+        v[u] = e < nld ? elem(e, li[u]) : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < PER; ++u)
+        if (threadIdx.x + 256 * u < nld) tile[li[u]] = v[u];
+    } else {
+      for (int e = threadIdx.x; e < nld; e += blockDim.x) {
+        int li;
+        const float v = elem(e, li);
+        tile[li] = v;
+      }
+    }
+    __syncthreads();
+    const int cw = min(PK_C, a.cstride - c0);
+    for (int e = threadIdx.x; e < PK_R * ntaps * PK_C; e += blockDim.x) {
+      const int cl = e % PK_C, q = e / PK_C, t = q % ntaps, rl = q / ntaps;
+      const int r = r0 + rl;
+      const int tk = NT == 9 && KHW == 9 ? t : (NT == -9 && KHW == 9 ? 8 - t : (NT == 1 && KHW == 1 ? 0 : toff[t]));
+      if (cl < cw && r < a.rows_pad) pack_store(a, r * a.k_pad + t * a.cstride + c0 + cl, tile[rl * PK_ROW + cl * 9 + tk], rflag);
+    }
+    if (c0 == 0)  // the row's k_pad tail
+      for (int e = threadIdx.x; e < PK_R * (a.k_pad - kt); e += blockDim.x) {
+        const int rl = e / (a.k_pad - kt), kk = kt + e % (a.k_pad - kt);
+        if (r0 + rl < a.rows_pad) pack_store(a, (r0 + rl) * a.k_pad + kk, 0.f, rflag);
+      }
+    __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(256) k_pack_multi(const zp_pack_job* __restrict__ jobs, unsigned* rflag, int forms) {
   const zp_pack_job& a = jobs[blockIdx.y];
   // tap offsets in LDS (a private copy of the job's tap arrays would live in scratch)
   __shared__ int toff[ZP_MAX_TAPS];
@@ -160,40 +225,16 @@ __global__ void __launch_bounds__(256) k_pack_multi(const zp_pack_job* __restric
   const int rows = a.transposed ? a.d1 : a.d0;
   const int chans = a.transposed ? a.d0 : a.d1;
   if (a.kh * a.kw <= 9) {
-    const int khw = a.kh * a.kw, ct = (a.cstride + PK_C - 1) / PK_C, rt = (a.rows_pad + PK_R - 1) / PK_R;
-    const int kt = a.ntaps * a.cstride, nld = PK_R * PK_C * khw;
-    for (int tl = blockIdx.x; tl < rt * ct; tl += gridDim.x) {
-      const int r0 = (tl / ct) * PK_R, c0 = (tl % ct) * PK_C;
-      for (int e = threadIdx.x; e < nld; e += blockDim.x) {
-        const int k = e % khw, q = e / khw;
-        int rl, cl;
-        if (a.transposed) {  // src[c][r][tap]: runs of consecutive r per channel
-          rl = q % PK_R;
-          cl = q / PK_R;
-        } else {  // src[r][c][tap]: runs of consecutive c per row
-          cl = q % PK_C;
-          rl = q / PK_C;
-        }
-        const int r = r0 + rl, c = c0 + cl;
-        float v = 0.f;
-        if (r < rows && c < chans)
-          v = a.src[(a.transposed ? ((size_t)c * a.d1 + r) : ((size_t)r * a.d1 + c)) * khw + k];
-        tile[rl * PK_ROW + cl * 9 + k] = v;
-      }
-      __syncthreads();
-      const int cw = min(PK_C, a.cstride - c0);
-      for (int e = threadIdx.x; e < PK_R * a.ntaps * PK_C; e += blockDim.x) {
-        const int cl = e % PK_C, q = e / PK_C, t = q % a.ntaps, rl = q / a.ntaps;
-        const int r = r0 + rl;
-        if (cl < cw && r < a.rows_pad) pack_store(a, r * a.k_pad + t * a.cstride + c0 + cl, tile[rl * PK_ROW + cl * 9 + toff[t]], rflag);
-      }
-      if (c0 == 0)  // the row's k_pad tail
-        for (int e = threadIdx.x; e < PK_R * (a.k_pad - kt); e += blockDim.x) {
-          const int rl = e / (a.k_pad - kt), kk = kt + e % (a.k_pad - kt);
-          if (r0 + rl < a.rows_pad) pack_store(a, (r0 + rl) * a.k_pad + kk, 0.f, rflag);
-        }
-      __syncthreads();
+    bool ident = true, rev = true;
+    for (int t = 0; t < a.ntaps; ++t) {
+      ident = ident && a.ky[t] * a.kw + a.kx[t] == t;
+      rev = rev && a.ky[t] * a.kw + a.kx[t] == a.ntaps - 1 - t;
     }
+    if (!forms) pack_tiled<0, 0>(a, toff, tile, rflag);  // (A/B: ZP_PACK_FORMS=0)
+    else if (ident && a.kh * a.kw == 9 && a.ntaps == 9) pack_tiled<9, 9>(a, toff, tile, rflag);
+    else if (rev && a.kh * a.kw == 9 && a.ntaps == 9) pack_tiled<9, -9>(a, toff, tile, rflag);
+    else if (ident && a.kh * a.kw == 1 && a.ntaps == 1) pack_tiled<1, 1>(a, toff, tile, rflag);
+    else pack_tiled<0, 0>(a, toff, tile, rflag);
     return;
   }
   const int pairs = a.rows_pad * a.cstride;
@@ -1535,7 +1576,14 @@ extern "C" int zp_pack_weight_multi(int n, const zp_pack_job* jobs, const long l
   ZP_CHECK_ARG(n >= 0 && n <= 65535 && total >= 0 && total < (1ll << 40) && (n == 0 || (jobs && prefix)),
                "zp_pack_weight_multi: bad args");
   if (n == 0 || total == 0) return ZP_OK;
-  hipLaunchKernelGGL(k_pack_multi, dim3(256, n), dim3(256), 0, (hipStream_t)stream, jobs, range_flag());
+  // blocks per job, each walking the job's 8-row x 64-channel tiles: 64 measured best of 32 / 64 / 128
+  // / 256 on the training step's ~100 jobs (256: 170 us, most blocks of the small jobs empty; 64: 134
+  // us; a flat tile space over all jobs, blocks scanning the jobs' tile counts, ran 228 us at 172
+  // VGPRs); ZP_PACK_GX for A/B
+  static const int gx = getenv("ZP_PACK_GX") ? atoi(getenv("ZP_PACK_GX")) : 64;
+  static const int forms = getenv("ZP_PACK_FORMS") ? atoi(getenv("ZP_PACK_FORMS")) : 1;
+  hipLaunchKernelGGL(k_pack_multi, dim3(gx > 0 ? gx : 64, n), dim3(256), 0, (hipStream_t)stream, jobs, range_flag(),
+                     forms);
   ZP_LAUNCH_CHECK("zp_pack_weight_multi");
   return ZP_OK;
 }
