@@ -158,7 +158,8 @@ int zp_conv2d_bnr_parts(const zp_conv_args* a);
  * (0 = k_conv, 1 = k_conv_strip: 3x3 stride-1 convs with activation-strip reuse, 2 = k_conv_strip2:
  * the same with the lean main loop, 3 = k_conv_quad: the four phases of a stride-2 transposed
  * structure in one tile, 4 = k_conv3: the split-fp32 (ZP_F32X3) kernel, 5 = k_conv3s: its 3x3
- * stride-1 form with activation-strip reuse) */
+ * stride-1 form with activation-strip reuse, 6 = k_conv3w: the 256 x 256 two-plane tile, 7 = k_conv1x1n: a
+ * 1x1 with 32 / 64 input channels and a wide output, the weights held in LDS) */
 int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* stages, int* variant);
 /* Split-fp32 forms (ZP_F32X3 / ZP_F32H2) only: a launch whose grid would leave most CUs idle (an
  * NHWC conv -- one sub-problem or several: ConvT phases, merged ASPP branches -- with under 256

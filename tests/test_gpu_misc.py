@@ -98,3 +98,44 @@ def test_pack_weight_multi_matches_single_packs(gpu, dt):
     L.call("zp_pack_weight_multi", len(jobs), table.data_ptr(), prefix.data_ptr(), pre[-1], L.stream_ptr())
     for ref, got in zip(singles, outs):
         assert torch.equal(ref, got)
+
+
+@pytest.mark.parametrize("cin,cout,ldy,cy0", [(32, 320, 320, 0), (64, 64, 128, 64)])
+def test_conv1x1_narrow_k(gpu, cin, cout, ldy, cy0):
+    """k_conv1x1n (zp_conv2d_config variant 7): a 1x1 conv with 32 / 64 input channels and a wide
+    bf16 output -- the head's data gradient in training, 32 -> 320 at 128 x 128 -- against a float64
+    matmul of the same bf16 operands, to 1 bf16 ulp of the output (+2^-16 of the scale for cancelling
+    sums), written into a channel slice (ldy / cy0) without touching its neighbours."""
+    import ctypes as C
+    from zebrapose_amd import _lib as L
+    torch.manual_seed(cin + cout)
+    N, H, W = 4, 128, 128
+    x = torch.randn(N, H, W, cin).to(torch.bfloat16).cuda()
+    w = (torch.randn(cout, cin, 1, 1) * 0.2)
+    rows = L.lib.zp_conv_rows_pad(cout)
+    kp = 64
+    wp = torch.empty((rows, kp), dtype=torch.bfloat16, device="cuda")
+    wd = w.cuda()
+    L.call("zp_pack_weight", wd.data_ptr(), cout, cin, 1, 1, 0, 1, (C.c_int * 1)(0), (C.c_int * 1)(0), cin, L.ZP_BF16,
+           wp.data_ptr(), rows, kp, L.stream_ptr())
+    y = torch.full((N, H, W, ldy), 3.0, dtype=torch.bfloat16, device="cuda")
+    a = L.ConvArgs()
+    a.dtype, a.x, a.ldx, a.cx0, a.IH, a.IW, a.Cin = L.ZP_BF16, x.data_ptr(), cin, 0, H, W, cin
+    a.N, a.GH, a.GW, a.sy, a.sx = N, H, W, 1, 1
+    a.Cout, a.k_pad, a.w_rows, a.relu, a.out_mode, a.nsub = cout, kp, rows, 0, L.ZP_OUT_NHWC, 1
+    s = a.sub[0]
+    s.w, s.y, s.ldy, s.cy0, s.OH, s.OW, s.oys, s.oxs, s.ntaps = wp.data_ptr(), y.data_ptr(), ldy, cy0, H, W, 1, 1, 1
+    s.kw, s.dil, s.pad = 1, 1, 0
+    tc, tp, st, var = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+    L.call("zp_conv2d_config", C.byref(a), C.byref(tc), C.byref(tp), C.byref(st), C.byref(var))
+    assert var.value == 7
+    L.check(L.lib.zp_conv2d(C.byref(a), L.stream_ptr()), "zp_conv2d")
+    torch.cuda.synchronize()
+    wb = w.reshape(cout, cin).to(torch.bfloat16).double()
+    ref = (x.cpu().double().reshape(-1, cin) @ wb.t()).reshape(N, H, W, cout)
+    got = y.cpu()[..., cy0:cy0 + cout].double()
+    ulp = ref.abs().clamp_min(1e-30) * 2.0 ** -7
+    err = (got - ref).abs()
+    assert bool((err <= ulp + 2.0 ** -16 * float(ref.abs().max())).all()), float((err / ulp).max())
+    keep = torch.cat([y.cpu()[..., :cy0], y.cpu()[..., cy0 + cout:]], -1)
+    assert bool((keep == 3.0).all())

@@ -1750,6 +1750,65 @@ __global__ void __launch_bounds__(512) k_conv_quad(const zp_conv_args A, const q
 // 1024): measured 16.8 vs 17.7 us per eager launch, i.e. both are launch latency, which the
 // hipGraph-replayed inference step does not pay; the network tests pass with it enabled.
 // ------------------------------------------------------------------------------------
+// 1 x 1 conv with a narrow K and a wide output (the head's data gradient in training: 32 -> 320
+// channels at 128 x 128, bs 32 -- 34 MB in, 335 MB out).  On k_conv's small-Cin tile it took 177 us
+// (2.1 TB/s): one K step per 128 x 256 tile, so every workgroup was prologue + epilogue at one
+// workgroup per CU.  Here a block stages the whole packed weight (Cout x Cin, <= 48 KB) in LDS in
+// MFMA fragment order once, and each wave walks 16-pixel groups: one 16-byte activation load per lane
+// and K step, Cout / 16 MFMAs from LDS fragments, the paired 8-channel epilogue's 16-byte stores.
+// Same MFMAs over the same K order as k_conv (its extra K step of zero weights only adds zeros).
+constexpr int C1N_MAXCB = 24;  // cout blocks of 16 (384 channels)
+template <typename T, int NCB>  // NCB = Cout / 16 (compile-time: the accumulators stay in registers)
+__global__ void __launch_bounds__(256) k_conv1x1n(const zp_conv_args A) {
+  __shared__ uint4 wl[NCB * 2 * 64];
+  const zp_conv_sub& S = A.sub[0];
+  constexpr int ncb = NCB;
+  const int nks = A.Cin / 32;
+  for (int f = threadIdx.x; f < ncb * nks * 64; f += blockDim.x) {  // fragment (i, s), lane l
+    const int l = f & 63, fs = f >> 6, i = fs / nks, ks = fs - i * nks;
+    wl[f] = *(const uint4*)((const unsigned short*)S.w + (size_t)(i * 16 + (l & 15)) * A.k_pad + ks * 32 + (l >> 4) * 8);
+  }
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4;
+  const long M = (long)A.N * A.GH * A.GW;
+  const long ngroups = (M + 15) / 16;
+  for (long grp = (long)blockIdx.x * 4 + wave; grp < ngroups; grp += (long)gridDim.x * 4) {
+    const long p = grp * 16 + (lane & 15);
+    const bool pok = p < M;
+    uint4 b[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      b[ks] = (pok && ks < nks) ? *(const uint4*)((const unsigned short*)A.x + p * A.ldx + A.cx0 + ks * 32 + g * 8)
+                                : make_uint4(0u, 0u, 0u, 0u);
+    f32x4 acc[NCB];
+#pragma unroll
+    for (int i = 0; i < NCB; ++i) {
+      acc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      MfmaTraits<T>::mma(acc[i], wl[(i * nks) * 64 + lane], b[0]);
+      if (nks > 1) MfmaTraits<T>::mma(acc[i], wl[(i * nks + 1) * 64 + lane], b[1]);
+    }
+    // (stride 1, one sub-problem on the input grid: output pixel = p)
+    unsigned short* Y = (unsigned short*)S.y + p * S.ldy + S.cy0;
+#pragma unroll
+    for (int i = 0; i < NCB; i += 2) {
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {  // all lanes active (cross-lane op)
+        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][r]), __float_as_uint(acc[i + 1][r]), false,
+                                                         false);
+        v[r] = __uint_as_float(sw[0]);
+        v[r + 4] = __uint_as_float(sw[1]);
+      }
+      if (!pok) continue;
+      const int cs = (i + (g & 1)) * 16 + (g >> 1) * 8;
+      uint32_t o[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = H16<T>::to(v[2 * r]) | (H16<T>::to(v[2 * r + 1]) << 16);
+      *(uint4*)(Y + cs) = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+  }
+}
+
 template <typename T>
 __device__ __forceinline__ void ld16x8(const T* p, float* v) {  // 8 16-bit values, one 16-byte load
   const uint4 u = *(const uint4*)p;
@@ -2711,6 +2770,19 @@ static int conv_stages(const zp_conv_args& a, int tc) {
 
 extern "C" int zp_conv2d_stat_parts(const zp_conv_args* a);
 
+// k_conv1x1n's geometry (ZP_CONV1X1N=0 turns it off)
+static int num_cus();
+static bool conv1x1n_ok(const zp_conv_args& a) {
+  static const int en1n = getenv("ZP_CONV1X1N") ? env_int("ZP_CONV1X1N") : 1;
+  const zp_conv_sub& S = a.sub[0];
+  return en1n && (a.dtype == ZP_BF16 || a.dtype == ZP_F16) && a.nsub == 1 && S.ntaps == 1 && S.ty[0] == 0 &&
+         S.tx[0] == 0 && (a.Cin == 32 || a.Cin == 64) && a.Cout % 64 == 0 && a.Cout / 16 <= C1N_MAXCB &&
+         a.w_rows >= a.Cout && a.k_pad >= a.Cin && !a.stats && !a.bnr_part && !a.res && !a.relu &&
+         a.out_mode == ZP_OUT_NHWC && !S.scale && !S.shift && S.ldy % 8 == 0 && S.cy0 % 8 == 0 && a.ldx % 8 == 0 &&
+         a.cx0 % 8 == 0 && a.sy == 1 && a.sx == 1 && a.GH == a.IH && a.GW == a.IW && S.OH == a.GH && S.OW == a.GW &&
+         S.oys == 1 && S.oxs == 1 && S.oyo == 0 && S.oxo == 0 && (long)a.N * a.GH * a.GW >= 65536;
+}
+
 extern "C" int zp_conv2d_grid(const zp_conv_args* a) {
   if (!a) return 0;
   long M = (long)a->N * a->GH * a->GW;
@@ -2786,6 +2858,23 @@ extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
       for (int t = 0; grid && t < S.ntaps; ++t)
         grid = S.ty[t] == tg.ty0[s] + (t / nx) * tg.dty[s] && S.tx[t] == tg.tx0[s] + (t % nx) * tg.dtx[s];
       ZP_CHECK_ARG(grid, "zp_conv2d: sub %d taps must form a (row x column) grid of at most 32 x 32, rows outer", s);
+    }
+  }
+  // narrow-K 1x1 convs with a wide output (k_conv1x1n: the head's data gradient in training)
+  {
+    if (conv1x1n_ok(a)) {
+      const long groups = ((long)a.N * a.GH * a.GW + 15) / 16;
+      const long want = (groups + 3) / 4;
+      const int blocks = (int)(want < 2L * num_cus() ? want : 2L * num_cus());  // (~200 VGPRs: 2 blocks per CU)
+#define ZP_C1N(NCB)                                                                                           \
+  case NCB:                                                                                                   \
+    if (a.dtype == ZP_F16) hipLaunchKernelGGL((k_conv1x1n<f16_t, NCB>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, a); \
+    else hipLaunchKernelGGL((k_conv1x1n<bf16_t, NCB>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, a);    \
+    break;
+      switch (a.Cout / 16) { ZP_C1N(4) ZP_C1N(8) ZP_C1N(12) ZP_C1N(16) ZP_C1N(20) ZP_C1N(24) }
+#undef ZP_C1N
+      ZP_LAUNCH_CHECK("zp_conv2d 1x1 narrow-K");
+      return ZP_OK;
     }
   }
   // tiny-M 1x1 convs (the ASPP image-pool conv): one wave per (grid point, 16 output channels)
@@ -3169,7 +3258,7 @@ extern "C" int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* st
   *tc = conv_tc(*a);
   *tp = conv_tp(*a);
   *stages = *tc == 256 ? 2 : conv_stages(*a, *tc);
-  *variant = (a->dtype == ZP_F32X3 || a->dtype == ZP_F32H2) ? (*tc == 256 ? 6 : conv3_nsplit(*a) == 1 && conv3_strip_ok(*a, *tc) ? 5 : 4) : quad_plan(*a, nullptr) ? 3 : *tc <= 128 && strip_eligible(*a, nullptr) ? ((conv_flags() & 64) ? 2 : 1) : 0;
+  *variant = (a->dtype == ZP_F32X3 || a->dtype == ZP_F32H2) ? (*tc == 256 ? 6 : conv3_nsplit(*a) == 1 && conv3_strip_ok(*a, *tc) ? 5 : 4) : conv1x1n_ok(*a) ? 7 : quad_plan(*a, nullptr) ? 3 : *tc <= 128 && strip_eligible(*a, nullptr) ? ((conv_flags() & 64) ? 2 : 1) : 0;
   return ZP_OK;
 }
 

@@ -408,6 +408,8 @@ class Engine:
             return f"k_conv_strip<{tn},WC={tc.value // 32},ST=3>"
         if var.value == 3:  # rocprofv3 name: k_conv_quad<T, W>
             return f"k_conv_quad<{tn},W={plan.GW}>"
+        if var.value == 7:  # rocprofv3 name: k_conv1x1n<T> (narrow-K 1x1: the head's data gradient)
+            return f"k_conv1x1n<{tn}>"
         if var.value == 2:  # rocprofv3 name: k_conv_strip2<T, WC, SPW = 5>
             return f"k_conv_strip2<{tn},WC={tc.value // 32}>"
         # rocprofv3 name: k_conv<T, WC = tc / 32, WP = 4, NWP = tp / 64, STAGES, smallC>
