@@ -580,6 +580,64 @@ def run(args):
     value, ms_per_step, n_corr, out = main["value"], main["ms_per_step"], main["n_corr"], main["out"]
     roofline = conv_roofline(net, x, args.steps, args.precision, ms_per_step, args.layer_report, rank)
 
+    # (the training leg runs right after the headline: measured inside the full bench after the bf16
+    # and bs=1 hipGraph legs with the world-size-1 RCCL group alive, the same step read ~1 ms slower
+    # (16.95 vs 15.9-16.0 ms with any one of the three absent, tools/plans/r05_g34.txt) -- an
+    # interaction of the process's earlier legs, not of the step)
+    # ------------------------------------------------------------------ training step (extra)
+    # configs[2]: bs=32 per GPU, bf16 (BASELINE.json), hist-weighted BCE + mask loss, backward, Adam;
+    # configs[3] at N > 1 (DDP over RCCL).  At N = 1 the same step also runs through a world-size-1
+    # RCCL group (rccl_world1): every bucket's all_reduce is a real RCCL collective on its stream.
+    train = None
+    tprec = "bf16"
+    if not args.no_train:
+        from zebrapose_amd.train import TrainStep
+        tnet = BinaryCodeNet_Deeplab(34, 16, 2, concat=True, output_kernel_size=1, precision=tprec).to(dev)
+        calibrate_bn(tnet, x)
+        tnet.train()
+        lr = 2e-4 * world  # train_v6.py:89-91
+        g = torch.Generator(device="cpu").manual_seed(7 + rank)
+        gt_code = (torch.rand((B, 16, S // 2, S // 2), generator=g) < 0.5).to(torch.uint8).to(dev)
+        gt_mask = (torch.rand((B, S // 2, S // 2), generator=g) < 0.7).float().to(dev)
+        K = args.train_steps or max(3, args.steps // 2)
+
+        def timed_train(ts):
+            for _ in range(max(2, args.warmup // 2)):
+                ts(x, gt_code, gt_mask)
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(K):
+                loss = ts(x, gt_code, gt_mask)
+            torch.cuda.synchronize()
+            tel = time.perf_counter() - t0
+            if world > 1:
+                t = torch.tensor([tel], device=dev, dtype=torch.float64)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                tel = t.item()
+            return tel, loss
+
+        ts = TrainStep(tnet, learning_rate=lr)
+        tel, loss = timed_train(ts)
+        train = {"crops_per_s": round(world * B * K / tel, 2), "ms_per_step": round(tel / K * 1e3, 3),
+                 "steps": K, "global_batch": world * B, "dtype": tprec, "loss": round(float(loss[0].item()), 5),
+                 "achieved_tflops": round(3 * FWD_GFLOP_PER_CROP * 1e9 * world * B * K / tel / 1e12 / world, 2),
+                 "parallelism": f"ddp{world}" if world > 1 else "single"}
+        train["breakdown"] = train_breakdown(ts, tnet, x, gt_code, gt_mask, world, rank)
+        del ts
+        if rccl1:
+            ts = TrainStep(tnet, learning_rate=lr, ddp=True, device=local)
+            tel, _ = timed_train(ts)
+            train["rccl_world1"] = {
+                "what": "the same step through a world-size-1 RCCL process group (backend nccl): GradBuckets' "
+                        "bucketed async all_reduce on the RCCL stream, overlapped with the backward, plus the "
+                        "per-forward BN buffer broadcast -- configs[3]'s exchange code, on one GPU",
+                "ms_per_step": round(tel / K * 1e3, 3), "crops_per_s": round(B * K / tel, 2),
+                "breakdown": train_breakdown(ts, tnet, x, gt_code, gt_mask, 1, rank)}
+            del ts
+        del tnet
+
     # ------------------------------------------------------------------ bf16 leg (throughput mode)
     # the same step with bf16 storage / bf16 MFMA (f32 accumulate): narrower than the reference's
     # fp32, so a labelled extra with its own roofline, not the headline
@@ -686,60 +744,6 @@ def run(args):
                 "what": "640x480 BGR images -> 256 px INTER_LINEAR normalised crop + 128 px GT code planes and "
                         "2 masks (INTER_NEAREST), padding 1.5"}
     del imgs, gts, msk
-
-    # ------------------------------------------------------------------ training step (extra)
-    # configs[2]: bs=32 per GPU, bf16 (BASELINE.json), hist-weighted BCE + mask loss, backward, Adam;
-    # configs[3] at N > 1 (DDP over RCCL).  At N = 1 the same step also runs through a world-size-1
-    # RCCL group (rccl_world1): every bucket's all_reduce is a real RCCL collective on its stream.
-    train = None
-    tprec = "bf16"
-    if not args.no_train:
-        from zebrapose_amd.train import TrainStep
-        tnet = BinaryCodeNet_Deeplab(34, 16, 2, concat=True, output_kernel_size=1, precision=tprec).to(dev)
-        calibrate_bn(tnet, x)
-        tnet.train()
-        lr = 2e-4 * world  # train_v6.py:89-91
-        g = torch.Generator(device="cpu").manual_seed(7 + rank)
-        gt_code = (torch.rand((B, 16, S // 2, S // 2), generator=g) < 0.5).to(torch.uint8).to(dev)
-        gt_mask = (torch.rand((B, S // 2, S // 2), generator=g) < 0.7).float().to(dev)
-        K = args.train_steps or max(3, args.steps // 2)
-
-        def timed_train(ts):
-            for _ in range(max(2, args.warmup // 2)):
-                ts(x, gt_code, gt_mask)
-            torch.cuda.synchronize()
-            if world > 1:
-                dist.barrier()
-            t0 = time.perf_counter()
-            for _ in range(K):
-                loss = ts(x, gt_code, gt_mask)
-            torch.cuda.synchronize()
-            tel = time.perf_counter() - t0
-            if world > 1:
-                t = torch.tensor([tel], device=dev, dtype=torch.float64)
-                dist.all_reduce(t, op=dist.ReduceOp.MAX)
-                tel = t.item()
-            return tel, loss
-
-        ts = TrainStep(tnet, learning_rate=lr)
-        tel, loss = timed_train(ts)
-        train = {"crops_per_s": round(world * B * K / tel, 2), "ms_per_step": round(tel / K * 1e3, 3),
-                 "steps": K, "global_batch": world * B, "dtype": tprec, "loss": round(float(loss[0].item()), 5),
-                 "achieved_tflops": round(3 * FWD_GFLOP_PER_CROP * 1e9 * world * B * K / tel / 1e12 / world, 2),
-                 "parallelism": f"ddp{world}" if world > 1 else "single"}
-        train["breakdown"] = train_breakdown(ts, tnet, x, gt_code, gt_mask, world, rank)
-        del ts
-        if rccl1:
-            ts = TrainStep(tnet, learning_rate=lr, ddp=True, device=local)
-            tel, _ = timed_train(ts)
-            train["rccl_world1"] = {
-                "what": "the same step through a world-size-1 RCCL process group (backend nccl): GradBuckets' "
-                        "bucketed async all_reduce on the RCCL stream, overlapped with the backward, plus the "
-                        "per-forward BN buffer broadcast -- configs[3]'s exchange code, on one GPU",
-                "ms_per_step": round(tel / K * 1e3, 3), "crops_per_s": round(B * K / tel, 2),
-                "breakdown": train_breakdown(ts, tnet, x, gt_code, gt_mask, 1, rank)}
-            del ts
-        del tnet
 
     # ------------------------------------------------------------------ 3-head v3 network (extra, §8f rank 3)
     v3 = None
