@@ -74,7 +74,7 @@ def test_bn_stat_merge_one_launch_equals_two(gpu, parts, C):
     stores exactly the bits of the two-launch form (same parts, same fixed merge order), re-arms its
     counters (three calls in a row agree), and matches a float64 merge of the same partials (Chan's
     formula: the train-mode batch mean / biased variance, train_v6.py's BatchNorm2d in training).
-    129 .. 512 parts (200, 512) run the one-level merge (k_bn_stat_merge1) in both modes."""
+    Up to 512 parts (200, 512) run the one-level merge (k_bn_stat_merge1) in both modes."""
     from zebrapose_amd import _lib as L
     g = torch.Generator().manual_seed(parts + C)
     cnt = torch.randint(1, 33, (parts, C), generator=g).float()

@@ -301,9 +301,15 @@ def test_train_backward_teacher_forced(step):
                 P = raw.shape[0] * raw.shape[1] * raw.shape[2]
                 gm = step["w0"][id(unit.bn.weight)].cuda()
                 sgP, sgxP = (sg / P).float(), (sgx / P).float()
+                # d raw = gamma invstd (g - sum_g / P - xhat sum_gx / P): where the bracket cancels, one f32
+                # ulp of the device's per-channel totals (f32 partial sums) moves the bf16 rounding of a
+                # whole channel (1 / C of the elements).  On the B = 2 fixture's small BNs (P <= 4096
+                # batch pixels) allow 8 channels' worth (observed: one 256-channel 8 x 8 BN at 1.56%);
+                # the bench-geometry layers keep 0.5%
+                mf = max(0.005, 8.0 / C) if P <= 4096 else 0.005
                 for b in sample:
                     exp = (gm * inv) * (g[b] - sgP - xh[b] * sgxP)
-                    ck.bf16(f"crop {b} {lab} d raw", _h(_q(exp.unsqueeze(0).cpu())), _h(r["graw"], b))
+                    ck.bf16(f"crop {b} {lab} d raw", _h(_q(exp.unsqueeze(0).cpu())), _h(r["graw"], b), max_frac=mf)
                     if r["gres"] is not None:
                         before, after = r["gres"]
                         e = g[b:b + 1].cpu()

@@ -312,8 +312,14 @@ __device__ __forceinline__ void conv_epilogue(const zp_conv_args& A, const zp_co
     // Train-mode BatchNorm statistics of the raw (stored) conv output, per wave half:
     // (count, mean, M2) with M2 centred on the local mean (two passes over the registers, no
     // E[x^2] - E[x]^2 cancellation); zp_bn_train_finalize merges the parts (Chan et al.).
-    const int parts = gridDim.x * nz * NWP;
-    const int part = (zi * gridDim.x + bx) * NWP + wp;
+    // red (k_conv_strip2, round 5): the NWP wave halves of a cout block are merged in LDS first, in
+    // wave order (Chan's pairwise update in f32), and the tile writes one part
+    // (zp_conv2d_stat_parts): a quarter of the partials for the merge to read -- at 128 x 128,
+    // bs 32, 2048 parts instead of 8192 (that merge took 43 us)
+    const int parts = red ? gridDim.x * nz : gridDim.x * nz * NWP;
+    const int part = red ? zi * gridDim.x + bx : (zi * gridDim.x + bx) * NWP + wp;
+    constexpr int TCS = 32 * WC;  // channels of the tile's cout block
+    if (red) __syncthreads();  // every wave's last main-loop LDS read precedes the writes below
     float cnt = 0.f;
 #pragma unroll
     for (int j = 0; j < WP; ++j) cnt += (p0 + wp * 16 * WP + j * 16 + (lane & 15) < M) ? 1.f : 0.f;
@@ -358,12 +364,39 @@ __device__ __forceinline__ void conv_epilogue(const zp_conv_args& A, const zp_co
           for (int off = 1; off < 16; off <<= 1) m2 += __shfl_xor(m2, off);
         }
         const int c = cbase + i * 16 + r;
-        if ((lane & 15) == 0 && c < A.Cout) {
+        if (red) {
+          if ((lane & 15) == 0) {  // [wp][cnt, mean, m2][channel of the tile]
+            red[(wp * 3 + 0) * TCS + c - c0] = cnt;
+            red[(wp * 3 + 1) * TCS + c - c0] = mean;
+            red[(wp * 3 + 2) * TCS + c - c0] = m2;
+          }
+        } else if ((lane & 15) == 0 && c < A.Cout) {
           A.stats[(size_t)part * A.Cout + c] = cnt;
           A.stats[((size_t)parts + part) * A.Cout + c] = mean;
           A.stats[((size_t)2 * parts + part) * A.Cout + c] = m2;
         }
       }
+    if (red) {
+      __syncthreads();
+      const int t = wc * NWP * 64 + wp * 64 + lane;  // flat thread id: thread t merges channel c0 + t
+      if (t < TCS && c0 + t < A.Cout) {
+        float n = red[t], mu = red[TCS + t], q = red[2 * TCS + t];
+#pragma unroll
+        for (int w = 1; w < NWP; ++w) {
+          const float nw = red[(w * 3 + 0) * TCS + t];
+          if (nw > 0.f) {
+            const float mw = red[(w * 3 + 1) * TCS + t], qw = red[(w * 3 + 2) * TCS + t];
+            const float nn = n + nw, d = mw - mu;
+            mu += d * (nw / nn);
+            q += qw + d * d * (n * nw / nn);
+            n = nn;
+          }
+        }
+        A.stats[(size_t)part * A.Cout + c0 + t] = n;
+        A.stats[((size_t)parts + part) * A.Cout + c0 + t] = mu;
+        A.stats[((size_t)2 * parts + part) * A.Cout + c0 + t] = q;
+      }
+    }
   }
   if (A.bnr_part) {
     // Data gradient feeding a train-mode BN + ReLU backward (zp.h bnr_*): per wave half, the sums
@@ -2903,7 +2936,7 @@ extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
     // train-mode statistics: the caller sized the partials buffer with zp_conv2d_stat_parts; the
     // launch must emit exactly that many parts (NWP = 4 wave-halves per 256-pixel tile)
     ZP_CHECK_ARG(!a.bnr_part || (fl0 & 64) || 4 * sgx == zp_conv2d_stat_parts(&a), "zp_conv2d: strip bnr parts");
-    ZP_CHECK_ARG(!a.stats || 4 * sgx == zp_conv2d_stat_parts(&a),
+    ZP_CHECK_ARG(!a.stats || ((fl0 & 64) ? 1 : 4) * sgx == zp_conv2d_stat_parts(&a),
                  "zp_conv2d: strip launch emits %d stat parts, zp_conv2d_stat_parts says %d", 4 * sgx,
                  zp_conv2d_stat_parts(&a));
     const int fl = conv_flags();
@@ -3184,6 +3217,10 @@ extern "C" int zp_conv2d_wgrad(const zp_wgrad_args* ap, void* ws, void* stream) 
 
 extern "C" int zp_conv2d_stat_parts(const zp_conv_args* a) {
   if (!a) return 0;
+  // k_conv_strip2 merges its wave halves in LDS: one part per 256-pixel tile (round 5)
+  if (a->dtype != ZP_F32 && a->dtype != ZP_F32X3 && a->dtype != ZP_F32H2 && conv_tc(*a) <= 128 &&
+      strip_eligible(*a, nullptr) && (conv_flags() & 64))
+    return (int)(((long)a->N * a->GH * a->GW) / 256);
   return (conv_tp(*a) / 64) * zp_conv2d_grid(a) * a->nsub;
 }
 

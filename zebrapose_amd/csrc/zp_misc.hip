@@ -447,8 +447,8 @@ __global__ void __launch_bounds__(256) k_bn_stat_merge_fin(float* __restrict__ p
   bn_finalize_block(part, parts, BN_MERGE_R, C, blockIdx.x, f, sh);
 }
 
-// One level for up to BN_MERGE1_MAX parts (round 5; most layers of the bs 32 training step have
-// 512): block = 8 channels x 128 part lanes, a lane's (at most 4) parts loaded once; the two passes of
+// One level for up to BN_MERGE1_MAX parts (round 5; with the strip tile's per-tile parts most layers
+// of the bs 32 training step have 128): block = 8 channels x 128 part lanes, a lane's (at most 4) parts loaded once; the two passes of
 // Chan's merge (n, sum n_k mean_k -> mean; sum M2_k + n_k (mean_k - mean)^2) read registers, each
 // followed by a fixed pairwise tree over the 128 lanes in f64 (deterministic); then the finalize of
 // bn_finalize_block.  One launch without the two-level form's counter hand-off, whose release /
@@ -1609,7 +1609,7 @@ extern "C" int zp_bn_train_finalize(float* partials, int parts, int C, long long
   hipStream_t st = (hipStream_t)stream;
   // the partials buffer is the caller's scratch (zp_conv2d stats): level 1 merges in place
   int stride = 1;
-  if (parts > 2 * BN_MERGE_R && parts <= BN_MERGE1_MAX) {  // (both key-15 modes: one level, one launch)
+  if (parts <= BN_MERGE1_MAX) {  // (both key-15 modes: one level, one launch)
     hipLaunchKernelGGL(k_bn_stat_merge1, dim3((C + 7) / 8), dim3(1024), 0, st, partials, parts, C, f);
     ZP_LAUNCH_CHECK("zp_bn_train_finalize (one level)");
     return ZP_OK;
