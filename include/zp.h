@@ -149,8 +149,9 @@ int zp_conv2d(const zp_conv_args* a, void* stream);
 int zp_conv_rows_pad(int Cout);
 /* number of pixel tiles (grid_x) a zp_conv2d launch with these args uses */
 int zp_conv2d_grid(const zp_conv_args* a);
-/* number of partial-sum slots `stats` needs: (pixel tile / 64) * grid_x * nsub (one per wave half), or
- * one per 256-pixel tile where the 16-bit strip kernel merges its wave halves first (round 5) */
+/* number of partial-sum slots `stats` needs: one per pixel tile and sub-problem (round 5: the conv
+ * kernels merge their wave halves in LDS first; the split-fp32 forms and k_conv_strip, ZP_CONV_FLAGS
+ * without 64, keep one per wave half: (pixel tile / 64) * grid_x * nsub) */
 int zp_conv2d_stat_parts(const zp_conv_args* a);
 /* number of partial-sum slots a launch with bnr_part emits: zp_conv2d_stat_parts, or one per
  * 256-pixel tile where the strip kernel sums its wave halves first (ABI 3) */

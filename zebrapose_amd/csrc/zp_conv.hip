@@ -815,7 +815,9 @@ __global__ void __launch_bounds__(128 * NWP) k_conv(const zp_conv_args A, const 
 
   if (pingpong && wid < 4) __builtin_amdgcn_s_barrier();  // same barrier count for both groups
 
-  conv_epilogue<T, WC, WP, NWP>(A, S, acc, p0, c0, wc, wp, lane, M, GHW, bx, blockIdx.z, gridDim.z, TG.rflag);
+  // (lds0 as the epilogue's LDS scratch: the BN partials of the tile's wave halves meet there)
+  conv_epilogue<T, WC, WP, NWP>(A, S, acc, p0, c0, wc, wp, lane, M, GHW, bx, blockIdx.z, gridDim.z, TG.rflag,
+                                (float*)lds0);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1770,7 +1772,8 @@ __global__ void __launch_bounds__(512) k_conv_quad(const zp_conv_args A, const q
     if (sm == 1.f) ((float*)A.sub[0].y)[tid] = sm;
   } else {
     static_for<4>([&](auto ph) {
-      conv_epilogue<T, WC, WP, NWP>(A, A.sub[ph], acc[ph], p0, c0, wc, wp, lane, M, GHW, bx, ph, 4);
+      conv_epilogue<T, WC, WP, NWP>(A, A.sub[ph], acc[ph], p0, c0, wc, wp, lane, M, GHW, bx, ph, 4, nullptr,
+                                    (float*)lds);
     });
   }
 }
@@ -2975,8 +2978,8 @@ extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
     qg.w_bytes = tg.w_bytes[0];
     const int qgx = (int)(((long)a.N * a.GH * a.GW) / 256);
     const dim3 grid(qgx, gy, 1);
-    ZP_CHECK_ARG(!(a.stats || a.bnr_part) || 4 * 4 * qgx == zp_conv2d_stat_parts(&a),
-                 "zp_conv2d: quad launch emits %d stat parts, zp_conv2d_stat_parts says %d", 16 * qgx,
+    ZP_CHECK_ARG(!(a.stats || a.bnr_part) || 4 * qgx == zp_conv2d_stat_parts(&a),
+                 "zp_conv2d: quad launch emits %d stat parts, zp_conv2d_stat_parts says %d", 4 * qgx,
                  zp_conv2d_stat_parts(&a));
     const int fl = conv_flags();
 #define ZP_QUAD(T)                                                                             \
@@ -2992,9 +2995,8 @@ extern "C" int zp_conv2d(const zp_conv_args* ap, void* stream) {
   const int nwp = conv_tp(a) / 64;
   const int stages = conv_stages(a, tc);
   {
-    const int launched_nwp = tc == 256 ? 4 : nwp;  // launch_conv_tc256 is always the 256-pixel tile
-    ZP_CHECK_ARG(!(a.stats || a.bnr_part) || launched_nwp * gx * a.nsub == zp_conv2d_stat_parts(&a),
-                 "zp_conv2d: launch emits %d stat parts, zp_conv2d_stat_parts says %d", launched_nwp * gx * a.nsub,
+    ZP_CHECK_ARG(!(a.stats || a.bnr_part) || gx * a.nsub == zp_conv2d_stat_parts(&a),
+                 "zp_conv2d: launch emits %d stat parts, zp_conv2d_stat_parts says %d", gx * a.nsub,
                  zp_conv2d_stat_parts(&a));
   }
 #define ZP_DISPATCH_ST(T, WC, NWP, ST)                                   \
@@ -3217,11 +3219,13 @@ extern "C" int zp_conv2d_wgrad(const zp_wgrad_args* ap, void* ws, void* stream) 
 
 extern "C" int zp_conv2d_stat_parts(const zp_conv_args* a) {
   if (!a) return 0;
-  // k_conv_strip2 merges its wave halves in LDS: one part per 256-pixel tile (round 5)
-  if (a->dtype != ZP_F32 && a->dtype != ZP_F32X3 && a->dtype != ZP_F32H2 && conv_tc(*a) <= 128 &&
-      strip_eligible(*a, nullptr) && (conv_flags() & 64))
-    return (int)(((long)a->N * a->GH * a->GW) / 256);
-  return (conv_tp(*a) / 64) * zp_conv2d_grid(a) * a->nsub;
+  if (a->dtype == ZP_F32X3 || a->dtype == ZP_F32H2) return (conv_tp(*a) / 64) * zp_conv2d_grid(a) * a->nsub;
+  // round 5: k_conv_strip2, k_conv_quad and k_conv merge their wave halves in LDS -- one part per tile
+  // (k_conv_quad: per tile and phase); k_conv_strip (flags & 64 off) keeps one per wave half
+  if (conv_tc(*a) <= 128 && strip_eligible(*a, nullptr))
+    return (int)(((long)a->N * a->GH * a->GW) / 256) * ((conv_flags() & 64) ? 1 : 4);
+  if (quad_plan(*a, nullptr)) return 4 * (int)(((long)a->N * a->GH * a->GW) / 256);
+  return zp_conv2d_grid(a) * a->nsub;
 }
 
 extern "C" int zp_conv2d_bnr_parts(const zp_conv_args* a) {
