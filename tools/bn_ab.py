@@ -54,7 +54,15 @@ def main():
             L.call("zp_bn_bwd_apply", gout.data_ptr(), Cc, 0, y.data_ptr(), Cc, 0, raw.data_ptr(), P, Cc,
                    save.data_ptr(), partials.data_ptr(), gamma.data_ptr(), mode, code, dx.data_ptr(), None, 0, 0, 0,
                    st)
-        legs = {"apply_fwd": fwd, "reduce_m1": lambda: red(1), "reduce_m2": lambda: red(2),
+        def fwd_old():
+            os.environ["ZP_BN_APPLY_U"] = "0"
+            fwd()
+            os.environ["ZP_BN_APPLY_U"] = "1"
+
+        def fwd_res():
+            L.call("zp_bn_apply", raw.data_ptr(), P, Cc, scale.data_ptr(), shift.data_ptr(), gout.data_ptr(), Cc, 0,
+                   1, code, y.data_ptr(), Cc, 0, st)
+        legs = {"apply_fwd": fwd, "apply_old": fwd_old, "apply_res": fwd_res, "reduce_m1": lambda: red(1), "reduce_m2": lambda: red(2),
                 "bwd_apply_m1": lambda: app(1), "bwd_apply_m2": lambda: app(2)}
         fwd()
         times = {k: [] for k in legs}
@@ -69,7 +77,7 @@ def main():
                 torch.cuda.synchronize()
                 times[k].append(e0.elapsed_time(e1) * 1e3 / a.iters)
         T = P * Cc * 2
-        nread = {"apply_fwd": 2, "reduce_m1": 3, "reduce_m2": 2, "bwd_apply_m1": 4, "bwd_apply_m2": 3}
+        nread = {"apply_fwd": 2, "apply_old": 2, "apply_res": 3, "reduce_m1": 3, "reduce_m2": 2, "bwd_apply_m1": 4, "bwd_apply_m2": 3}
         print(spec, " ".join(f"{k} {np.median(v):7.1f}us ({nread[k] * T / np.median(v) / 1e3:5.0f} GB/s)"
                              for k, v in times.items()), flush=True)
 

@@ -45,15 +45,24 @@ __device__ __forceinline__ double gt_value(const void* gt, int gt_f64, size_t id
 }
 
 // per block: [0..L) hamming, [L..2L) bce, [2L] mask sum
+__device__ __forceinline__ double wave_sum(double v) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
 __global__ void __launch_bounds__(256) k_code_partials(const float* __restrict__ clog, const double* __restrict__ m01,
                                                        const float* __restrict__ mlog, const void* __restrict__ gt,
                                                        int gt_f64, int B, int L, int HW, int mask_code,
                                                        double* __restrict__ part) {
-  __shared__ double sh[4];
+  // (round 5) every value is wave-summed into its own LDS slot per wave and the 2L+1 block sums are
+  // taken after one barrier (the per-value block_sum paid two barriers each, 66 per block); the sums
+  // and their order (wave xor tree, then waves 0+1+2+3) are block_sum's, so the partials are unchanged
+  __shared__ double sh[4][2 * LOSS_MAXL + 1];
   const long N = (long)B * HW;
   const long e = (long)blockIdx.x * 256 + threadIdx.x;
   const int nv = 2 * L + 1;
-  double* out = part + (size_t)blockIdx.x * nv;
+  const int w = threadIdx.x >> 6;
+  const bool lead = (threadIdx.x & 63) == 0;
   double m = 0, mraw = 0;
   long b = 0, p = 0;
   const bool ok = e < N;
@@ -63,26 +72,45 @@ __global__ void __launch_bounds__(256) k_code_partials(const float* __restrict__
     m = mask_value(m01, mlog, e);                 // HammingLoss: mask.round().clamp(0, 1)
     mraw = m01 ? m01[e] : m;                      // BinaryCodeLoss :47-48 multiplies by the raw mask
   }
-  for (int i = 0; i < L; ++i) {
-    double h = 0, c = 0;
-    if (ok) {
-      size_t idx = ((size_t)b * L + i) * HW + p;
-      float z = clog[idx];
-      double graw = gt_value(gt, gt_f64, idx);
-      double t2 = rint(graw);
-      t2 = t2 < 0.0 ? 0.0 : (t2 > 1.0 ? 1.0 : t2);
-      double bit = z > kHalf ? 1.0 : 0.0;
-      h = fabs(bit - t2) * m;
-      double zz = mask_code ? mraw * (double)z : (double)z;
-      c = bce_logits(zz, graw);
+  constexpr int LB = 8;  // bits per batch: their loads are issued before any use
+  for (int i0 = 0; i0 < L; i0 += LB) {
+    float zb[LB];
+    double gb[LB];
+#pragma unroll
+    for (int k = 0; k < LB; ++k) {
+      const int i = i0 + k;
+      const size_t idx = ((size_t)b * L + i) * HW + p;
+      zb[k] = (ok && i < L) ? clog[idx] : 0.f;
+      gb[k] = (ok && i < L) ? gt_value(gt, gt_f64, idx) : 0.0;
     }
-    h = block_sum(h, sh);
-    if (threadIdx.x == 0) out[i] = h;
-    c = block_sum(c, sh);
-    if (threadIdx.x == 0) out[L + i] = c;
+#pragma unroll
+    for (int k = 0; k < LB; ++k) {
+      const int i = i0 + k;
+      if (i >= L) break;
+      double h = 0, c = 0;
+      if (ok) {
+        const float z = zb[k];
+        const double graw = gb[k];
+        double t2 = rint(graw);
+        t2 = t2 < 0.0 ? 0.0 : (t2 > 1.0 ? 1.0 : t2);
+        double bit = z > kHalf ? 1.0 : 0.0;
+        h = fabs(bit - t2) * m;
+        double zz = mask_code ? mraw * (double)z : (double)z;
+        c = bce_logits(zz, graw);
+      }
+      h = wave_sum(h);
+      c = wave_sum(c);
+      if (lead) {
+        sh[w][i] = h;
+        sh[w][L + i] = c;
+      }
+    }
   }
-  m = block_sum(m, sh);
-  if (threadIdx.x == 0) out[2 * L] = m;
+  m = wave_sum(m);
+  if (lead) sh[w][2 * L] = m;
+  __syncthreads();
+  const int j = threadIdx.x;
+  if (j < nv) part[(size_t)blockIdx.x * nv + j] = sh[0][j] + sh[1][j] + sh[2][j] + sh[3][j];
 }
 
 // column sums of the per-block partials: one block per column (same summation order as a

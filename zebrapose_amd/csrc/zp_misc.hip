@@ -596,6 +596,47 @@ __global__ void k_bn_apply(const T* __restrict__ x, long P, int C, const float* 
   }
 }
 
+// (round 5) the same pass with U chunks per thread in flight and 32-bit shift indexing, for C/N a
+// power of two dividing 256: a block's chunk runs start at multiples of 256, so a thread's channel
+// chunk is fixed (tid mod C/N) and its scale / shift are loaded once
+template <typename T, int U>
+__global__ void __launch_bounds__(256) k_bn_apply_u(const T* __restrict__ x, unsigned total, int cvs, int C,
+                                                    const float* __restrict__ scale, const float* __restrict__ shift,
+                                                    const T* __restrict__ res, int ldr, int cr0, int relu,
+                                                    T* __restrict__ y, int ldy, int cy0) {
+  constexpr int N = V16<T>::N;
+  const unsigned tid = threadIdx.x;
+  const int c = (int)(tid & ((1u << cvs) - 1u)) * N;
+  float sc[N], sh[N];
+  load_chan<N>(scale + c, sc);
+  load_chan<N>(shift + c, sh);
+  for (unsigned base = blockIdx.x * 256u * U; base < total; base += gridDim.x * 256u * U) {
+    float v[U][N], r[U][N];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const unsigned e = base + k * 256u + tid;
+      if (e < total) {
+        const unsigned p = e >> cvs;
+        V16<T>::load(x + (size_t)p * C + c, v[k]);
+        if (res) V16<T>::load(res + (size_t)p * ldr + cr0 + c, r[k]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const unsigned e = base + k * 256u + tid;
+      if (e >= total) break;
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        float o = __builtin_fmaf(v[k][i], sc[i], sh[i]);
+        if (res) o += r[k][i];
+        if (relu) o = fmaxf(o, 0.f);
+        v[k][i] = o;
+      }
+      V16<T>::store(y + (size_t)(e >> cvs) * ldy + cy0 + c, v[k]);
+    }
+  }
+}
+
 // Pixels per partial slot of the backward reduction: 16 pixel rows per thread row, fewer (down to
 // 4) while that leaves fewer than 512 slots -- 32x32 layers at 256-512 channels would otherwise
 // run on 64 workgroups (more slots make the totals pass, which reads every slot, the slower one).  Rows per block assume 16-byte bf16 lanes (C/8 lanes, at most 256); any
@@ -1418,6 +1459,26 @@ __global__ void k_head_grad(const float* __restrict__ dmask, const float* __rest
   for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
     long b = e / HW, s = e - b * HW;
     T* o = y + e * ldy;
+    if constexpr (sizeof(T) == 2) {
+      if (ldy % 8 == 0) {  // (round 5) 16-byte stores of 8 channels: the 2-byte form took 50 us at bs 32
+        for (int c0 = 0; c0 < ldy; c0 += 8) {
+          uint32_t w[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            uint32_t h[2];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+              const int c = c0 + 2 * q + k;
+              const float v = c == 0 ? dmask[b * HW + s] : (c <= L ? dcode[(b * L + c - 1) * HW + s] : 0.f);
+              h[k] = H16<T>::to(v);
+            }
+            w[q] = h[0] | (h[1] << 16);
+          }
+          *(uint4*)(o + c0) = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+        continue;
+      }
+    }
     o[0] = Elem<T>::cvt(dmask[b * HW + s]);
     for (int c = 0; c < L; ++c) o[1 + c] = Elem<T>::cvt(dcode[(b * L + c) * HW + s]);
     for (int c = L + 1; c < ldy; ++c) o[c] = Elem<T>::cvt(0.f);
@@ -1654,6 +1715,27 @@ extern "C" int zp_bn_apply(const void* x, int P, int C, const float* scale, cons
                "zp_bn_apply: bad args");
   if (res) ZP_CHECK_ARG(ldr % N == 0 && cr0 % N == 0, "zp_bn_apply: residual alignment");
   long total = (long)P * (C / N);
+  const int CV = C / N;
+  const char* ev = getenv("ZP_BN_APPLY_U");  // A/B knob (0: the grid-stride kernel), read per call
+  const int use_u = ev ? atoi(ev) : 1;
+  if (use_u && (CV & (CV - 1)) == 0 && 256 % CV == 0 && total < (1L << 31) - (1L << 20)) {
+    constexpr int U = 4;
+    const int cvs = __builtin_ctz((unsigned)CV);
+    long g = (total + 256L * U - 1) / (256L * U);
+    const dim3 grid((unsigned)(g > 65535 ? 65535 : g));
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == ZP_BF16)
+      hipLaunchKernelGGL((k_bn_apply_u<bf16_t, U>), grid, dim3(256), 0, st, (const bf16_t*)x, (unsigned)total, cvs, C,
+                         scale, shift, (const bf16_t*)res, ldr, cr0, relu, (bf16_t*)y, ldy, cy0);
+    else if (dtype == ZP_F16)
+      hipLaunchKernelGGL((k_bn_apply_u<f16_t, U>), grid, dim3(256), 0, st, (const f16_t*)x, (unsigned)total, cvs, C,
+                         scale, shift, (const f16_t*)res, ldr, cr0, relu, (f16_t*)y, ldy, cy0);
+    else
+      hipLaunchKernelGGL((k_bn_apply_u<float, U>), grid, dim3(256), 0, st, (const float*)x, (unsigned)total, cvs, C,
+                         scale, shift, (const float*)res, ldr, cr0, relu, (float*)y, ldy, cy0);
+    ZP_LAUNCH_CHECK("zp_bn_apply");
+    return ZP_OK;
+  }
   if (dtype == ZP_BF16)
     hipLaunchKernelGGL(k_bn_apply<bf16_t>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
                        (long)P, C, scale, shift, (const bf16_t*)res, ldr, cr0, relu, (bf16_t*)y, ldy, cy0);
