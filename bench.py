@@ -624,6 +624,11 @@ def run(args):
                  "steps": K, "global_batch": world * B, "dtype": tprec, "loss": round(float(loss[0].item()), 5),
                  "achieved_tflops": round(3 * FWD_GFLOP_PER_CROP * 1e9 * world * B * K / tel / 1e12 / world, 2),
                  "parallelism": f"ddp{world}" if world > 1 else "single"}
+        tpk = PEAK["bf16"] if tprec in ("bf16", "fp16") else PEAK["fp32"]
+        train["roofline"] = {"bound": "mfma", "achieved": train["achieved_tflops"], "peak": tpk, "unit": "TFLOP/s",
+                             "frac": round(train["achieved_tflops"] / tpk, 4), "traffic": None,
+                             "scope": "whole step, wall clock: 3 x the forward's algorithmic FLOPs (forward, data "
+                                      "gradient, weight gradient) over the step time, against the dense MFMA peak"}
         train["breakdown"] = train_breakdown(ts, tnet, x, gt_code, gt_mask, world, rank)
         del ts
         if rccl1:
