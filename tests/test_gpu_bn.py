@@ -111,3 +111,43 @@ def test_bn_stat_merge_one_launch_equals_two(gpu, parts, C):
     assert torch.allclose(got_mean, mu, rtol=1e-6, atol=1e-6)
     assert torch.allclose(got_inv, 1.0 / torch.sqrt(var + 1e-5), rtol=1e-6)
     assert int(two[5][0]) == 1
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f16", "f32"])
+@pytest.mark.parametrize("P,Cc,res,relu", [(4096, 64, False, 1), (2048, 256, True, 1), (1000, 512, True, 0),
+                                           (37, 8, False, 1), (513, 2048, True, 1), (300, 24, True, 1),
+                                           (129, 96, False, 0)])
+def test_bn_apply_unrolled_equals_grid_stride(dt, P, Cc, res, relu, monkeypatch):
+    """zp_bn_apply's k_bn_apply_u (C / N a power of two dividing 256: a fixed channel chunk per
+    thread, 4 chunks in flight) against the grid-stride k_bn_apply (ZP_BN_APPLY_U=0, read per call):
+    bit-identical, with and without the residual and ReLU, into a channel slice of a wider buffer;
+    channel counts 24 / 96 (C / N not a power of two) take the grid-stride kernel either way.  Both
+    match y = relu(x * scale + shift (+ res)) in f32 within the storage type's rounding."""
+    import zebrapose_amd._lib as L
+    dev = torch.device("cuda", 0)
+    tdt = {"bf16": torch.bfloat16, "f16": torch.float16, "f32": torch.float32}[dt]
+    code = L.dtype_code(tdt)
+    g = torch.Generator(device="cpu").manual_seed(P * 7 + Cc)
+    x = torch.randn(P, Cc, generator=g).to(tdt).to(dev)
+    r = torch.randn(P, 2 * Cc, generator=g).to(tdt).to(dev) if res else None
+    scale = (torch.rand(Cc, generator=g) + 0.5).to(dev)
+    shift = torch.randn(Cc, generator=g).to(dev)
+    outs = []
+    for knob in ("1", "0"):
+        monkeypatch.setenv("ZP_BN_APPLY_U", knob)
+        y = torch.full((P, 3 * Cc), 7.0, dtype=tdt, device=dev)
+        L.call("zp_bn_apply", x.data_ptr(), P, Cc, scale.data_ptr(), shift.data_ptr(),
+               None if r is None else r.data_ptr(), 2 * Cc, Cc if res else 0, relu, code, y.data_ptr(), 3 * Cc, Cc,
+               L.stream_ptr())
+        torch.cuda.synchronize()
+        outs.append(y)
+    assert torch.equal(outs[0], outs[1])
+    y = outs[0]
+    assert torch.all(y[:, :Cc] == 7.0) and torch.all(y[:, 2 * Cc:] == 7.0)  # outside the slice untouched
+    ref = x.float() * scale + shift
+    if res:
+        ref = ref + r[:, Cc:2 * Cc].float()
+    if relu:
+        ref = ref.clamp_min(0.0)
+    tol = {"bf16": 1e-2, "f16": 2e-3, "f32": 1e-6}[dt]
+    torch.testing.assert_close(y[:, Cc:2 * Cc].float(), ref, rtol=tol, atol=tol)
