@@ -828,16 +828,19 @@ __global__ void __launch_bounds__(256) k_bn_bwd_apply(const T* __restrict__ dy, 
       sgx[i] *= invP;
     }
   }
-  const uint4 z = make_uint4(0, 0, 0, 0);
+  // optional streams loaded under their (uniform) condition and read only under it -- a select
+  // between the stream and a zero constant made the compiler load through a pointer select of
+  // global and private memory (flat loads, a 32-byte private segment)
+  const bool hx = dx != nullptr, hr = dres != nullptr && racc;
   for (long pb = p0 + row; pb < p1; pb += U * R) {
     uint4 gd[U], yd[U], xd[U], rd[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const long pp = min(pb + u * R, p1 - 1);
       gd[u] = *(const uint4*)(dy + pp * lddy + cdy0 + c);
-      yd[u] = relu == 1 ? *(const uint4*)(y + pp * ldy + cy0 + c) : z;
-      xd[u] = dx ? *(const uint4*)(x + pp * C + c) : z;
-      rd[u] = (dres && racc) ? *(const uint4*)(dres + pp * lddres + cdres0 + c) : z;
+      if constexpr (relu == 1) yd[u] = *(const uint4*)(y + pp * ldy + cy0 + c);
+      if (hx) xd[u] = *(const uint4*)(x + pp * C + c);
+      if (hr) rd[u] = *(const uint4*)(dres + pp * lddres + cdres0 + c);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
