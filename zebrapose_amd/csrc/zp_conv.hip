@@ -2571,30 +2571,62 @@ __global__ void __launch_bounds__(512) k_wgrad2(const zp_wgrad_args A, float* __
     }
 }
 
-// ws (summed over splits) -> dw in the weight's own layout
-__global__ void k_wgrad_reduce(const zp_wgrad_args A, const float* __restrict__ ws, int splits, int cols_max) {
+// ws (summed over splits) -> dw in the weight's own layout.  Per element the splits are summed into
+// 8 partial sums (split k into q[k % 8] for the whole batches of 8, the rest into q[0]), combined as
+// ((q0 + q1) + (q2 + q3)) + ((q4 + q5) + (q6 + q7)): fixed order, deterministic.  (Round 5) up to 32
+// splits' loads are issued before their adds (the same adds in the same order as batches of 8; one
+// batch of 8 in flight left the launch bound by 3-4 dependent memory round trips per thread), and
+// the element index is 32-bit.
+__global__ void __launch_bounds__(256) k_wgrad_reduce(const zp_wgrad_args A, const float* __restrict__ ws, int splits,
+                                                      int cols_max) {
   const int sub = blockIdx.y;
   const auto& S = A.sub[sub];
-  const int cols = S.ntaps * A.Cin;
-  const long total = (long)A.Cout * cols;
-  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    const int co = (int)(e / cols), col = (int)(e - (long)co * cols);
-    const int t = col / A.Cin, ci = col - t * A.Cin;
+  const unsigned cols = (unsigned)(S.ntaps * A.Cin);
+  const unsigned total = (unsigned)A.Cout * cols;
+  const size_t stride = (size_t)A.nsub * A.Cout * cols_max;
+  for (unsigned e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    const unsigned co = e / cols, col = e - co * cols;
+    const int t = (int)(col / (unsigned)A.Cin), ci = (int)col - t * A.Cin;
     const int ky = S.ky[t], kx = S.kx[t];
     if (ci >= A.Cw || ky < 0) continue;  // padded input channels / padding taps
-    // 8 independent partial sums (loads in flight together; fixed order -> deterministic)
-    const size_t stride = (size_t)A.nsub * A.Cout * cols_max;
     const float* p = ws + ((size_t)sub * A.Cout + co) * cols_max + col;
     float q[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     int k = 0;
-    for (; k + 8 <= splits; k += 8) {
+    for (; k + 32 <= splits; k += 32) {
+      float v[32];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) v[u] = p[(size_t)(k + u) * stride];
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int u = 0; u < 8; ++u) q[u] += v[8 * b + u];
+    }
+    if (k + 16 <= splits) {
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = p[(size_t)(k + u) * stride];
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int u = 0; u < 8; ++u) q[u] += v[8 * b + u];
+      k += 16;
+    }
+    if (k + 8 <= splits) {
       float v[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) v[u] = p[(size_t)(k + u) * stride];
 #pragma unroll
       for (int u = 0; u < 8; ++u) q[u] += v[u];
+      k += 8;
     }
-    for (; k < splits; ++k) q[0] += p[(size_t)k * stride];
+    {
+      float v[7];  // the remaining < 8 splits, loaded together, added to q[0] in split order
+#pragma unroll
+      for (int u = 0; u < 7; ++u) v[u] = k + u < splits ? p[(size_t)(k + u) * stride] : 0.f;
+#pragma unroll
+      for (int u = 0; u < 7; ++u)
+        if (k + u < splits) q[0] += v[u];
+    }
     const float s = ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
     size_t idx = A.transposed_w ? (((size_t)ci * A.Cout + co) * A.kh + ky) * A.kw + kx
                                 : (((size_t)co * A.Cw + ci) * A.kh + ky) * A.kw + kx;
