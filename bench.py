@@ -427,6 +427,51 @@ def pmc_traffic(kname):
     return None, f"no committed PMC pass of this libzp.so build (lib_sha16 {sha})"
 
 
+def train_pmc():
+    """The newest committed training-step PMC summary (tools/prof_train.py ->
+    profiles/<tag>_train_pmc_traffic.json) measured on THIS libzp.so build, or (None, reason)."""
+    sha = lib_sha16()
+    for pf in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_train_pmc_traffic.json")), reverse=True):
+        with open(pf) as fh:
+            d = json.load(fh)
+        if d.get("lib_sha16") == sha and "step" in d:
+            return d, os.path.relpath(pf, ROOT)
+    return None, f"no committed training PMC pass of this libzp.so build (lib_sha16 {sha})"
+
+
+def train_kernel_roofline(ts, tnet, x, gt_code, gt_mask, steps=2):
+    """The dominant training kernel (largest total time over one step's conv / weight-gradient
+    launches): every launch bracketed by HIP events on the stream it runs on (engine timing: the
+    weight gradients then run on the compute stream, not the side stream); achieved = algorithmic
+    FLOPs / launch time against the bf16 dense peak; traffic per launch from the training PMC pass of
+    this build (VERDICT r5 #7)."""
+    eng = tnet.net._engine
+    per = {}
+    for _ in range(steps):
+        eng.timing = []
+        ts(x, gt_code, gt_mask)
+        torch.cuda.synchronize()
+        for label, e0, e1, flops, kname, nbytes in eng.timing:
+            d = per.setdefault(kname, [0.0, 0.0, 0, 0.0])
+            d[0] += flops
+            d[1] += e0.elapsed_time(e1) * 1e-3
+            d[2] += 1
+            d[3] += nbytes
+    eng.timing = None
+    kname, (fl, tsec, nl, nb) = max(per.items(), key=lambda kv: kv[1][1])
+    pmc, src = train_pmc()
+    row = (pmc or {}).get("by_label", {}).get(kname)
+    traffic = None if row is None else row["hbm_bytes_per_launch"]
+    achieved = fl / tsec / 1e12
+    return {"kernel": kname, "launches_per_step": nl // steps, "avg_launch_us": round(tsec / nl * 1e6, 2),
+            "achieved": round(achieved, 2), "peak": PEAK["bf16"], "unit": "TFLOP/s",
+            "frac": round(achieved / PEAK["bf16"], 4), "algorithmic_flop_per_launch": round(fl / nl),
+            "algorithmic_bytes_per_launch": round(nb / nl), "traffic": traffic,
+            "traffic_over_algorithmic": None if traffic is None else round(traffic / (nb / nl), 3),
+            "traffic_source": src if row is not None else (src if pmc is None else f"{src}: no row for {kname}"),
+            "share_of_conv_time": round(tsec / sum(v[1] for v in per.values()), 3)}
+
+
 def time_infer(net, x, dec, bboxes, steps, warmup, world, dev, rank, use_graph=True):
     """configs[1] step = forward + on-device decode of one bs=B batch resident in HBM.  The timed
     step is one hipGraph replay of that step (zebrapose_amd.graphs; the crops are copied into the
@@ -629,7 +674,17 @@ def run(args):
                              "frac": round(train["achieved_tflops"] / tpk, 4), "traffic": None,
                              "scope": "whole step, wall clock: 3 x the forward's algorithmic FLOPs (forward, data "
                                       "gradient, weight gradient) over the step time, against the dense MFMA peak"}
+        pmc, psrc = train_pmc()
+        if pmc is not None:  # whole-step HBM bytes from the training PMC passes of this build
+            st = pmc["step"]
+            train["roofline"].update(
+                traffic=st["hbm_bytes"], traffic_unit="HBM bytes per training step (PMC, one-stream step)",
+                traffic_source=psrc,
+                hbm_gbps_over_step=round(st["hbm_bytes"] / (train["ms_per_step"] * 1e-3) / 1e9, 1))
+        else:
+            train["roofline"]["traffic_source"] = psrc
         train["breakdown"] = train_breakdown(ts, tnet, x, gt_code, gt_mask, world, rank)
+        train["roofline"]["dominant_kernel"] = train_kernel_roofline(ts, tnet, x, gt_code, gt_mask)
         del ts
         if rccl1:
             ts = TrainStep(tnet, learning_rate=lr, ddp=True, device=local)

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define ZP_ABI_VERSION 3
+#define ZP_ABI_VERSION 4
 
 #define ZP_OK 0
 #define ZP_ERR_ARG 1
@@ -182,7 +182,9 @@ long long zp_conv2d_split_ws(const zp_conv_args* a);
  * (default 1, 0 off); keys 10-12 = the 256 x 256 two-plane tile (on / fewest workgroups / split-K);
  * key 13 = its accumulation form (0 the flushed correction accumulator, default; 1 one scaled
  * accumulator; 2 per-step partial sums; 3 flushed on the 2^11 scale); key 14 = its 256 x 128 tile
- * (default 0); key 15 = zp_bn_train_finalize's merge in one launch (1, default) or two (0).  Returns
+ * (default 0); key 15 = zp_bn_train_finalize's merge in one launch (1, default) or two (0); key 16 =
+ * k_conv3's multi-sub launches with a tile's subs adjacent on one XCD (default 0); key 17 = k_conv3w's
+ * multi-sub launches (ConvT phases) with a pixel tile's phases adjacent on one XCD (default 1).  Returns
  * the previous value, -1 for an unknown key. */
 int zp_conv_tuning(int key, int value);
 
@@ -270,11 +272,16 @@ int zp_bn_fold(const float* gamma, const float* beta, const float* mean, const f
  * update running stats (momentum, unbiased var; the conv bias, if any, is added to the mean)
  * and emit scale/shift for the apply pass, plus save[4][C] = (mean, invstd, scale, shift) of the
  * raw values (shift = fma(-mean, scale, beta)).
- * partials is scratch: a first merge level overwrites it in place (every 64th part). */
+ * partials is scratch: a first merge level overwrites it in place (every 64th part).
+ * ABI 4: partials holds zp_bn_finalize_floats(parts, C) floats -- the [3][parts][C] statistics and,
+ * past them, the one-launch merge's per-launch hand-off counters (zeroed on `stream` by this call),
+ * so concurrent finalizes on different streams or hipGraphs never share counters. */
 int zp_bn_train_finalize(float* partials, int parts, int C, long long count, float eps,
                          float momentum, const float* gamma, const float* beta, const float* conv_bias,
                          float* running_mean, float* running_var, int64_t* num_batches_tracked,
                          float* scale, float* shift, float* save, void* stream);
+/* size in floats of zp_bn_train_finalize's partials buffer for (parts, C) (ABI 4) */
+long long zp_bn_finalize_floats(int parts, int C);
 /* y[p, cy0+c] = act(fma(x[p, c], scale[c], shift[c]) (+ res[p, cr0+c])), x: raw conv output [P][C] */
 int zp_bn_apply(const void* x, int P, int C, const float* scale, const float* shift,
                 const void* res, int ldr, int cr0, int relu, int dtype, void* y, int ldy, int cy0,

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
 def test_python_binding_covers_header():
     from zebrapose_amd import _lib
     assert set(_declared()) <= set(_lib._SIGS), set(_declared()) - set(_lib._SIGS)
-    assert _lib.lib.zp_abi_version() == 3
+    assert _lib.lib.zp_abi_version() == 4
 
 
 def test_struct_layout():

@@ -86,7 +86,8 @@ def test_bn_stat_merge_one_launch_equals_two(gpu, parts, C):
     def run(mode):
         old = L.lib.zp_conv_tuning(15, mode)
         try:
-            part = base.clone().to(gpu)
+            part = torch.empty(L.lib.zp_bn_finalize_floats(parts, C), device=gpu)
+            part[:base.numel()] = base.reshape(-1).to(gpu)
             rm, rv = torch.zeros(C, device=gpu), torch.ones(C, device=gpu)
             nbt = torch.zeros(1, dtype=torch.int64, device=gpu)
             sc, sh = torch.empty(C, device=gpu), torch.empty(C, device=gpu)
@@ -111,6 +112,61 @@ def test_bn_stat_merge_one_launch_equals_two(gpu, parts, C):
     assert torch.allclose(got_mean, mu, rtol=1e-6, atol=1e-6)
     assert torch.allclose(got_inv, 1.0 / torch.sqrt(var + 1e-5), rtol=1e-6)
     assert int(two[5][0]) == 1
+
+
+def test_bn_stat_merge_concurrent_streams(gpu):
+    """the one-launch merge's hand-off counters are per launch (ABI 4: in the caller's
+    partials buffer, zeroed on the launch's stream).  Six finalizes of >512 parts enqueued round-robin
+    on three streams without waiting, so their level-1 blocks interleave, each equal bit for bit to
+    the same finalize run alone."""
+    from zebrapose_amd import _lib as L
+    C, parts = 256, 4100
+    streams = [torch.cuda.Stream(device=gpu) for _ in range(3)]
+    cases = []
+    for i in range(6):
+        g = torch.Generator().manual_seed(100 + i)
+        cnt = torch.randint(1, 33, (parts, C), generator=g).float()
+        base = torch.cat([cnt, torch.randn(parts, C, generator=g) * 3 + i, torch.rand(parts, C, generator=g) * cnt])
+        cases.append((base.to(gpu), (torch.rand(C, generator=g) + 0.5).to(gpu), torch.randn(C, generator=g).to(gpu),
+                      int(cnt.sum())))
+
+    def launch(case, st):
+        base, gamma, beta, count = case
+        part = torch.empty(L.lib.zp_bn_finalize_floats(parts, C), device=gpu)
+        part[:base.numel()].copy_(base.reshape(-1))
+        out = [torch.zeros(C, device=gpu), torch.ones(C, device=gpu), torch.zeros(1, dtype=torch.int64, device=gpu),
+               torch.empty(C, device=gpu), torch.empty(C, device=gpu), torch.empty(4 * C, device=gpu)]
+        torch.cuda.synchronize()
+        with torch.cuda.stream(st):
+            L.call("zp_bn_train_finalize", part.data_ptr(), parts, C, count, 1e-5, 0.1, gamma.data_ptr(),
+                   beta.data_ptr(), None, out[0].data_ptr(), out[1].data_ptr(), out[2].data_ptr(), out[3].data_ptr(),
+                   out[4].data_ptr(), out[5].data_ptr(), st.cuda_stream)
+        return part, out
+
+    alone = []
+    for c in cases:
+        _, out = launch(c, streams[0])
+        torch.cuda.synchronize()
+        alone.append([t.cpu() for t in out])
+    # concurrent: all buffers prepared first, then every launch enqueued before any wait
+    prepared = []
+    for c in cases:
+        base, gamma, beta, count = c
+        part = torch.empty(L.lib.zp_bn_finalize_floats(parts, C), device=gpu)
+        part[:base.numel()].copy_(base.reshape(-1))
+        prepared.append((part, [torch.zeros(C, device=gpu), torch.ones(C, device=gpu),
+                                torch.zeros(1, dtype=torch.int64, device=gpu), torch.empty(C, device=gpu),
+                                torch.empty(C, device=gpu), torch.empty(4 * C, device=gpu)], gamma, beta, count))
+    torch.cuda.synchronize()
+    for i, (part, out, gamma, beta, count) in enumerate(prepared):
+        st = streams[i % 3]
+        L.call("zp_bn_train_finalize", part.data_ptr(), parts, C, count, 1e-5, 0.1, gamma.data_ptr(), beta.data_ptr(),
+               None, out[0].data_ptr(), out[1].data_ptr(), out[2].data_ptr(), out[3].data_ptr(), out[4].data_ptr(),
+               out[5].data_ptr(), st.cuda_stream)
+    torch.cuda.synchronize()
+    for (part, out, *_), ref in zip(prepared, alone):
+        for a, b in zip(out, ref):
+            assert torch.equal(a.cpu(), b)
 
 
 @pytest.mark.parametrize("dt", ["bf16", "f16", "f32"])

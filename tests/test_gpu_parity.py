@@ -325,6 +325,38 @@ def test_fused_adam_multi_tensor_matches_torch():
         np.testing.assert_allclose(d.detach().cpu().numpy(), r.detach().numpy(), rtol=1e-6, atol=1e-8)
 
 
+@pytest.mark.parametrize("capturable", [False, True])
+def test_fused_adam_intermittent_none_grad(capturable):
+    """a parameter whose gradient is None at step 2 only (present at 1, 3, 4, 5).  Step 1
+    builds the cached launch plan, step 2 takes the general path (advancing all but one tensor),
+    steps 3.. must not reuse a plan that assumes one shared step count: bias correction per tensor
+    as torch.optim.Adam, and the saved 'step' state per tensor."""
+    from zebrapose_amd.optim import FusedAdam
+    torch.manual_seed(4)
+    sizes = [17, 4096, 5, 300]
+    ref = [torch.randn(n, dtype=torch.float32, requires_grad=True) for n in sizes]
+    dev = [r.detach().clone().cuda().requires_grad_(True) for r in ref]
+    o_ref = torch.optim.Adam(ref, lr=1e-2)
+    o = FusedAdam(dev, lr=1e-2, capturable=capturable)
+    for s in range(5):
+        for i, (r, d) in enumerate(zip(ref, dev)):
+            if i == 1 and s == 1:
+                r.grad, d.grad = None, None
+                continue
+            g = torch.randn(r.shape) * (s + 1)
+            r.grad = g.clone()
+            d.grad = g.cuda()
+        o_ref.step()
+        o.step()
+    torch.cuda.synchronize()
+    sd, sd_ref = o.state_dict()["state"], o_ref.state_dict()["state"]
+    for i in range(len(sizes)):
+        assert float(sd[i]["step"]) == float(sd_ref[i]["step"]), i
+    assert float(sd[1]["step"]) == 4.0 and float(sd[0]["step"]) == 5.0
+    for r, d in zip(ref, dev):
+        np.testing.assert_allclose(d.detach().cpu().numpy(), r.detach().numpy(), rtol=1e-6, atol=1e-8)
+
+
 def test_binary_code_helper_dropins(golden):
     """Reference-signature helpers (host arrays in/out, device decode inside)."""
     from zebrapose_amd.binary_code_helper.CNN_output_to_pose import decode_correspondences

@@ -6,7 +6,8 @@ RCCL-stream hand-off, finish()'s wait(), the per-forward BN buffer broadcast; an
 DistributedDataParallel(net) over the libzp network (ZP_TORCH_DDP=1).
 
 At world size 1 the mean over ranks is the local gradient, so the averaged gradients must equal
-the plain local ones BIT FOR BIT (the backward is deterministic: fixed-order split reductions)."""
+the plain local ones BIT FOR BIT (the backward is deterministic: fixed-order split reductions), and
+under GradBuckets every gradient is a view of its bucket (round 6: written there by the engine)."""
 import os
 import socket
 
@@ -100,6 +101,12 @@ def _worker(port, mode, q):
         res = {"mode": mode, "diffs": diffs, "bcast": calls["bcast"] - bc0, "nparams": len(local),
                "hook_progress": {n: list(v) for n, v in seen.items()}}
         if mode == "buckets":
+            # gradient as bucket view (round 6): every p.grad lies inside its bucket's flat buffer --
+            # written there by the engine, adopted by AccumulateGrad without a clone
+            spans = [(bk[0].data_ptr(), bk[0].data_ptr() + bk[0].numel() * bk[0].element_size())
+                     for bk in ts.buckets.buckets]
+            res["outside_bucket"] = [n for n, p in net.named_parameters()
+                                     if not any(lo <= p.grad.data_ptr() < hi for lo, hi in spans)]
             res["nbuckets"] = len(ts.buckets.buckets)
             res["launched"] = len(works)
             res["completed"] = sum(1 for w in works if w.is_completed())
@@ -163,3 +170,4 @@ def test_rccl_world1_grad_exchange(gpu, mode):
         assert res["done_event"] == 1
         assert res["bcast"] == 1  # rank 0's BN buffers broadcast before the forward
         assert res["allreduce_identity"]
+        assert not res["outside_bucket"], res["outside_bucket"]

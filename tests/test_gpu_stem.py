@@ -57,3 +57,34 @@ def test_stem_nchw_equals_nhwc_and_is_f32_accurate(gpu, B, H):
     e, ef = float((got - ref).abs().max()), float((f32 - ref).abs().max())
     print(f"stem B={B} {H}x{H}: max |d| two-plane {e:.3g}, CPU f32 conv {ef:.3g} (scale {scale:.3g})")
     assert e <= 4.0 * ef + 2.0 ** -21 * scale, (e, ef, scale)
+
+
+@pytest.mark.parametrize("knob", ["split_stem", "stem_direct"])
+def test_stem_knobs_keep_fp32_eval_working(gpu, golden, knob):
+    """nchw_stem (the NCHW input handed to the stem) and unit_fwd's zp_stem_split branch
+    share one predicate.  With ZP_SPLIT_STEM=0 (the exact-f32 small-Cin stem) or ZP_STEM_DIRECT=0 (the
+    im2col stem) the fp32 eval forward must still run -- from the NHWC copy -- and stay within the
+    north star's 1e-3 of the default two-plane forward and of the reference's logits at 64x64."""
+    from oracle import ref_cpu
+    from zebrapose_amd import _lib as L
+    from zebrapose_amd.model.BinaryCodeNet import BinaryCodeNet_Deeplab
+    bn = dict(golden("r34_bn_buffers.npz"))
+    sd = ref_cpu.synthetic_state(34, 16, 0, bn)
+    net = BinaryCodeNet_Deeplab(34, 16, 2, concat=True, output_kernel_size=1, precision="fp32")
+    net.load_state_dict(sd)
+    net = net.cuda().eval()
+    f = golden("r34_fwd64.npz")
+    x = torch.from_numpy(f["fwd64_x"]).cuda()
+    with torch.no_grad():
+        m0, c0 = (t.clone() for t in net(x))
+        eng = net.eval_engine()
+        assert eng.dt == L.ZP_F32H2
+        setattr(eng, knob, False)
+        m1, c1 = net(x)
+    torch.cuda.synchronize()
+    for a, b, ref in ((m0, m1, f["fwd64_mask"]), (c0, c1, f["fwd64_code"])):
+        assert torch.isfinite(b).all()
+        assert float((a - b).abs().max()) <= 1e-3, float((a - b).abs().max())
+        # and the reference's own logits (the fixture), as tests/test_gpu_parity.py holds the default
+        r = torch.from_numpy(ref).cuda()
+        assert float(((b - r).abs() - 1e-4 * r.abs()).max()) <= 1e-3

@@ -178,6 +178,41 @@ def test_unit_fp16_eval(gpu, geom, tile_mode):
     assert err <= 4e-3 * max(1.0, scale), f"forward max|d| {err} (scale {scale})"
 
 
+# configs[4]'s ResNet50-OS8 + ASPP_50 widths (reference model/resnet.py:206-227: torchvision's
+# Bottleneck layer1 / layer2 at 64 x 64 / 32 x 32, then BasicBlocks 512 -> 1024 at dilation 2 and
+# 1024 -> 2048 at dilation 4; model/aspp.py:117-225: 2048 -> 256 branches, up2's ConvT over the
+# [up1 | x_64] concat of 256 + 256 channels), each at the 32 x 32 / 64 x 64 grid it runs on
+R50_GEOMS = [
+    ("conv", 64, 64, 1, 1, 0, 1, False, 64),      # layer1 Bottleneck conv1 (1x1 reduce)
+    ("conv", 64, 256, 1, 1, 0, 1, False, 64),     # conv3 (1x1 expand) / downsample
+    ("conv", 256, 64, 1, 1, 0, 1, False, 64),     # the next blocks' conv1
+    ("conv", 256, 128, 1, 1, 0, 1, False, 64),    # layer2 block 0 conv1
+    ("conv", 128, 128, 3, 2, 1, 1, False, 64),    # its strided 3x3 (torchvision v1.5: stride on the 3x3)
+    ("conv", 256, 512, 1, 2, 0, 1, False, 64),    # its strided downsample
+    ("conv", 128, 512, 1, 1, 0, 1, False, 32),    # layer2 conv3
+    ("conv", 512, 1024, 3, 1, 2, 2, False, 32),   # layer4 block 0 conv1 (BasicBlock, dilation 2)
+    ("conv", 512, 1024, 1, 1, 0, 1, False, 32),   # its downsample
+    ("conv", 1024, 1024, 3, 1, 2, 2, False, 32),  # layer4 3x3s
+    ("conv", 1024, 2048, 3, 1, 4, 4, False, 32),  # layer5 block 0 conv1 (dilation 4)
+    ("conv", 1024, 2048, 1, 1, 0, 1, False, 32),  # its downsample
+    ("conv", 2048, 2048, 3, 1, 4, 4, False, 32),  # layer5 3x3s
+    ("conv", 2048, 256, 1, 1, 0, 1, True, 32),    # ASPP_50 conv_1x1_1
+    ("conv", 2048, 256, 3, 1, 6, 6, True, 32),    # conv_3x3_1
+    ("conv", 2048, 256, 3, 1, 12, 12, True, 32),  # conv_3x3_2
+    ("conv", 2048, 256, 3, 1, 18, 18, True, 32),  # conv_3x3_3
+    ("convT", 512, 256, 3, 2, 1, 1, False, 64),   # up2's ConvT over [up1 | x_64]
+]
+
+
+@pytest.mark.parametrize("geom", R50_GEOMS, ids=[f"{g[0]}{g[1]}-{g[2]}k{g[3]}s{g[4]}d{g[6]}h{g[8]}" for g in R50_GEOMS])
+def test_unit_fp16_eval_r50(gpu, geom, tile_mode):
+    """the fp16 kernels at configs[4]'s R50 widths, per op, against the fp32 CPU
+    reference on fp16-representable inputs (4e-3 of the output scale, as test_unit_fp16_eval).  The
+    whole R50 fp16 forward is replayed op by op from the device's own inputs in
+    test_gpu_multi_object.py::test_configs4_r50_fp16_teacher_forced."""
+    test_unit_fp16_eval(gpu, geom, tile_mode)
+
+
 @pytest.mark.parametrize("prec", ["fp32", "bf16", "fp16"])
 def test_maxpool(gpu, prec):
     from zebrapose_amd import _lib as L

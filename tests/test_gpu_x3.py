@@ -557,8 +557,11 @@ def test_schedule_flags_are_bit_identical(gpu, geom, B, kernel, tp128):
     outs = {}
     old14 = L.lib.zp_conv_tuning(14, tp128)
     try:
-        for extra in [0] + _BITWISE_FLAGS:
-            old = L.lib.zp_conv_tuning(1, 478 + extra)
+        # (round 6) "subint0": zp_conv_tuning key 17 = 0, the ConvT phases dispatched phase by phase
+        # instead of interleaved per pixel tile on one XCD (the default)
+        for extra in [0] + _BITWISE_FLAGS + ["subint0"]:
+            old = L.lib.zp_conv_tuning(1, 478 + (0 if extra == "subint0" else extra))
+            old17 = L.lib.zp_conv_tuning(17, 0 if extra == "subint0" else -1)
             try:
                 oa = Act(eng._empty((B, OH, OW, cout), gpu))
                 eng.stage_log = []
@@ -566,11 +569,12 @@ def test_schedule_flags_are_bit_identical(gpu, geom, B, kernel, tp128):
                 torch.cuda.synchronize()
             finally:
                 L.lib.zp_conv_tuning(1, old)
+                L.lib.zp_conv_tuning(17, old17)
             outs[extra] = oa.buf._base.clone()
     finally:
         L.lib.zp_conv_tuning(14, old14)
     names = [r[1] for r in eng.stage_log]
     print(geom, names)
     assert names == [kernel], names
-    for extra in _BITWISE_FLAGS:
+    for extra in _BITWISE_FLAGS + ["subint0"]:
         assert torch.equal(outs[extra], outs[0]), (geom, extra)

@@ -29,7 +29,8 @@ def main():
     ap.add_argument("--layer-report", default=None)
     ap.add_argument("--mode", default="train", choices=["train", "infer"])
     ap.add_argument("--stage-log", default=None, help="infer: write the last step's conv launches (stage, kernel, "
-                                                       "flops, algorithmic bytes) in launch order here")
+                                                       "flops, algorithmic bytes) in launch order here; train: "
+                                                       "per kernel label, one step's launches, FLOPs and bytes")
     a = ap.parse_args()
     from bench import lib_sha16
     print(f"lib_sha16 {lib_sha16()}", flush=True)
@@ -78,6 +79,23 @@ def main():
     for _ in range(a.warmup):
         ts(x, gt_code, gt_mask)
     torch.cuda.synchronize()
+    if a.stage_log:  # train: per kernel label, the step's launches, algorithmic FLOPs and bytes (engine timing)
+        from bench import lib_sha16
+        eng = net.net._engine
+        eng.timing = []
+        ts(x, gt_code, gt_mask)
+        torch.cuda.synchronize()
+        agg = {}
+        for label, e0, e1, flops, kname, nbytes in eng.timing:
+            d = agg.setdefault(kname, {"launches": 0, "flops": 0.0, "bytes": 0.0, "us": 0.0})
+            d["launches"] += 1
+            d["flops"] += flops
+            d["bytes"] += nbytes
+            d["us"] += e0.elapsed_time(e1) * 1e3
+        eng.timing = None
+        with open(a.stage_log, "w") as f:
+            json.dump({"precision": a.precision, "batch": a.batch, "lib_sha16": lib_sha16(), "mode": "train",
+                       "kernels": agg}, f, indent=1)
     if a.layer_report:
         eng = net.net._engine
         eng.timing = []

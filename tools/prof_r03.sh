@@ -8,6 +8,8 @@
 #                SQ_VALU_MFMA_BUSY_CYCLES + GRBM_GUI_ACTIVE + SQ_INSTS_VALU_MFMA_MOPS_{BF16,F32}
 #   train_1s     kernel-trace --stats of the bs=32 bf16 training step on ONE stream
 #                (ZP_SIDE_WGRAD=0: weight gradients not overlapped, so per-kernel durations attribute)
+#   ttrace / tfetch / twrite (TRAIN_PMC=1, round 6)   kernel trace + FETCH_SIZE + WRITE_SIZE passes over
+#                the same one-stream training step (tools/prof_train.py)
 # Summarise with tools/prof_stages.py <tag>.
 set -e -o pipefail
 TAG=${1:-r03}
@@ -35,5 +37,15 @@ if [ -z "$NO_TRAIN" ]; then
   ZP_SIDE_WGRAD=0 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/train_1s -o run -- \
       python3 tools/prof_driver.py --mode train --steps 5 --warmup 2 > $O/train_1s.log 2>&1
   echo "train ok"
+fi
+if [ -n "$TRAIN_PMC" ]; then  # round 6: counter passes over the training step (tools/prof_train.py)
+  T="python3 tools/prof_driver.py --mode train --steps 3 --warmup 2"
+  ZP_SIDE_WGRAD=0 timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d $O/ttrace -o run -- \
+      $T --stage-log $O/stage_log_train.json > $O/ttrace.log 2>&1
+  ZP_SIDE_WGRAD=0 timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/tfetch -o run -- \
+      $T > $O/tfetch.log 2>&1
+  ZP_SIDE_WGRAD=0 timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/twrite -o run -- \
+      $T > $O/twrite.log 2>&1
+  echo "train pmc ok"
 fi
 echo done

@@ -138,7 +138,18 @@ def stage_table(src, prec):
     at = attribute(tr, log["launches"])
     st = {s: defaultdict(float) for s in STAGES + ["other"]}
     per_kernel = defaultdict(lambda: defaultdict(float))
+    disp = []  # round 6: every conv dispatch of the step (traffic per launch against its algorithmic bytes)
     for (stage, t, ent), f, w, m in zip(at, fe, wr, mf):
+        if ent is not None:
+            rd, wb = 2.0 * 1024.0 * f[2].get("FETCH_SIZE", 0.0), 1024.0 * w[2].get("WRITE_SIZE", 0.0)
+            g = m[2].get("GRBM_GUI_ACTIVE", 0.0)
+            disp.append({"stage": stage, "kernel": ent["kernel"], "geo": ent.get("geo"), "us": round(t[2] / 1e3, 2),
+                         "tflops": round(ent["flops"] / t[2] / 1e3, 1) if t[2] else None,
+                         "read_mb": round(rd / 1e6, 2), "write_mb": round(wb / 1e6, 2),
+                         "algo_mb": round(ent["bytes"] / 1e6, 2),
+                         "traffic_over_algo": round((rd + wb) / ent["bytes"], 3) if ent["bytes"] else None,
+                         "mfma_busy_pct": round(100.0 * m[2].get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (g / 8.0 * 1024.0), 1)
+                         if g else None})
         d = st[stage]
         d["dispatches"] += 1
         d["ns"] += t[2]
@@ -178,7 +189,7 @@ def stage_table(src, prec):
                 "mfma_busy_pct": round(100.0 * v["mfma_busy"] / (v["grbm"] / 8.0 * 1024.0), 1) if v["grbm"] else None}
             for k, v in per_kernel.items()}
     return {"precision": prec, "batch": log["batch"], "lib_sha16": log["lib_sha16"], "stages": rows,
-            "split_form": form, "kernels": kern}
+            "split_form": form, "kernels": kern, "dispatches": disp}
 
 
 def summarise(name, d, prec, form=None):
@@ -259,6 +270,13 @@ def main(tag="r03", precs=("fp32", "bf16")):
         with open(os.path.join(dst, f"{tag}_stages_{p}.json"), "w") as fh:
             json.dump(tab, fh, indent=1)
         write_leg_csv(tab, os.path.join(dst, f"{tag}_{p}_step_kernels.csv"))
+        with open(os.path.join(dst, f"{tag}_{p}_dispatches.csv"), "w", newline="") as fh:
+            w = csv.writer(fh)
+            keys = ["stage", "kernel", "geo", "us", "tflops", "read_mb", "write_mb", "algo_mb", "traffic_over_algo",
+                    "mfma_busy_pct"]
+            w.writerow(keys + ["lib_sha16"])
+            for d in tab["dispatches"]:
+                w.writerow([d[k] for k in keys] + [tab["lib_sha16"]])
         text.append(md(tab))
         print(md(tab))
     with open(os.path.join(dst, f"{tag}_pmc_traffic.json"), "w") as fh:

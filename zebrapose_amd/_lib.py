@@ -83,6 +83,7 @@ _SIGS = {
     "zp_conv2d_wgrad": (i32, [C.POINTER(WgradArgs), vp, vp]),
     "zp_bn_fold": (i32, [vp, vp, vp, vp, vp, f32, i32, vp, vp, vp]),
     "zp_bn_train_finalize": (i32, [vp, i32, i32, i64, f32, f32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+    "zp_bn_finalize_floats": (C.c_longlong, [i32, i32]),
     "zp_bn_apply": (i32, [vp, i32, i32, vp, vp, vp, i32, i32, i32, i32, vp, i32, i32, vp]),
     "zp_bn_bwd_parts": (i32, [i32, i32]),
     "zp_bn_bwd_reduce": (i32, [vp, i32, i32, vp, i32, i32, vp, i32, i32, vp, i32, i32, vp, vp, vp, i32, vp]),
@@ -145,7 +146,7 @@ def _load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.zp_abi_version() != 3:
+    if lib.zp_abi_version() != 4:
         raise ImportError("libzp.so ABI version mismatch")
     return lib
 

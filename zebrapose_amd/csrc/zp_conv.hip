@@ -3348,7 +3348,9 @@ extern "C" int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* st
  * default; -1 = ZP_CONV3W_ACC); key 14: its 256 x 128 pixel tile (0 off, 1 on; -1 = ZP_CONV3W_TP128);
  * key 15: zp_bn_train_finalize's statistics merge in one launch (1, default) or two (0; -1 = ZP_BN_FUSED);
  * key 16: k_conv3's multi-sub launches (the merged ASPP) with a tile's subs adjacent on one XCD (1) or
- * the sub slowest (0, default: measured faster; -1 = ZP_CONV3_SUBINT).
+ * the sub slowest (0, default: measured faster; -1 = ZP_CONV3_SUBINT); key 17: k_conv3w's multi-sub
+ * launches (the ConvT phases) with a pixel tile's phases adjacent on one XCD (1, default) or phase by
+ * phase, longest first (0; -1 = ZP_CONV3W_SUBINT).
  * Returns the previous value. */
 /* split-fp32 split-K workspace: bytes of f32 slices zp_conv2d uses for these args when a.stats
  * points to that many (0: the launch is not split) */
@@ -3399,6 +3401,7 @@ extern "C" int zp_conv_tuning(int key, int value) {
   if (key == 14) return conv3w_tp128_mode(value);
   if (key == 15) return bn_fused_mode(value);
   if (key == 16) return conv3_subint_mode(value);
+  if (key == 17) return conv3w_subint_mode(value);
   if (key == 4) {
     const int old = g_wgrad2_rounds;
     g_wgrad2_rounds = value > 0 ? value : 1;

@@ -23,5 +23,6 @@ int conv3w_splitk_mode(int v);                    // zp_conv_tuning key 12; retu
 int conv3w_tp(const zp_conv_args& a);            // pixel tile of the wide kernel (256, or 128)
 int conv3w_acc_mode(int v);                       // zp_conv_tuning key 13; returns the previous value
 int conv3w_tp128_mode(int v);                     // zp_conv_tuning key 14; returns the previous value
+int conv3w_subint_mode(int v);                    // zp_conv_tuning key 17; returns the previous value
 void conv3w_head_launch(const zp_conv_args& a, const conv_taps& tg, const zp_head_args& h, hipStream_t st, int flags);
 }  // namespace zp

@@ -94,21 +94,36 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
   __shared__ uint4 lds[LDSU * 64];
   static_assert(LDSU * 1024 <= 160 * 1024, "LDS");
   static_assert(((NPL - 1) * NT + NT - 1) * 1024 < 65536, "ds_read immediate range");
-  const int tb = (int)blockIdx.z / nsplit, kz = (int)blockIdx.z - tb * nsplit;
-  const zp_conv_sub& S = A.sub[tb];
+  int tb = (int)blockIdx.z / nsplit;
+  const int kz = (int)blockIdx.z - tb * nsplit;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wc = wid >> 2, wp = wid & 3;
   const int GHW = A.GH * A.GW;
   const int M = A.N * GHW;
   int bx = blockIdx.x, by = blockIdx.y;
-  if (flags & 2) {  // XCD-aware order (k_conv): consecutive pixel tiles (shared halo rows) on one XCD
-    const int total = gridDim.x * gridDim.y;
+  const int total = gridDim.x * gridDim.y;
+  if ((flags & 32768) && nsplit == 1 && A.nsub > 1 && (total & 7) == 0) {
+    // sub-interleaved order (round 6, conv3w_launch sets it for the ConvT phases): the subs of a
+    // pixel tile are dispatched back to back on one XCD (dispatch id % 8 picks the XCD), longest
+    // first, so the input strip all four phases read is fetched from HBM once and hit in that
+    // XCD's L2 by the others (phase-major order re-read the input once per phase: up2's ConvT read
+    // 721 MB for a 168 MB input, profiles/r06a_fp32_dispatches.csv); the phases' weights (2.9 MB in
+    // all for up2) stay L2-resident.  Consecutive pixel tiles (shared halo rows) stay on one XCD.
+    const int gid = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const int q = gid >> 3;
+    tb = q % A.nsub;
+    const int tile = (gid & 7) * (total >> 3) + q / A.nsub;
+    bx = tile / gridDim.y;
+    by = tile - bx * gridDim.y;
+  } else if (flags & 2) {  // XCD-aware order (k_conv): consecutive pixel tiles (shared halo rows) on one XCD
     const int bid = blockIdx.x + gridDim.x * blockIdx.y;
     const int lin = (total & 7) ? bid : (bid & 7) * (total >> 3) + (bid >> 3);
     bx = lin / gridDim.y;
     by = lin - bx * gridDim.y;
   }
+  tb = __builtin_amdgcn_readfirstlane(tb);
+  const zp_conv_sub& S = A.sub[tb];
   const int p0 = bx * TP, c0 = by * TC;
   const int CB = A.Cin / 32;
   const int ny = TG.ny[tb], nx = TG.nx[tb], dty = TG.dty[tb], dtx = TG.dtx[tb];
@@ -849,6 +864,19 @@ static bool conv3w_strip_ok(const zp_conv_args& a, const conv_taps& tg, int fl, 
   return nxmax >= 2;
 }
 
+// zp_conv_tuning key 17: the subs (ConvT phases) of a multi-sub launch interleaved per pixel tile on
+// one XCD (1, default) or dispatched phase by phase, longest first (0) (-1: ZP_CONV3W_SUBINT or 1)
+static int g_conv3w_subint = -1;
+int conv3w_subint_mode(int v) {
+  const int old = g_conv3w_subint;
+  g_conv3w_subint = v;
+  return old;
+}
+static bool conv3w_subint() {
+  static const int env = getenv("ZP_CONV3W_SUBINT") ? atoi(getenv("ZP_CONV3W_SUBINT")) : 1;
+  return (g_conv3w_subint >= 0 ? g_conv3w_subint : env) != 0;
+}
+
 void conv3w_launch(const zp_conv_args& a0, const conv_taps& tg0, hipStream_t st, int fl, float* ws, int ns) {
   // several sub-problems (the ConvT phases: 1 / 2 / 2 / 4 taps): dispatched longest first (the
   // dispatcher walks blockIdx.z slowest, so the 4-tap phase's workgroups start first and the
@@ -878,6 +906,7 @@ void conv3w_launch(const zp_conv_args& a0, const conv_taps& tg0, hipStream_t st,
   }
   const zp_head_args H{};
   const int acc = (fl & 536870912) ? ACC_FLUSH : conv3w_acc();  // (flag 536870912: the flushed form, as in round 4)
+  if (a.nsub > 1 && ns == 1 && conv3w_subint()) fl |= 32768;  // the phases of a pixel tile adjacent on one XCD
   const bool str = conv3w_strip_ok(a, tg, fl, ns);
   if (ns == 1 && conv3w_tp(a) == 128) {  // the 256 x 128 tile (zp_conv_tuning key 14)
     const dim3 g128((unsigned)(((long)a.N * a.GH * a.GW + 127) / 128), (unsigned)(a.Cout / 256), (unsigned)a.nsub);

@@ -520,10 +520,10 @@ __global__ void __launch_bounds__(1024) k_bn_stat_merge1(const float* __restrict
   if (c == 0 && f.nbt) f.nbt[0] += 1;
 }
 
-// the fused merge's per-device counters (one per channel group, zero between launches: each launch's
-// last block re-arms its own); allocated and zeroed on first use outside a stream capture
-static unsigned* g_bn_cnt[64];
-static constexpr int BN_CNT = 1024;
+// the fused merge's hand-off counters (one per channel group) live in the caller's partials buffer,
+// past the [3][parts][C] statistics (ABI 4, zp_bn_finalize_floats), and are zeroed on the launch's
+// stream before the merge: every launch has its own, whatever stream or hipGraph it runs in (ADVICE
+// r5: one static array per device was shared by concurrent launches on different streams)
 static int g_bn_fused = -1;  // zp_conv_tuning key 15: 1 the one-launch merge, 0 two launches (-1: ZP_BN_FUSED or 1)
 int bn_fused_mode(int v) {
   const int old = g_bn_fused;
@@ -1601,6 +1601,10 @@ extern "C" int zp_split_range_flag(unsigned int* flag) {
 }
 
 extern "C" int zp_abi_version(void) { return ZP_ABI_VERSION; }
+extern "C" long long zp_bn_finalize_floats(int parts, int C) {
+  if (parts <= 0 || C <= 0) return 0;
+  return 3LL * parts * C + (C + 31) / 32;  // statistics + the one-launch merge's counters (ABI 4)
+}
 extern "C" const char* zp_last_error(void) { return g_err; }
 extern "C" int zp_conv_rows_pad(int Cout) {
   int tc = Cout > 64 ? 128 : (Cout > 32 ? 64 : 32);
@@ -1682,19 +1686,12 @@ extern "C" int zp_bn_train_finalize(float* partials, int parts, int C, long long
     const int groups = (C + 31) / 32;
     static const int env = getenv("ZP_BN_FUSED") ? atoi(getenv("ZP_BN_FUSED")) : 1;
     const bool fused_on = (g_bn_fused >= 0 ? g_bn_fused : env) != 0;
-    int dev = -1;
-    unsigned* cnt = nullptr;
-    if (fused_on && groups <= BN_CNT && hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
-      cnt = g_bn_cnt[dev];
-      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-      if (!cnt && hipStreamIsCapturing(st, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
-        unsigned* p = nullptr;
-        if (hipMalloc((void**)&p, BN_CNT * sizeof(unsigned)) == hipSuccess &&
-            hipMemset(p, 0, BN_CNT * sizeof(unsigned)) == hipSuccess)
-          cnt = g_bn_cnt[dev] = p;
+    if (fused_on) {
+      unsigned* cnt = (unsigned*)(partials + (size_t)3 * parts * C);
+      if (hipMemsetAsync(cnt, 0, (size_t)groups * sizeof(unsigned), st) != hipSuccess) {
+        set_error("zp_bn_train_finalize: counter reset failed");
+        return ZP_ERR_HIP;
       }
-    }
-    if (cnt) {
       hipLaunchKernelGGL(k_bn_stat_merge_fin, dim3(groups, (parts + BN_MERGE_R - 1) / BN_MERGE_R), dim3(256), 0, st,
                          partials, parts, C, cnt, f);
       ZP_LAUNCH_CHECK("zp_bn_train_finalize (fused merge)");

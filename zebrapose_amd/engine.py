@@ -334,7 +334,7 @@ class Engine:
             a.bnr_x, a.bnr_save, a.bnr_part = raw.data_ptr(), save.data_ptr(), stats.data_ptr()
         elif stats == "alloc":
             parts = L.lib.zp_conv2d_stat_parts(C.byref(a))
-            stats = torch.empty(3 * parts * cout, dtype=torch.float32, device=x.buf.device)
+            stats = torch.empty(L.lib.zp_bn_finalize_floats(parts, cout), dtype=torch.float32, device=x.buf.device)
         if bnr is not None:
             pass
         elif stats is not None:
@@ -444,9 +444,7 @@ class Engine:
             assert not train, "the split engine runs eval forwards only"
             cr = unit.conv.weight.shape[1]
             kp = G.ceil_to(unit.k * unit.k * cr, 32)
-            if (self.dt == L.ZP_F32H2 and self.stem_direct and (unit.k, unit.s, unit.p, cr, unit.cout) == (7, 2, 3, 3, 64)
-                    and OW <= 128 and 256 % OW == 0 and (OH * OW) % 256 == 0 and out.ld % 8 == 0 and out.c0 % 8 == 0
-                    and x.ld % 4 == 0):
+            if self._stem_direct_ok(unit, OH, OW, out.ld, out.c0, x.ld):
                 # one launch from the f32 image (zp_stem_split): no patch tensor
                 taps = [(ky, kx) for ky in range(unit.k) for kx in range(unit.k)]
                 rows = G.ceil_to(unit.cout, 128)
@@ -462,6 +460,8 @@ class Engine:
                 if self.trace is not None:
                     self.trace.append(("conv", unit, x, out, res))
                 return
+            if isinstance(x, NchwInput):
+                raise AssertionError("the NCHW stem input reached the im2col stem (nchw_stem / unit_fwd disagree)")
             col = Act(self._empty((x.B, OH, OW, kp), x.buf.device))
             L.call("zp_im2col_split", x.ptr, x.B, x.H, x.W, x.ld, cr, unit.k, unit.s, unit.p, OH, OW, kp, self.dt,
                    col.ptr, L.stream_ptr())
@@ -475,6 +475,8 @@ class Engine:
             if self.trace is not None:
                 self.trace.append(("conv", unit, x, out, res))
             return
+        if isinstance(x, NchwInput):
+            raise AssertionError("the NCHW stem input reaches zp_stem_split only (nchw_stem / unit_fwd disagree)")
         if self.x3 and unit.cin < _KE[self.dt]:
             # the split-mode stem: its 3 (-> 8) input channels are below k_conv3's 32-channel K step;
             # it runs the exact-f32 small-Cin kernel on the f32 NHWC input and writes split output
@@ -559,11 +561,25 @@ class Engine:
         elif self.trace is not None:
             self.trace.append(("head", unit, x, (mask, code), None))
 
-    def nchw_stem(self, B, H, W, tape):
+    def _stem_direct_ok(self, unit, OH, OW, out_ld, out_c0, x_ld):
+        """The one-launch two-plane stem (zp_stem_split) takes this 7x7 / s2 conv: split stem on,
+        output width <= 128 dividing 256, whole 256-pixel tiles, 16-byte output rows and input rows
+        of 4 floats (x_ld 0: the NCHW input itself)."""
+        cr = unit.conv.weight.shape[1]
+        return (self.x3 and self.split_stem and self.dt == L.ZP_F32H2 and self.stem_direct
+                and unit.cin < _KE[self.dt] and unit.d == 1
+                and (unit.k, unit.s, unit.p, cr, unit.cout) == (7, 2, 3, 3, 64)
+                and OW <= 128 and 256 % OW == 0 and (OH * OW) % 256 == 0 and out_ld % 8 == 0 and out_c0 % 8 == 0
+                and x_ld % 4 == 0)
+
+    def nchw_stem(self, stem_unit, H, W, tape):
         """True when the two-plane stem (zp_stem_split) reads the f32 NCHW input directly: eval, no
-        trace (the teacher-forced replays start from the NHWC copy), output width <= 128."""
-        return (self.dt == L.ZP_F32H2 and self.stem_direct and tape is None and self.trace is None
-                and W // 2 <= 128 and 256 % (W // 2) == 0 and ((H // 2) * (W // 2)) % 256 == 0)
+        trace (the teacher-forced replays start from the NHWC copy), and the stem unit takes
+        unit_fwd's zp_stem_split branch (same predicate) on the 64-channel x_128 output."""
+        if tape is not None or self.trace is not None:
+            return False
+        OH, OW = stem_unit.out_hw(H, W)
+        return (OH, OW) == (H // 2, W // 2) and self._stem_direct_ok(stem_unit, OH, OW, 64, 0, 0)
 
     def head_fusable(self, B, H, W):
         """True when up2's last conv (3x3, 256 -> 256) and the 1x1 head run fused (zp_conv2d_head):
@@ -672,7 +688,10 @@ class Engine:
             flops = 2.0 * x.B * plan.GH * plan.GW * sum(len(sb.taps) for sb in plan.subs) * x.C * unit.cout
             geo = (f"wgrad:{x.C}->{unit.cout} taps{max(len(sb.taps) for sb in plan.subs)} "
                    f"{x.H}x{x.W}->{plan.GH}x{plan.GW}x{a.nsub}")
-            self.timing.append((geo, e0, e1, flops, "k_wgrad+reduce", 0))
+            # algorithmic bytes: x and dy read once (16-bit), dw written once (f32)
+            esz = x.buf.element_size()
+            nbytes = (x.P * x.C + dy.P * unit.cout) * esz + dw.numel() * 4
+            self.timing.append((geo, e0, e1, flops, "k_wgrad+reduce", nbytes))
             return
         L.check(L.lib.zp_conv2d_wgrad(C.byref(a), ws.data_ptr(), L.stream_ptr()), "zp_conv2d_wgrad")
 
@@ -726,6 +745,13 @@ class Engine:
         st = L.stream_ptr()
         plan = unit.fwd_plan(x.H, x.W)
         pending = {}  # this unit's gradients, handed over with the weight gradient
+        # where a gradient is written: the parameter's bucket slice when the sink offers one
+        # (parallel.GradBuckets.dest, gradient as bucket view), else a fresh tensor
+        sink_dest = getattr(grads, "dest", None)
+
+        def dest(p):
+            v = sink_dest(p) if sink_dest is not None else None
+            return torch.empty_like(p) if v is None else v
         tr = None if self.bwd_trace is None else {"kind": kind, "unit": unit, "x": x, "out": out, "res": res,
                                                    "raw": raw, "save": save}
         if kind == "head":
@@ -737,8 +763,8 @@ class Engine:
                 parts = L.lib.zp_bn_bwd_parts(P, unit.cout)
                 if out.buf.data_ptr() not in gmap.get("__bnr__", {}):
                     partials = torch.empty(2 * (parts + 1) * unit.cout, dtype=torch.float32, device=dev)
-                dgamma = torch.empty_like(bn.weight)
-                dbeta = torch.empty_like(bn.bias)
+                dgamma = dest(bn.weight)
+                dbeta = dest(bn.bias)
                 # ReLU without a residual: the mask is recomputed from raw (mode 2), out is not read
                 rm = (2 if res is None and self.bn_mask_from_raw else 1) if unit.relu else 0
                 fused = gmap.get("__bnr__", {}).pop(out.buf.data_ptr(), None)
@@ -765,7 +791,7 @@ class Engine:
                               gres=None if gres is None else (gres_before, self._snap(gres)))
                 if conv.bias is not None:
                     # train-mode BN removes the per-channel mean: d loss / d conv bias == 0 exactly
-                    pending[conv.bias] = torch.zeros_like(conv.bias)
+                    pending[conv.bias] = dest(conv.bias).zero_()
                 gy = Act(graw)
             else:
                 raise NotImplementedError("eval-mode backward")
@@ -781,9 +807,10 @@ class Engine:
         wdy = Act(gy.buf, 0, unit.cout) if kind == "head" else gy
         side = self._side_stream(dev)
         if side is None:
-            dw = torch.empty_like(conv.weight)
+            dw = dest(conv.weight)
             self._wgrad(unit, x, plan, wdy, dw)
-            grads.update(pending)
+            for k, v in pending.items():  # (item by item: dict.update would bypass _ReadyDict's reporting)
+                grads[k] = v
             grads[conv.weight] = dw
         else:
             # the side stream starts after everything enqueued so far (gy, dgamma / dbeta, the head
@@ -793,8 +820,8 @@ class Engine:
             # dw is allocated on the main stream, which consumes and frees it (Adam, zero_grad):
             # the block belongs to that stream's pool, and record_stream keeps it from being
             # reused there before the side stream's wgrad has written it
-            dw = torch.empty_like(conv.weight)
-            dw.record_stream(side)
+            dw = dest(conv.weight)
+            dw.record_stream(side)  # (a bucket slice: its storage is never freed; harmless)
             with torch.cuda.stream(side):
                 self._wgrad(unit, x, plan, wdy, dw)
                 for k, v in pending.items():
@@ -908,7 +935,9 @@ class Engine:
         self._prepack(dev)
         st = L.stream_ptr()
         self.stage = "stem"
-        if self.nchw_stem(B, H, W, tape):  # zp_stem_split reads the NCHW input itself (ldx 0)
+        r = rn.resnet
+        stem_unit = self._u(r[0], r[1], True, cin_act=8)
+        if self.nchw_stem(stem_unit, H, W, tape):  # zp_stem_split reads the NCHW input itself (ldx 0)
             xin = NchwInput(x.permute(0, 2, 3, 1), 0, 8)
         elif self.x3:  # the stem reads f32 (exact-f32 small-Cin kernel) and writes split output
             xin = Act(torch.empty((B, H, W, 8), dtype=torch.float32, device=dev))
@@ -929,7 +958,7 @@ class Engine:
         else:
             head_in = self._empty((B, H2, W2, 320), dev)
             x128 = Act(head_in, 256, 64)
-        self.unit_fwd(self._u(r[0], r[1], True, cin_act=8), xin, x128, tape, label="stem")
+        self.unit_fwd(stem_unit, xin, x128, tape, label="stem")
         self.stage = "layer1"
         pooled = new(H4, W4, 64)
         L.call("zp_maxpool3s2", x128.ptr, B, H2, W2, x128.ld, x128.c0, 64, self.dt, pooled.ptr, H4, W4, 64, 0, st)

@@ -61,6 +61,7 @@ class FusedAdam(torch.optim.Optimizer):
         plans = self.__dict__.setdefault("_plans", {})
         ps = group["params"]
         plan = plans.get(gi)
+        # (valid while every step of the group went through the fast path: the general path drops it)
         if plan is not None and plan[0] == len(ps) and all(a is b for a, b in zip(plan[1], ps)):
             return plan
         if not ps or any(len(self.state[p]) == 0 or p not in steps for p in ps):
@@ -111,6 +112,9 @@ class FusedAdam(torch.optim.Optimizer):
                     torch.autograd.graph.increment_version(list(ps))
                     continue
             self._sync_steps()
+            # the general path may advance only part of the group (a parameter without a gradient):
+            # the cached plan assumed one shared step count, so it is rebuilt once they agree again
+            self.__dict__.setdefault("_plans", {}).pop(gi, None)
             live, step_t = [], []
             for p in group["params"]:
                 if p.grad is None:

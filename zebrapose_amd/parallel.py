@@ -74,12 +74,21 @@ class GradBuckets:
 
     torch's DDP sees the network as one autograd node that returns all 152 gradients at once, so
     its buckets could only all-reduce after the whole backward.  Here the engine reports each
-    gradient as it is enqueued (``ready``); the gradient is copied into its bucket's flat f32
-    buffer, and when a bucket is complete it is divided by the world size and all-reduced (SUM)
-    with ``async_op=True``.  The collective is ordered after the kernels enqueued so far on the
-    current stream and runs on the process group's own stream (RCCL over xGMI for 'nccl') while
-    the rest of the backward is computed.  ``finish`` makes the current stream wait for every
-    bucket and returns the averaged gradients.
+    gradient as it is enqueued (``ready``), and when a bucket is complete it is all-reduced with
+    ``async_op=True``.  The collective is ordered after the kernels enqueued so far on the current
+    stream and runs on the process group's own stream (RCCL over xGMI for 'nccl') while the rest of
+    the backward is computed.  ``finish`` makes the current stream wait for every bucket and returns
+    the averaged gradients.
+
+    Gradient as bucket view (round 6; DDP's ``gradient_as_bucket_view=True``): the engine asks
+    ``dest(p)`` for the parameter's slice of its bucket's flat buffer and writes the gradient there
+    (weight gradients by zp_conv2d_wgrad's split reduce, dgamma / dbeta by the BN backward), so no
+    per-gradient copy is made; a gradient produced elsewhere is still copied in.  The mean over
+    ranks is RCCL's ncclAvg (``ReduceOp.AVG``: each input pre-multiplied by 1 / world inside the
+    collective, exact for world sizes that are powers of two), so no separate division pass runs;
+    backends without AVG (gloo) divide the bucket first, as DDP does; at world size 1 the mean is
+    the gradient itself.  ``finish`` returns fresh views of the buckets, which autograd's
+    AccumulateGrad adopts as ``p.grad`` without cloning them.
 
     DDP semantics kept: parameters broadcast from rank 0 at construction, module buffers (BN
     running statistics) broadcast from rank 0 before every forward (broadcast_buffers=True),
@@ -97,6 +106,7 @@ class GradBuckets:
             states = [t for t in list(module.parameters()) + list(module.buffers())]
             if states:
                 dist._broadcast_coalesced(self._pg(), states, 250 * 1024 * 1024, 0)
+        self._flatten_buffers()
         cap = int(bucket_mb * 1024 * 1024)
         self.buckets = []  # [flat, [params], pending count, work]
         self.slot = {}  # param -> (bucket index, view)
@@ -112,6 +122,7 @@ class GradBuckets:
         # optional per-step timeline (bench.py's DDP leg): (bucket, event recorded on the current
         # stream when the bucket's all-reduce is enqueued); finish() appends ("done", event)
         self.timing = None
+        self._avg = None  # the backend's ReduceOp.AVG in use (decided at the first launch)
         self._reset()
 
     def describe(self, names=None):
@@ -127,11 +138,11 @@ class GradBuckets:
         dt, dev = ps[0].dtype, ps[0].device
         if any(p.dtype != dt or p.device != dev for p in ps):
             raise ValueError("GradBuckets: one dtype / device per bucket")
-        flat = torch.empty(sum(p.numel() for p in ps), dtype=dt, device=dev)
+        flat = torch.zeros(sum(p.numel() for p in ps), dtype=dt, device=dev)
         b = len(self.buckets)
         off = 0
         for p in ps:
-            self.slot[p] = (b, flat[off:off + p.numel()].view_as(p))
+            self.slot[p] = (b, flat[off:off + p.numel()].view_as(p), off)
             off += p.numel()
         self.buckets.append([flat, ps, 0, None])
 
@@ -141,12 +152,42 @@ class GradBuckets:
             bk[3] = None
         self.seen = set()
 
+    def _flatten_buffers(self):
+        """The module's buffers (BN running mean / var, num_batches_tracked) become views of one flat
+        tensor per (dtype, device), so that the per-forward broadcast is one collective per flat
+        tensor in place -- _broadcast_coalesced flattened ~150 buffers into a scratch tensor and copied
+        each back: ~0.6 ms of copy launches per step (BENCH r06 train.rccl_world1)."""
+        groups, seen = {}, {}
+        for m in self.module.modules():
+            for name, b in m._buffers.items():
+                if b is None:
+                    continue
+                groups.setdefault((b.dtype, b.device), []).append((m, name, b))
+        self._buf_flats = []
+        with torch.no_grad():
+            for (dt, dev), items in groups.items():
+                uniq = [b for b in {id(b): b for _, _, b in items}.values()]
+                flat = torch.empty(sum(b.numel() for b in uniq), dtype=dt, device=dev)
+                off = 0
+                for b in uniq:
+                    v = flat[off:off + b.numel()].view_as(b)
+                    v.copy_(b)
+                    seen[id(b)] = v
+                    off += b.numel()
+                for m, name, b in items:
+                    m._buffers[name] = seen[id(b)]
+                self._buf_flats.append(flat)
+
     def sync_buffers(self):
-        """DDP broadcast_buffers=True: rank 0's BN running statistics before every forward."""
-        bufs = list(self.module.buffers())
-        if bufs:
-            with torch.no_grad():
-                dist._broadcast_coalesced(self._pg(), bufs, 250 * 1024 * 1024, 0)
+        """DDP broadcast_buffers=True: rank 0's BN running statistics before every forward (one
+        in-place broadcast per flat buffer tensor; their version counters are bumped, as the copy
+        back of a coalesced broadcast did, so version-keyed caches -- the eval BN folds -- refresh)."""
+        if not self._buf_flats:
+            return
+        with torch.no_grad():
+            for f in self._buf_flats:
+                dist.broadcast(f, 0, group=self.group)
+        torch.autograd.graph.increment_version(self._buf_flats)
 
     def _launch(self, b):
         bk = self.buckets[b]
@@ -154,19 +195,33 @@ class GradBuckets:
             ev = torch.cuda.Event(enable_timing=True)
             ev.record()
             self.timing.append((b, ev))
-        bk[0].div_(self.world)
-        bk[3] = dist.all_reduce(bk[0], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        op = dist.ReduceOp.SUM
+        if self.world > 1:
+            if self._avg is None:
+                self._avg = dist.get_backend(self._pg()) == "nccl" and hasattr(dist.ReduceOp, "AVG")
+            if self._avg:
+                op = dist.ReduceOp.AVG
+            else:
+                bk[0].div_(self.world)
+        bk[3] = dist.all_reduce(bk[0], op=op, group=self.group, async_op=True)
+
+    def dest(self, p):
+        """The slice of p's bucket the engine writes p's gradient into (None: p is not bucketed)."""
+        s = self.slot.get(p)
+        return None if s is None else s[1]
 
     def ready(self, p, g):
-        """Gradient g of parameter p has been enqueued on the current stream."""
+        """Gradient g of parameter p has been enqueued on the current stream (written into dest(p),
+        or anywhere else: then copied in)."""
         s = self.slot.get(p)
         if s is None:
             return
         if p in self.seen:
             raise RuntimeError("GradBuckets: a parameter received two gradients in one backward")
         self.seen.add(p)
-        b, view = s
-        view.copy_(g)
+        b, view = s[0], s[1]
+        if g.data_ptr() != view.data_ptr():
+            view.copy_(g)
         self.buckets[b][2] -= 1
         if self.buckets[b][2] == 0:
             self._launch(b)
@@ -186,17 +241,21 @@ class GradBuckets:
             ev = torch.cuda.Event(enable_timing=True)
             ev.record()  # the current stream has waited for every bucket
             self.timing.append(("done", ev))
-        out = {p: self.slot[p][1] for p in self.params}
+        # fresh views (the slot's own view stays referenced here, so autograd would clone it)
+        out = {p: self.buckets[self.slot[p][0]][0][self.slot[p][2]:self.slot[p][2] + p.numel()].view_as(p)
+               for p in self.params}
         self._reset()
         return out
 
 
 class _ReadyDict(dict):
-    """The engine's {parameter: gradient} map; each assignment reports to GradBuckets.ready."""
+    """The engine's {parameter: gradient} map; each assignment reports to GradBuckets.ready.
+    ``dest(p)``: where the engine may write p's gradient (its bucket slice)."""
 
     def __init__(self, reducer):
         super().__init__()
         self._reducer = reducer
+        self.dest = reducer.dest
 
     def __setitem__(self, k, v):
         super().__setitem__(k, v)
