@@ -144,8 +144,8 @@ def test_configs4_r50_fp16_teacher_forced(gpu, golden):
     256x256; the dispatch the multi-object bench runs: strip, four-phase, merged-ASPP tiles at the
     1024 / 2048-channel widths) replayed on the host from the device's own stored fp16 inputs with the
     device's roundings (oracle/ref_cpu.py lp_conv, as tests/test_gpu_bench_geometry.py does for bf16
-    R34): stored outputs within 1 fp16 ulp (+ 2^-15 of the layer's rms for outputs that cancel to ~0),
-    at most 1% of any layer's elements not bit-identical, the f32 head within 2e-5 of its scale.
+    R34): stored outputs within 1 fp16 ulp (+ 2^-12 of the layer's rms for outputs that cancel to ~0),
+    at most 1% of any layer's elements (or 8 of a layer of a few hundred) not bit-identical, the f32 head within 2e-5 of its scale.
     Reference: model/resnet.py:206-227, model/aspp.py:117-225, test_vivo.py:99-114."""
     from oracle import ref_cpu
     from tests.test_gpu_bench_geometry import _label, replay
@@ -184,13 +184,16 @@ def test_configs4_r50_fp16_teacher_forced(gpu, golden):
                 continue
             rms = float(exp.pow(2).mean().sqrt())
             ulp = _ulp_f16(torch.maximum(exp.abs(), got.abs()))
-            bad = d > ulp + 2.0 ** -15 * rms
+            # (the absolute term is the f32 accumulation's, as in the bf16 test: 2^-12 of the layer rms
+            # -- the K = 2048 sums of R50's widths cancel; the storage format does not shrink it)
+            bad = d > ulp + 2.0 ** -12 * rms
             frac = float((d > 0).float().mean())
             worst_frac = max(worst_frac, frac)
             worst_ulp = max(worst_ulp, float((d / ulp).max()))
             assert not bool(bad.any()), (f"crop {b} {_label(rec, i)}: {int(bad.sum())} elements beyond 1 ulp, "
                                          f"max |d| {float(d.max()):.3g} rms {rms:.3g}")
-            assert frac <= 0.01, (f"crop {b} {_label(rec, i)}", frac)
+            # (the ASPP image pool's 1x1 conv has 256 outputs per crop: a count bound there)
+            assert frac <= 0.01 or int((d > 0).sum()) <= 8, (f"crop {b} {_label(rec, i)}", frac)
     print(f"R50 fp16 teacher-forced: {len(trace)} ops ({nconv} convs) x 2 crops; worst not-bit-identical "
           f"fraction {worst_frac:.4f}, worst |d| {worst_ulp:.2f} ulp")
     del net

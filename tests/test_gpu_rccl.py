@@ -61,13 +61,21 @@ def _worker(port, mode, q):
         ts0(x, gt, gm, *extra)
         local = {n: p.grad.detach().clone() for n, p in net.named_parameters()}
         # count the BN-buffer broadcasts (DDP broadcast_buffers=True: one per forward)
-        calls = {"bcast": 0}
+        # (round 6: GradBuckets broadcasts its flat buffer tensors in place, one dist.broadcast each;
+        # torch's DDP uses _broadcast_coalesced)
+        calls = {"bcast": 0, "bcast_flat": 0}
         orig = dist._broadcast_coalesced
+        orig_b = dist.broadcast
 
         def counting(*a, **k):
             calls["bcast"] += 1
             return orig(*a, **k)
+
+        def counting_b(*a, **k):
+            calls["bcast_flat"] += 1
+            return orig_b(*a, **k)
         dist._broadcast_coalesced = counting
+        dist.broadcast = counting_b
         ts = TrainStep(net, ddp=True, learning_rate=0.0, device=0)
         ts.optimizer.step = lambda: None
         works = []
@@ -92,15 +100,21 @@ def _worker(port, mode, q):
                 seen.setdefault(n, getattr(eng, "bwd_progress", (0, 1)))
             return hook
         hooks = [p.register_post_accumulate_grad_hook(hook_for(n)) for n, p in net.named_parameters()]
-        bc0 = calls["bcast"]
+        bc0, bf0 = calls["bcast"], calls["bcast_flat"]
         ts(x, gt, gm, *extra)
         torch.cuda.synchronize()
         for h in hooks:
             h.remove()
         diffs = {n: int((p.grad != local[n]).sum().item()) for n, p in net.named_parameters()}
-        res = {"mode": mode, "diffs": diffs, "bcast": calls["bcast"] - bc0, "nparams": len(local),
+        res = {"mode": mode, "diffs": diffs, "bcast": calls["bcast"] - bc0, "bcast_flat": calls["bcast_flat"] - bf0,
+               "nparams": len(local),
                "hook_progress": {n: list(v) for n, v in seen.items()}}
         if mode == "buckets":
+            res["nflats"] = len(ts.buckets._buf_flats)
+            # every BN buffer is a view of one of those flat tensors
+            res["buf_outside"] = [n for n, b in net.named_buffers()
+                                  if not any(f.data_ptr() <= b.data_ptr() < f.data_ptr() + f.numel() * f.element_size()
+                                             for f in ts.buckets._buf_flats)]
             # gradient as bucket view (round 6): every p.grad lies inside its bucket's flat buffer --
             # written there by the engine, adopted by AccumulateGrad without a clone
             spans = [(bk[0].data_ptr(), bk[0].data_ptr() + bk[0].numel() * bk[0].element_size())
@@ -168,6 +182,9 @@ def test_rccl_world1_grad_exchange(gpu, mode):
         assert res["nbuckets"] >= 4  # 116 MB of f32 gradients in ~25 MB buckets
         assert res["launched"] == res["nbuckets"] == res["completed"]
         assert res["done_event"] == 1
-        assert res["bcast"] == 1  # rank 0's BN buffers broadcast before the forward
+        # rank 0's BN buffers broadcast before the forward: one in-place broadcast per flat buffer
+        # tensor (f32 running stats, int64 num_batches_tracked), no coalescing copies
+        assert res["bcast"] == 0 and res["bcast_flat"] == res["nflats"] == 2, res
+        assert not res["buf_outside"], res["buf_outside"]
         assert res["allreduce_identity"]
         assert not res["outside_bucket"], res["outside_bucket"]

@@ -77,7 +77,7 @@ def test_stem_knobs_keep_fp32_eval_working(gpu, golden, knob):
     x = torch.from_numpy(f["fwd64_x"]).cuda()
     with torch.no_grad():
         m0, c0 = (t.clone() for t in net(x))
-        eng = net.eval_engine()
+        eng = net.net.eval_engine()
         assert eng.dt == L.ZP_F32H2
         setattr(eng, knob, False)
         m1, c1 = net(x)

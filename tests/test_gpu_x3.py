@@ -454,7 +454,9 @@ def test_wide_accumulation_forms(gpu, geom):
       1 = round 4's one scaled accumulator: every correction product is added by the MFMA into the
           large running sum, whose alignment truncates its low bits -- a systematic negative bias;
       2 = per-step partial sums from zero added by v_add_f32: smaller rms, but the corrections are
-          still truncated against the step's main partial.
+          still truncated against the step's main partial;
+      4 = (round 6) a persistent correction accumulator per block for the whole K loop, joined to the
+          main sum by one rounding FMA after it (the 256 x 128 tile).
     The default's mean signed error (relative to the mean |output|) must be within 3x the exact-f32
     MFMA kernel's (+ a 2^-27 floor) and under a tenth of the one-accumulator form's, its rms within
     the two-plane bound of the f32 kernel's."""
@@ -490,24 +492,30 @@ def test_wide_accumulation_forms(gpu, geom):
     eng = Engine(torch.nn.Module(), torch.float32, split="h2")
     old_min, old_acc, old_sk = L.lib.zp_conv_tuning(11, 1), L.lib.zp_conv_tuning(13, -1), L.lib.zp_conv_tuning(12, 0)
     try:
-        for acc in (-1, 0, 1, 2):
+        for acc in (-1, 0, 1, 2, 4):
             L.lib.zp_conv_tuning(13, acc)
             oa = Act(eng._empty((B, H, H, cout), gpu))
             eng.stage_log = []
             eng.unit_fwd(unit, xa, oa, None)
             torch.cuda.synchronize()
-            assert [r[1] for r in eng.stage_log] == ["k_conv3w<h2>"]
+            want = "k_conv3w<h2,TP=128>" if acc == 4 else "k_conv3w<h2>"
+            assert [r[1] for r in eng.stage_log] == [want], eng.stage_log
             stat[acc] = stats(oa)
     finally:
         L.lib.zp_conv_tuning(11, old_min)
         L.lib.zp_conv_tuning(13, old_acc)
         L.lib.zp_conv_tuning(12, old_sk)
     print(f"{geom}: (bias, rms) relative -- f32 MFMA {stat['f32']}, flushed {stat[0]}, one accumulator {stat[1]}, "
-          f"per-step partial {stat[2]}")
-    assert stat[-1] == stat[0]  # the default is the flushed form
-    assert abs(stat[0][0]) <= 3.0 * abs(stat["f32"][0]) + 2.0 ** -27, stat
-    assert abs(stat[0][0]) <= abs(stat[1][0]) / 10.0, stat
-    assert stat[0][1] <= BOUND["h2"][0] * stat["f32"][1], stat
+          f"per-step partial {stat[2]}, persistent correction accumulator {stat[4]}")
+    dflt = L.lib.zp_conv_tuning(13, -1)
+    L.lib.zp_conv_tuning(13, dflt)
+    # the default (-1) is one of the unbiased forms: the flushed one (0) or, since round 6, the
+    # persistent correction accumulator on the 256 x 128 tile (4)
+    assert stat[-1] in (stat[0], stat[4])
+    for form in (0, 4):  # both unbiased: the corrections are never added into the 2^11-larger main sum
+        assert abs(stat[form][0]) <= 3.0 * abs(stat["f32"][0]) + 2.0 ** -27, (form, stat)
+        assert abs(stat[form][0]) <= abs(stat[1][0]) / 10.0, (form, stat)
+        assert stat[form][1] <= BOUND["h2"][0] * stat["f32"][1], (form, stat)
 
 
 # schedule flags of the two-plane kernels that must not change a single stored bit (zp_conv_tuning
@@ -557,11 +565,11 @@ def test_schedule_flags_are_bit_identical(gpu, geom, B, kernel, tp128):
     outs = {}
     old14 = L.lib.zp_conv_tuning(14, tp128)
     try:
-        # (round 6) "subint0": zp_conv_tuning key 17 = 0, the ConvT phases dispatched phase by phase
-        # instead of interleaved per pixel tile on one XCD (the default)
-        for extra in [0] + _BITWISE_FLAGS + ["subint0"]:
-            old = L.lib.zp_conv_tuning(1, 478 + (0 if extra == "subint0" else extra))
-            old17 = L.lib.zp_conv_tuning(17, 0 if extra == "subint0" else -1)
+        # (round 6) "subint1": zp_conv_tuning key 17 = 1, the ConvT phases interleaved per pixel tile on
+        # one XCD instead of dispatched phase by phase (the default)
+        for extra in [0] + _BITWISE_FLAGS + ["subint1"]:
+            old = L.lib.zp_conv_tuning(1, 478 + (0 if extra == "subint1" else extra))
+            old17 = L.lib.zp_conv_tuning(17, 1 if extra == "subint1" else -1)
             try:
                 oa = Act(eng._empty((B, OH, OW, cout), gpu))
                 eng.stage_log = []
@@ -576,5 +584,5 @@ def test_schedule_flags_are_bit_identical(gpu, geom, B, kernel, tp128):
     names = [r[1] for r in eng.stage_log]
     print(geom, names)
     assert names == [kernel], names
-    for extra in _BITWISE_FLAGS + ["subint0"]:
+    for extra in _BITWISE_FLAGS + ["subint1"]:
         assert torch.equal(outs[extra], outs[0]), (geom, extra)

@@ -42,7 +42,7 @@ def bench_label(name):
     m = re.search(r"k_conv3s<(\d+), (\d+)(?:, \d+)*>", name)
     if m:
         return f"k_conv3s<{sp[m.group(1)]},WC={m.group(2)}>"
-    m = re.search(r"k_conv1x1n<(unsigned short|_Float16)>", name)
+    m = re.search(r"k_conv1x1n<(unsigned short|_Float16)(?:, \d+)?>", name)
     if m:  # the narrow-K 1x1 (round 5)
         return f"k_conv1x1n<{tn[m.group(1)]}>"
     if "k_stem_h2" in name:  # the direct two-plane stem (zp_stem_split)

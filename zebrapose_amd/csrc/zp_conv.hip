@@ -3282,7 +3282,7 @@ extern "C" int zp_conv2d_head_ok(const zp_conv_args* a) {
   if (!a) return 0;
   if (a->dtype == ZP_BF16 || a->dtype == ZP_F16) return head16_ok(*a);
   return a->dtype == ZP_F32H2 && a->nsub == 1 && a->Cout == 256 && a->out_mode == ZP_OUT_NHWC &&
-         conv3_tc(*a) == 256 && conv3w_tp(*a) == 256 && conv3w_splitk(*a) == 1;
+         conv3_tc(*a) == 256 && conv3w_tp_head(*a) == 256 && conv3w_splitk(*a) == 1;
 }
 
 extern "C" long long zp_conv2d_head_ws(const zp_conv_args* a) {
@@ -3349,8 +3349,8 @@ extern "C" int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* st
  * key 15: zp_bn_train_finalize's statistics merge in one launch (1, default) or two (0; -1 = ZP_BN_FUSED);
  * key 16: k_conv3's multi-sub launches (the merged ASPP) with a tile's subs adjacent on one XCD (1) or
  * the sub slowest (0, default: measured faster; -1 = ZP_CONV3_SUBINT); key 17: k_conv3w's multi-sub
- * launches (the ConvT phases) with a pixel tile's phases adjacent on one XCD (1, default) or phase by
- * phase, longest first (0; -1 = ZP_CONV3W_SUBINT).
+ * launches (the ConvT phases) with a pixel tile's phases adjacent on one XCD (1) or phase by phase,
+ * longest first (0, default: measured faster; -1 = ZP_CONV3W_SUBINT).
  * Returns the previous value. */
 /* split-fp32 split-K workspace: bytes of f32 slices zp_conv2d uses for these args when a.stats
  * points to that many (0: the launch is not split) */

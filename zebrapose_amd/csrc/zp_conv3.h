@@ -21,6 +21,7 @@ void conv3w_launch(const zp_conv_args& a, const conv_taps& tg, hipStream_t st, i
 int conv3w_splitk(const zp_conv_args& a);         // split-K slices of the wide tile (1: none)
 int conv3w_splitk_mode(int v);                    // zp_conv_tuning key 12; returns the previous value
 int conv3w_tp(const zp_conv_args& a);            // pixel tile of the wide kernel (256, or 128)
+int conv3w_tp_head(const zp_conv_args& a);       // pixel tile the fused head's conv would run on
 int conv3w_acc_mode(int v);                       // zp_conv_tuning key 13; returns the previous value
 int conv3w_tp128_mode(int v);                     // zp_conv_tuning key 14; returns the previous value
 int conv3w_subint_mode(int v);                    // zp_conv_tuning key 17; returns the previous value

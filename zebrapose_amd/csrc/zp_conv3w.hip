@@ -44,6 +44,8 @@ constexpr int ACC_FLUSH = 0;  // k_conv3's: correction accumulator flushed per s
 constexpr int ACC_SA = 1;     // one scaled accumulator (round 4): biased, see the numerics note
 constexpr int ACC_PS = 2;     // per-step partial from zero, added by a rounding v_add_f32 (round 5)
 constexpr int ACC_FS = 3;     // ACC_FLUSH with acc on the 2^11 scale: the flush is a plain v_add_f32
+constexpr int ACC_P2 = 4;     // round 6: a persistent second accumulator for the corrections, joined once
+                              // after the K loop (the 256 x 128 tile only: 64 more accumulator VGPRs)
 
 __device__ __forceinline__ void wbarrier() {
   __builtin_amdgcn_s_barrier();
@@ -79,7 +81,9 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
   constexpr int TC = 256, TP = TPX;
   static_assert(TP == 256 || TP == 128, "pixel tile");
   static_assert(TP == 256 || (!HEAD && !BF && DM == 1), "the 256 x 128 tile: plain epilogue, default DMA order");
-  constexpr bool SA = NUM != ACC_FLUSH;              // accumulators on the 2^11 scale (NUM 1, 2, 3)
+  constexpr bool SA = NUM == ACC_SA || NUM == ACC_PS || NUM == ACC_FS;  // accumulators on the 2^11 scale
+  constexpr bool P2 = NUM == ACC_P2;
+  static_assert(!P2 || (TPX == 128 && !HEAD), "the persistent correction accumulator: 256 x 128 tiles");
   constexpr int NTW = TC / 16, NT = (TC + TP) / 16;  // weight tiles / all tiles per plane (16 rows each)
   constexpr int UNITS = NPL * NT;                    // 1 KB DMA units per stage
   constexpr int WC = 8, WP = TP / 64;                // per wave: 8 cout blocks x 4 (TP 128: 2) pixel blocks
@@ -104,7 +108,7 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
   int bx = blockIdx.x, by = blockIdx.y;
   const int total = gridDim.x * gridDim.y;
   if ((flags & 32768) && nsplit == 1 && A.nsub > 1 && (total & 7) == 0) {
-    // sub-interleaved order (round 6, conv3w_launch sets it for the ConvT phases): the subs of a
+    // sub-interleaved order (round 6, zp_conv_tuning key 17; measured slower, off): the subs of a
     // pixel tile are dispatched back to back on one XCD (dispatch id % 8 picks the XCD), longest
     // first, so the input strip all four phases read is fetched from HBM once and hit in that
     // XCD's L2 by the others (phase-major order re-read the input once per phase: up2's ConvT read
@@ -299,10 +303,20 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
   const unsigned sl0 = lds_addr(lds) + (unsigned)(2 * ASTG) * 1024u + (unsigned)(lane >> 4) * 256u;
 
   f32x4 acc[WC][WP];
+  // P2 (ACC_P2): the correction products' own running sums, one per block, for the whole K loop --
+  // no per-step flush (4 v_fma_f32 per block and step, which with 2 waves per SIMD kept the vector
+  // issue port ~95% busy beside the MFMAs: tools/conv3_ab.py ablations)
+  f32x4 c2acc[P2 ? WC : 1][P2 ? WP : 1];
 #pragma unroll
   for (int i = 0; i < WC; ++i)
 #pragma unroll
     for (int j = 0; j < WP; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  if constexpr (P2) {
+#pragma unroll
+    for (int i = 0; i < WC; ++i)
+#pragma unroll
+      for (int j = 0; j < WP; ++j) c2acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
 
   // fragment reads: inline-asm ds_read_b128 with explicit lgkmcnt waits.  Plain LDS loads would
   // make the compiler put an s_waitcnt vmcnt(0) in front of every fragment read issued after the
@@ -334,7 +348,7 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
     }
   };
   auto step = [&](auto s_c, const bool more, const bool strip_now) {
-    constexpr int s = decltype(s_c)::value;
+    const int s = (int)s_c;  // (a compile-time stage, or -- P2's one-step loop -- a runtime one)
     // the next step's DMA (into the other buffer: every wave has passed the barrier that ended the
     // step which read it): one piece per cout block, after that block's correction MFMAs, so that
     // the issue cost (~60 cycles per piece beside MFMAs) is spread over the step
@@ -406,6 +420,9 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
           MT::mma(acc[i][j], af[i % 3][1], bf[0][j]);
         } else if constexpr (NUM == ACC_PS) {
           MT::mma(c2[j], hs, bf[0][j]);
+        } else if constexpr (P2) {  // hi*lo', then lo'*hi (k_conv3's term order) into the block's running sum
+          MT::mma(c2acc[i][j], af[i % 3][0], bf[1][j]);
+          MT::mma(c2acc[i][j], af[i % 3][1], bf[0][j]);
         } else {
           MT::mma(c2[j], af[i % 3][0], bf[1][j]);
           MT::mma(c2[j], af[i % 3][1], bf[0][j]);
@@ -484,6 +501,15 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
       }
     }
   };
+  if constexpr (P2) {
+    // one step per iteration, the stage a runtime value: in the two-step unrolled loop LLVM gave the
+    // 128 loop-carried sums different registers in the two copies and spilled 52-61 VGPRs
+    for (int ks = 0; ks < nK; ++ks) {
+      const bool sn = STR && r_txi == 0 && ks + nx < nK;
+      step(ks & 1, ks + 1 < nK, sn);
+      end_step(sn);
+    }
+  } else
   for (int ks = 0; ks < nK; ks += 2) {
     // step ks on buffer 0, issuing the DMA of step ks + 1 into buffer 1
     const bool sn0 = STR && r_txi == 0 && ks + nx < nK;
@@ -493,6 +519,14 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
     const bool sn1 = STR && r_txi == 0 && ks + 1 + nx < nK;
     step(I1{}, ks + 2 < nK, sn1);
     end_step(sn1);
+  }
+  if constexpr (P2) {  // the corrections join the main sums once: acc = fma(c2, 2^-11, acc) (one rounding)
+#pragma unroll
+    for (int i = 0; i < WC; ++i)
+#pragma unroll
+      for (int j = 0; j < WP; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = __builtin_fmaf(c2acc[i][j][r], SplitF32<2>::CS, acc[i][j][r]);
   }
 
   if (!HEAD && nsplit > 1) {  // split-K slice: raw f32 sums (acc[i][j] = 4 channels x one grid point)
@@ -772,7 +806,7 @@ int conv3w_tp128_mode(int v) {
 static int conv3w_acc() {
   static const int env = getenv("ZP_CONV3W_ACC") ? atoi(getenv("ZP_CONV3W_ACC")) : ACC_FLUSH;
   const int v = g_conv3w_acc >= 0 ? g_conv3w_acc : env;
-  return (v == ACC_PS || v == ACC_SA || v == ACC_FS) ? v : ACC_FLUSH;
+  return (v == ACC_PS || v == ACC_SA || v == ACC_FS || v == ACC_P2) ? v : ACC_FLUSH;
 }
 static bool conv3w_tp128_on() {
   static const int env = getenv("ZP_CONV3W_TP128") ? atoi(getenv("ZP_CONV3W_TP128")) : 0;
@@ -790,6 +824,7 @@ int conv3w_min_blocks(int v) {
   return old;
 }
 
+static int conv3w_tp_base(const zp_conv_args& a);
 bool conv3w_ok(const zp_conv_args& a) {
   static const int env = getenv("ZP_CONV3W") ? atoi(getenv("ZP_CONV3W")) : 1;
   const int en = g_conv3w >= 0 ? g_conv3w : env;
@@ -806,14 +841,21 @@ bool conv3w_ok(const zp_conv_args& a) {
     for (int s = 0; s < a.nsub; ++s)
       if (a.sub[s].ntaps > 4) return false;
   const long blocks = (((long)a.N * a.GH * a.GW + 255) / 256) * (a.Cout / 256) * a.nsub;
-  return blocks >= g_conv3w_min || conv3w_splitk(a) > 1 || conv3w_tp(a) == 128;
+  return blocks >= g_conv3w_min || conv3w_splitk(a) > 1 || conv3w_tp_base(a) == 128;
 }
 
 // pixel tile of the wide kernel: 256, or 128 for a one-sub launch whose 256 x 256 grid would leave
 // CUs idle (fewer than g_conv3w_min tiles, no split-K) while its 256 x 128 grid fills them (bs 32:
 // layer4's 256 -> 256 3 x 3s at 32 x 32 and conv_1x1_3, 128 -> 256 tiles; they ran on k_conv3's
 // 128 x 256 tile).  k_conv3w<TP = 128>: a wave owns 8 x 2 blocks, 6 DMA pieces per step.
+// ACC_P2 (key 13 = 4) runs every unsplit launch on the 256 x 128 tile (its persistent correction
+// accumulator does not fit the 256 x 256 tile's registers); the fused head keeps the 256 x 256 tile
 int conv3w_tp(const zp_conv_args& a) {
+  if (conv3w_acc() == ACC_P2 && conv3w_splitk(a) == 1) return 128;
+  return conv3w_tp_base(a);
+}
+int conv3w_tp_head(const zp_conv_args& a) { return conv3w_tp_base(a); }
+static int conv3w_tp_base(const zp_conv_args& a) {
   const long M = (long)a.N * a.GH * a.GW;
   if (((M + 255) / 256) * (a.Cout / 256) * a.nsub >= g_conv3w_min) return 256;
   if (!conv3w_tp128_on() || a.nsub != 1 || conv3w_splitk(a) > 1) return 256;
@@ -865,7 +907,11 @@ static bool conv3w_strip_ok(const zp_conv_args& a, const conv_taps& tg, int fl, 
 }
 
 // zp_conv_tuning key 17: the subs (ConvT phases) of a multi-sub launch interleaved per pixel tile on
-// one XCD (1, default) or dispatched phase by phase, longest first (0) (-1: ZP_CONV3W_SUBINT or 1)
+// one XCD (1) or dispatched phase by phase, longest first (0, default) (-1: ZP_CONV3W_SUBINT or 0).
+// Measured (round 6, tools/conv3_ab.py --wsubint 0,1, bs 32): up2's ConvT 593 -> 803 us, up1's
+// 130 -> 170 us interleaved -- the input is read once instead of once per phase, but four phases'
+// weight streams and the 537 MB output then share each XCD's L2, and every workgroup of a round runs
+// a different phase: off
 static int g_conv3w_subint = -1;
 int conv3w_subint_mode(int v) {
   const int old = g_conv3w_subint;
@@ -873,7 +919,7 @@ int conv3w_subint_mode(int v) {
   return old;
 }
 static bool conv3w_subint() {
-  static const int env = getenv("ZP_CONV3W_SUBINT") ? atoi(getenv("ZP_CONV3W_SUBINT")) : 1;
+  static const int env = getenv("ZP_CONV3W_SUBINT") ? atoi(getenv("ZP_CONV3W_SUBINT")) : 0;
   return (g_conv3w_subint >= 0 ? g_conv3w_subint : env) != 0;
 }
 
@@ -908,11 +954,17 @@ void conv3w_launch(const zp_conv_args& a0, const conv_taps& tg0, hipStream_t st,
   const int acc = (fl & 536870912) ? ACC_FLUSH : conv3w_acc();  // (flag 536870912: the flushed form, as in round 4)
   if (a.nsub > 1 && ns == 1 && conv3w_subint()) fl |= 32768;  // the phases of a pixel tile adjacent on one XCD
   const bool str = conv3w_strip_ok(a, tg, fl, ns);
-  if (ns == 1 && conv3w_tp(a) == 128) {  // the 256 x 128 tile (zp_conv_tuning key 14)
+  if (ns == 1 && conv3w_tp(a) == 128) {  // the 256 x 128 tile (zp_conv_tuning key 14; key 13 = 4: ACC_P2)
     const dim3 g128((unsigned)(((long)a.N * a.GH * a.GW + 127) / 128), (unsigned)(a.Cout / 256), (unsigned)a.nsub);
-    if (conv3w_strip_ok(a, tg, fl, ns, 128))
+    const bool s128 = conv3w_strip_ok(a, tg, fl, ns, 128);
+    if (acc == ACC_P2) {
+      if (s128) hipLaunchKernelGGL((k_conv3w<0, 1, false, false, false, false, true, ACC_P2, 128>), g128, dim3(512), 0, st, a, tg, fl, H, ws, ns);
+      else hipLaunchKernelGGL((k_conv3w<0, 1, false, false, false, false, false, ACC_P2, 128>), g128, dim3(512), 0, st, a, tg, fl, H, ws, ns);
+    } else if (s128) {
       hipLaunchKernelGGL((k_conv3w<0, 1, false, false, false, false, true, ACC_FLUSH, 128>), g128, dim3(512), 0, st, a, tg, fl, H, ws, ns);
-    else hipLaunchKernelGGL((k_conv3w<0, 1, false, false, false, false, false, ACC_FLUSH, 128>), g128, dim3(512), 0, st, a, tg, fl, H, ws, ns);
+    } else {
+      hipLaunchKernelGGL((k_conv3w<0, 1, false, false, false, false, false, ACC_FLUSH, 128>), g128, dim3(512), 0, st, a, tg, fl, H, ws, ns);
+    }
     return;
   }
   const dim3 grid((unsigned)(((long)a.N * a.GH * a.GW + 255) / 256), (unsigned)(a.Cout / 256), (unsigned)(a.nsub * ns));
@@ -949,7 +1001,8 @@ void conv3w_launch(const zp_conv_args& a0, const conv_taps& tg0, hipStream_t st,
 void conv3w_head_launch(const zp_conv_args& a, const conv_taps& tg, const zp_head_args& h, hipStream_t st, int fl) {
   const dim3 grid((unsigned)(((long)a.N * a.GH * a.GW + 255) / 256), 1u, 1u);
   const bool str = conv3w_strip_ok(a, tg, fl, 1);
-  const int acc = (fl & 536870912) ? ACC_FLUSH : conv3w_acc();
+  int acc = (fl & 536870912) ? ACC_FLUSH : conv3w_acc();
+  if (acc == ACC_P2) acc = ACC_FLUSH;  // (the 256 x 256 head tile: the flushed form)
   if (acc == ACC_SA) {  // (A/B)
     if (str) hipLaunchKernelGGL((k_conv3w<0, 1, true, false, false, false, true, ACC_SA>), grid, dim3(512), 0, st, a, tg, fl, h, nullptr, 1);
     else hipLaunchKernelGGL((k_conv3w<0, 1, true, false, false, false, false, ACC_SA>), grid, dim3(512), 0, st, a, tg, fl, h, nullptr, 1);
