@@ -110,6 +110,7 @@ def _worker(port, mode, q):
                "nparams": len(local),
                "hook_progress": {n: list(v) for n, v in seen.items()}}
         if mode == "buckets":
+            res["avg"] = ts.buckets._avg  # RCCL's ReduceOp.AVG accepted (the 8-GPU run's mean)
             res["nflats"] = len(ts.buckets._buf_flats)
             # every BN buffer is a view of one of those flat tensors
             res["buf_outside"] = [n for n, b in net.named_buffers()
@@ -188,3 +189,4 @@ def test_rccl_world1_grad_exchange(gpu, mode):
         assert not res["buf_outside"], res["buf_outside"]
         assert res["allreduce_identity"]
         assert not res["outside_bucket"], res["outside_bucket"]
+        assert res["avg"] is True, res["avg"]  # the buckets' mean is RCCL's ReduceOp.AVG

@@ -195,15 +195,17 @@ class GradBuckets:
             ev = torch.cuda.Event(enable_timing=True)
             ev.record()
             self.timing.append((b, ev))
-        op = dist.ReduceOp.SUM
+        if self._avg is None:
+            self._avg = dist.get_backend(self._pg()) == "nccl" and hasattr(dist.ReduceOp, "AVG")
+        if self._avg:  # (also at world size 1, where it is the identity: the RCCL path stays exercised)
+            try:
+                bk[3] = dist.all_reduce(bk[0], op=dist.ReduceOp.AVG, group=self.group, async_op=True)
+                return
+            except (RuntimeError, ValueError):  # a backend build without ncclAvg: divide, then sum
+                self._avg = False
         if self.world > 1:
-            if self._avg is None:
-                self._avg = dist.get_backend(self._pg()) == "nccl" and hasattr(dist.ReduceOp, "AVG")
-            if self._avg:
-                op = dist.ReduceOp.AVG
-            else:
-                bk[0].div_(self.world)
-        bk[3] = dist.all_reduce(bk[0], op=op, group=self.group, async_op=True)
+            bk[0].div_(self.world)
+        bk[3] = dist.all_reduce(bk[0], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
     def dest(self, p):
         """The slice of p's bucket the engine writes p's gradient into (None: p is not bucketed)."""
