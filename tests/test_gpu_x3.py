@@ -445,6 +445,32 @@ def test_wide_tp128_is_f32_accurate(gpu, geom):
     assert names == ["k_conv3w<h2,TP=128>"], names
 
 
+MF32_GEOMS = [
+    ("conv", 256, 256, 3, 1, 1, 1, False, 64),    # up1's 3x3 (strips), residual
+    ("conv", 512, 512, 3, 1, 4, 4, False, 32),    # layer5 d4 (strips)
+    ("conv", 256, 512, 1, 1, 0, 1, False, 32),    # layer5's downsample (1x1: per-step tiles)
+    ("convT", 256, 256, 3, 2, 1, 1, False, 32),   # up1's ConvT (four phases)
+    ("convT", 320, 256, 3, 2, 1, 1, False, 32),   # up2's ConvT over [up1 | x_64] (Cin 320)
+]
+
+
+@pytest.mark.parametrize("geom", MF32_GEOMS, ids=[_gid(g) for g in MF32_GEOMS])
+def test_wide_mf32_is_f32_accurate(gpu, geom):
+    """k_conv3w32 (round 6, zp_conv_tuning key 18): the 256 x 256 two-plane tile on
+    v_mfma_f32_32x32x16_f16 -- the same staging and flushed numerics as k_conv3w, a different MFMA
+    shape, lane layout and epilogue pairing (v_permlane32_swap).  At bs 16 / 32 its error against float64
+    is within the two-plane bound of the exact-f32-MFMA kernel's (as every geometry in
+    test_split_conv_is_f32_accurate), residual on for the stride-1 convs."""
+    from zebrapose_amd import _lib as L
+    names = []
+    old = L.lib.zp_conv_tuning(18, 1)
+    try:
+        _check_geom(gpu, geom, "h2", B=16 if geom[-1] == 64 else 32, names_out=names)  # (>= 256 tiles)
+    finally:
+        L.lib.zp_conv_tuning(18, old)
+    assert names == ["k_conv3w<h2>"], names
+
+
 @pytest.mark.parametrize("geom", [("conv", 512, 512, 3, 1, 4, 4, False, 32), ("conv", 256, 256, 3, 1, 1, 1, False, 64)],
                          ids=["l5_d4_K144", "up1_K72"])
 def test_wide_accumulation_forms(gpu, geom):
@@ -456,7 +482,8 @@ def test_wide_accumulation_forms(gpu, geom):
       2 = per-step partial sums from zero added by v_add_f32: smaller rms, but the corrections are
           still truncated against the step's main partial;
       4 = (round 6) a persistent correction accumulator per block for the whole K loop, joined to the
-          main sum by one rounding FMA after it (the 256 x 128 tile).
+          main sum by one rounding FMA after it (the 256 x 128 tile);
+      mf32 = the flushed form on 32 x 32 x 16 MFMAs (k_conv3w32, key 18).
     The default's mean signed error (relative to the mean |output|) must be within 3x the exact-f32
     MFMA kernel's (+ a 2^-27 floor) and under a tenth of the one-accumulator form's, its rms within
     the two-plane bound of the f32 kernel's."""
@@ -492,12 +519,14 @@ def test_wide_accumulation_forms(gpu, geom):
     eng = Engine(torch.nn.Module(), torch.float32, split="h2")
     old_min, old_acc, old_sk = L.lib.zp_conv_tuning(11, 1), L.lib.zp_conv_tuning(13, -1), L.lib.zp_conv_tuning(12, 0)
     try:
-        for acc in (-1, 0, 1, 2, 4):
-            L.lib.zp_conv_tuning(13, acc)
+        for acc in (-1, 0, 1, 2, 4, "mf32"):
+            old18 = L.lib.zp_conv_tuning(18, 1 if acc == "mf32" else 0)
+            L.lib.zp_conv_tuning(13, 0 if acc == "mf32" else acc)
             oa = Act(eng._empty((B, H, H, cout), gpu))
             eng.stage_log = []
             eng.unit_fwd(unit, xa, oa, None)
             torch.cuda.synchronize()
+            L.lib.zp_conv_tuning(18, old18)
             want = "k_conv3w<h2,TP=128>" if acc == 4 else "k_conv3w<h2>"
             assert [r[1] for r in eng.stage_log] == [want], eng.stage_log
             stat[acc] = stats(oa)
@@ -512,7 +541,7 @@ def test_wide_accumulation_forms(gpu, geom):
     # the default (-1) is one of the unbiased forms: the flushed one (0) or, since round 6, the
     # persistent correction accumulator on the 256 x 128 tile (4)
     assert stat[-1] in (stat[0], stat[4])
-    for form in (0, 4):  # both unbiased: the corrections are never added into the 2^11-larger main sum
+    for form in (0, 4, "mf32"):  # unbiased: the corrections are never added into the 2^11-larger main sum
         assert abs(stat[form][0]) <= 3.0 * abs(stat["f32"][0]) + 2.0 ** -27, (form, stat)
         assert abs(stat[form][0]) <= abs(stat[1][0]) / 10.0, (form, stat)
         assert stat[form][1] <= BOUND["h2"][0] * stat["f32"][1], (form, stat)

@@ -47,6 +47,8 @@ def bench_label(name):
         return f"k_conv1x1n<{tn[m.group(1)]}>"
     if "k_stem_h2" in name:  # the direct two-plane stem (zp_stem_split)
         return "k_stem_h2"
+    if re.search(r"k_conv3w32<(true|false)>", name):  # the 256 x 256 tile on 32x32x16 MFMAs (round 6, key 18)
+        return "k_conv3w<h2>"  # (the engine's label: zp_conv2d_config reports the wide tile either way)
     # the 256 x 256 two-plane tile (+ fused head); template <ABL, DM, HEAD, SGB, PF, BF, STR, NUM, TPX>
     # (TPX 128: the 256 x 128 tile)
     m = re.search(r"k_conv3w<(\d+), (\d+), (true|false)((?:, (?:true|false|\d+))*)>", name)

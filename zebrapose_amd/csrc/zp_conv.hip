@@ -3350,7 +3350,8 @@ extern "C" int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* st
  * key 16: k_conv3's multi-sub launches (the merged ASPP) with a tile's subs adjacent on one XCD (1) or
  * the sub slowest (0, default: measured faster; -1 = ZP_CONV3_SUBINT); key 17: k_conv3w's multi-sub
  * launches (the ConvT phases) with a pixel tile's phases adjacent on one XCD (1) or phase by phase,
- * longest first (0, default: measured faster; -1 = ZP_CONV3W_SUBINT).
+ * longest first (0, default: measured faster; -1 = ZP_CONV3W_SUBINT); key 18: k_conv3w's 256 x 256 tile
+ * on v_mfma_f32_32x32x16_f16 (k_conv3w32; 1) or 16 x 16 x 32 (0, default; -1 = ZP_CONV3W_MF32).
  * Returns the previous value. */
 /* split-fp32 split-K workspace: bytes of f32 slices zp_conv2d uses for these args when a.stats
  * points to that many (0: the launch is not split) */
@@ -3402,6 +3403,7 @@ extern "C" int zp_conv_tuning(int key, int value) {
   if (key == 15) return bn_fused_mode(value);
   if (key == 16) return conv3_subint_mode(value);
   if (key == 17) return conv3w_subint_mode(value);
+  if (key == 18) return conv3w_mf32_mode(value);
   if (key == 4) {
     const int old = g_wgrad2_rounds;
     g_wgrad2_rounds = value > 0 ? value : 1;

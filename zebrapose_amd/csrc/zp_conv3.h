@@ -25,5 +25,9 @@ int conv3w_tp_head(const zp_conv_args& a);       // pixel tile the fused head's 
 int conv3w_acc_mode(int v);                       // zp_conv_tuning key 13; returns the previous value
 int conv3w_tp128_mode(int v);                     // zp_conv_tuning key 14; returns the previous value
 int conv3w_subint_mode(int v);                    // zp_conv_tuning key 17; returns the previous value
+// k_conv3w32 (zp_conv3w32.hip): the 256 x 256 tile on 32 x 32 MFMAs
+int conv3w_mf32_mode(int v);                      // zp_conv_tuning key 18; returns the previous value
+bool conv3w_mf32_on();
+void conv3w32_launch(const zp_conv_args& a, const conv_taps& tg, hipStream_t st, int flags, bool str);
 void conv3w_head_launch(const zp_conv_args& a, const conv_taps& tg, const zp_head_args& h, hipStream_t st, int flags);
 }  // namespace zp

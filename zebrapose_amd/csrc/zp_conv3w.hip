@@ -967,6 +967,10 @@ void conv3w_launch(const zp_conv_args& a0, const conv_taps& tg0, hipStream_t st,
     }
     return;
   }
+  if (ns == 1 && acc == ACC_FLUSH && conv3w_mf32_on()) {  // the 32 x 32 MFMA form (zp_conv_tuning key 18)
+    conv3w32_launch(a, tg, st, fl, str);
+    return;
+  }
   const dim3 grid((unsigned)(((long)a.N * a.GH * a.GW + 255) / 256), (unsigned)(a.Cout / 256), (unsigned)(a.nsub * ns));
   // flags 262144 / 524288: the DMA pieces over the first 2 / 8 cout blocks (default: the first one);
   // 1048576 / 2097152: DM 1 / 8 with the MFMA / flush interleave (SGB)
