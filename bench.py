@@ -647,7 +647,9 @@ def run(args):
         K = args.train_steps or max(3, args.steps // 2)
 
         def timed_train(ts):
-            for _ in range(max(2, args.warmup // 2)):
+            # (the first steps initialise the Adam state and grow the caching allocator: W full
+            # warm-up steps, not W / 2, so the timed steps are steady-state)
+            for _ in range(max(3, args.warmup)):
                 ts(x, gt_code, gt_mask)
             torch.cuda.synchronize()
             if world > 1:

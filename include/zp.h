@@ -184,8 +184,10 @@ long long zp_conv2d_split_ws(const zp_conv_args* a);
  * accumulator; 2 per-step partial sums; 3 flushed on the 2^11 scale); key 14 = its 256 x 128 tile
  * (default 0); key 15 = zp_bn_train_finalize's merge in one launch (1, default) or two (0); key 16 =
  * k_conv3's multi-sub launches with a tile's subs adjacent on one XCD (default 0); key 17 = k_conv3w's
- * multi-sub launches (ConvT phases) with a pixel tile's phases adjacent on one XCD (default 0).  Returns
- * the previous value, -1 for an unknown key. */
+ * multi-sub launches (ConvT phases) with a pixel tile's phases adjacent on one XCD (default 0); key 18
+ * = the 256 x 256 two-plane tile on 32x32x16 MFMAs (default 0); key 19 = the ring depth (2, 3, 4) of
+ * the register-pipelined two-plane 64-channel tile (default 2).  Returns the previous value, -1 for
+ * an unknown key. */
 int zp_conv_tuning(int key, int value);
 
 /* Fused 1x1 head (the reference's conv_1x1_4 over torch.cat([x, x_128]) and the mask / code split,

@@ -615,3 +615,46 @@ def test_schedule_flags_are_bit_identical(gpu, geom, B, kernel, tp128):
     assert names == [kernel], names
     for extra in _BITWISE_FLAGS + ["subint1"]:
         assert torch.equal(outs[extra], outs[0]), (geom, extra)
+
+
+@pytest.mark.parametrize("geom,B", [(("conv", 256, 256, 3, 1, 2, 2, False, 32), 1),   # bs 1 layer4: split-K
+                                    (("conv", 64, 128, 3, 2, 1, 1, False, 64), 2),    # layer2's first conv
+                                    (("conv", 64, 128, 3, 2, 1, 1, False, 64), 32)],  # the same, unsplit
+                         ids=["l4_bs1_splitk", "l2a_bs2_splitk", "l2a_bs32"])
+def test_pipe_ring_depth_is_bit_identical(gpu, geom, B):
+    """zp_conv_tuning key 19 (round 6): the register-pipelined two-plane 64-channel k_conv3 tile with
+    a 3- or 4-stage ring instead of 2 moves the DMA further ahead only -- the stored outputs (split-K
+    slices summed by k_splitk_epi, or the direct epilogue) are bit-identical to the default's."""
+    from zebrapose_amd import _lib as L
+    from zebrapose_amd.engine import Engine, Unit, Act
+    from zebrapose_amd.model import layers as LY
+    kind, cin, cout, k, s, p, d, bias, H = geom
+    torch.manual_seed(12)
+    conv = LY.Conv2d(cin, cout, k, s, p, d, bias=bias)
+    bn = LY.BatchNorm2d(cout)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.normal_(0, 0.1)
+        bn.running_mean.normal_(0, 0.1)
+        bn.running_var.uniform_(0.5, 1.5)
+    conv, bn = conv.to(gpu).eval(), bn.to(gpu).eval()
+    unit = Unit(conv, bn, relu=True)
+    OH, OW = unit.out_hw(H, H)
+    x = torch.randn(B, cin, H, H)
+    eng = Engine(torch.nn.Module(), torch.float32, split="h2")
+    xa = Act(_split_act(x.permute(0, 2, 3, 1).contiguous(), gpu, "h2"))
+    outs = {}
+    for st in (2, 3, 4):
+        old = L.lib.zp_conv_tuning(19, st)
+        try:
+            oa = Act(eng._empty((B, OH, OW, cout), gpu))
+            eng.stage_log = []
+            eng.unit_fwd(unit, xa, oa, None)
+            torch.cuda.synchronize()
+        finally:
+            L.lib.zp_conv_tuning(19, old)
+        assert [r[1] for r in eng.stage_log] == ["k_conv3<h2,WC=2,NWP=2>"], eng.stage_log
+        outs[st] = oa.buf._base.clone()
+    assert float(outs[2].float().abs().sum()) > 0
+    for st in (3, 4):
+        assert torch.equal(outs[st], outs[2]), (geom, B, st)

@@ -43,6 +43,8 @@ def main():
     ap.add_argument("--tp128", default="-1", help="zp_conv_tuning key 14 values to A/B (k_conv3w 256 x 128 tile: 0, 1)")
     ap.add_argument("--subint", default="-1", help="zp_conv_tuning key 16 values to A/B (k_conv3 multi-sub interleave: 0, 1)")
     ap.add_argument("--mf32", default="-1", help="zp_conv_tuning key 18 values to A/B (k_conv3w on 32x32x16 MFMAs: 0, 1)")
+    ap.add_argument("--graph", action="store_true", help="time hipGraph replays of the iters launches (no host "
+                    "launch overhead: the bs = 1 launches are shorter than their eager enqueue)")
     ap.add_argument("--wsubint", default="-1", help="zp_conv_tuning key 17 values to A/B (k_conv3w ConvT phases "
                     "interleaved per pixel tile: 0, 1)")
     a = ap.parse_args()
@@ -133,11 +135,24 @@ def main():
                                    f"max |ref| {float(jr.abs().max()):.3e}")
                         print(f"{name} {f}: {nd} of {ref.numel()} stored halves differ from the first setting{msg}")
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                for _ in range(a.iters):
-                    run1()
-                e1.record()
-                torch.cuda.synchronize()
+                if a.graph:
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g):
+                        for _ in range(a.iters):
+                            run1()
+                    g.replay()
+                    torch.cuda.synchronize()
+                    e0.record()
+                    g.replay()
+                    e1.record()
+                    torch.cuda.synchronize()
+                    del g
+                else:
+                    e0.record()
+                    for _ in range(a.iters):
+                        run1()
+                    e1.record()
+                    torch.cuda.synchronize()
                 us = e0.elapsed_time(e1) * 1e3 / a.iters
                 res.setdefault((name, f), []).append(us)
     L.lib.zp_conv_tuning(1, -1)

@@ -3351,7 +3351,9 @@ extern "C" int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* st
  * the sub slowest (0, default: measured faster; -1 = ZP_CONV3_SUBINT); key 17: k_conv3w's multi-sub
  * launches (the ConvT phases) with a pixel tile's phases adjacent on one XCD (1) or phase by phase,
  * longest first (0, default: measured faster; -1 = ZP_CONV3W_SUBINT); key 18: k_conv3w's 256 x 256 tile
- * on v_mfma_f32_32x32x16_f16 (k_conv3w32; 1) or 16 x 16 x 32 (0, default; -1 = ZP_CONV3W_MF32).
+ * on v_mfma_f32_32x32x16_f16 (k_conv3w32; 1) or 16 x 16 x 32 (0, default; -1 = ZP_CONV3W_MF32);
+ * key 19: ring depth (2, 3, 4) of k_conv3's register-pipelined two-plane 64-channel tile (-1 =
+ * ZP_CONV3_PIPE_ST or 2, the default: measured fastest).
  * Returns the previous value. */
 /* split-fp32 split-K workspace: bytes of f32 slices zp_conv2d uses for these args when a.stats
  * points to that many (0: the launch is not split) */
@@ -3404,6 +3406,7 @@ extern "C" int zp_conv_tuning(int key, int value) {
   if (key == 16) return conv3_subint_mode(value);
   if (key == 17) return conv3w_subint_mode(value);
   if (key == 18) return conv3w_mf32_mode(value);
+  if (key == 19) return conv3_pipe_st_mode(value);
   if (key == 4) {
     const int old = g_wgrad2_rounds;
     g_wgrad2_rounds = value > 0 ? value : 1;

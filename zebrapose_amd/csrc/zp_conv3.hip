@@ -403,7 +403,7 @@ __global__ void __launch_bounds__(128 * NWP) k_conv3(const zp_conv_args A, const
   constexpr int GRP = NPL * TPW;                     // DMA instructions per wave per stage
   using MT = SplitMfma<NPL>;
   using TM = Terms<NPL>;
-  static_assert(ST == 2 || ST == 3, "ring depth");
+  static_assert(ST == 2 || ST == 3 || (PIPE && ST == 4), "ring depth");
   static_assert(ST == 2 || NT % NW == 0, "counted vmcnt waits need the same DMA count on every wave");
   static_assert(!PIPE || NW == 4, "the register-pipelined schedule runs one wave per SIMD");
   static_assert(WP == 4 || WP == 8, "pixel fragments per wave");
@@ -757,11 +757,22 @@ __global__ void __launch_bounds__(128 * NWP) k_conv3(const zp_conv_args A, const
     using S0 = std::integral_constant<int, 0>;
     using S1 = std::integral_constant<int, 1>;
     using S2 = std::integral_constant<int, 2 % ST>;
+    using S3 = std::integral_constant<int, 3 % ST>;
     if constexpr (ST == 2) {
       for (int ks = 0; ks < nK; ks += 2) {
         pstep(S0{}, ks, fa0, fb0, fa1, fb1);
         if (ks + 1 >= nK) break;
         pstep(S1{}, ks + 1, fa1, fb1, fa0, fb0);
+      }
+    } else if constexpr (ST == 4) {  // buffer period 4, fragment-set period 2: unrolled by 4
+      for (int ks = 0; ks < nK; ks += 4) {
+        pstep(S0{}, ks, fa0, fb0, fa1, fb1);
+        if (ks + 1 >= nK) break;
+        pstep(S1{}, ks + 1, fa1, fb1, fa0, fb0);
+        if (ks + 2 >= nK) break;
+        pstep(S2{}, ks + 2, fa0, fb0, fa1, fb1);
+        if (ks + 3 >= nK) break;
+        pstep(S3{}, ks + 3, fa1, fb1, fa0, fb0);
       }
     } else {  // buffer period 3, fragment-set period 2: unrolled by 6
       for (int ks = 0; ks < nK; ks += 6) {
@@ -1186,6 +1197,23 @@ int conv3_subint_mode(int v) {
   return old;
 }
 
+// zp_conv_tuning key 19: ring depth of the register-pipelined two-plane 64 x 128 k_conv3 tile (one
+// wave per SIMD; 2, 3 or 4 stages; -1: ZP_CONV3_PIPE_ST or 2).  The DMA runs ST - 1 steps ahead of
+// the step computing; the bs = 1 launches' split-K slices run 5-18 K steps each.  Measured (whole
+// fp32 forward, hipGraph, tools/bs1_ab.py, profiles/r06_conv_ablations.md): bs 1 1.540 / 1.580 /
+// 1.616 ms and bs 32 9.527 / 9.548 / 9.549 ms for 2 / 3 / 4 stages, bit-identical -- 2 stays
+static int g_pipe_st = -1;
+int conv3_pipe_st_mode(int v) {
+  const int old = g_pipe_st;
+  g_pipe_st = v;
+  return old;
+}
+static int conv3_pipe_st() {
+  static const int env = getenv("ZP_CONV3_PIPE_ST") ? atoi(getenv("ZP_CONV3_PIPE_ST")) : 2;
+  const int v = g_pipe_st >= 0 ? g_pipe_st : env;
+  return v == 3 || v == 4 ? v : 2;
+}
+
 int conv3_splitk_mode(int v) {
   const int old = g_splitk;
   g_splitk = v;
@@ -1268,6 +1296,11 @@ static void conv3_dispatch(const zp_conv_args& a, const conv_taps& tg, int tc, h
   else if (tc == 128 && tp == 256)
     hipLaunchKernelGGL((k_conv3<NPL, 4, 4, 4, ST8, false>), grid, dim3(512), 0, st, a, tg, fl, ws, ns);
   else if (tc == 128) hipLaunchKernelGGL((k_conv3<NPL, 4, 4, 2, 2, true>), grid, dim3(256), 0, st, a, tg, fl, ws, ns);
+  // (key 19, the deeper rings: the two-plane 64-channel tile only)
+  else if (tc == 64 && NPL == 2 && conv3_pipe_st() == 3)
+    hipLaunchKernelGGL((k_conv3<NPL, 2, 4, 2, NPL == 2 ? 3 : 2, true>), grid, dim3(256), 0, st, a, tg, fl, ws, ns);
+  else if (tc == 64 && NPL == 2 && conv3_pipe_st() == 4)
+    hipLaunchKernelGGL((k_conv3<NPL, 2, 4, 2, NPL == 2 ? 4 : 2, true>), grid, dim3(256), 0, st, a, tg, fl, ws, ns);
   else if (tc == 64) hipLaunchKernelGGL((k_conv3<NPL, 2, 4, 2, 2, true>), grid, dim3(256), 0, st, a, tg, fl, ws, ns);
   else hipLaunchKernelGGL((k_conv3<NPL, 1, 4, 2, 2, true>), grid, dim3(256), 0, st, a, tg, fl, ws, ns);
   if (ns > 1) {
