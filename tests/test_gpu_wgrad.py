@@ -4,7 +4,9 @@ with identical inputs the only difference left is f32 accumulation order, so the
 Covers every geometry class of the R34 backward: stem (Cin 3 padded to 8, 7x7 s2), 3x3 d1/d2/d4,
 strided 3x3 and 1x1 downsample, dilated ASPP with most taps in padding, 1x1 head with Cout 17
 (dy row pitch 32), transposed-conv phases, and grids large enough for several splits and pixel
-rows that wrap across image rows and batch items inside one K step."""
+rows that wrap across image rows and batch items inside one K step.  Round 6: the lean kernel at
+stride 2 (W 32 / 64 / 128 output grids) and the ConvT weight gradient computed as the stride-2 conv
+over dy with x as its output gradient (swap) as well as by the four phases."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -23,14 +25,26 @@ GEOMS = [
     ("conv", 320, 320, 17, 1, 1, 0, 1, 32, 2),
     ("convT", 256, 256, 256, 3, 2, 1, 1, 8, 4),
     ("convT", 320, 320, 256, 3, 2, 1, 1, 16, 2),
+    # (round 6) k_wgrad2 at stride 2 (output grid W 32 / 64 / 128), and the ConvT weight gradient as
+    # the stride-2 conv over dy (Engine._convT_wgrad_swap) on that kernel: up1's and up2's ConvTs
+    ("conv", 64, 64, 128, 3, 2, 1, 1, 64, 2),
+    ("conv", 64, 64, 128, 1, 2, 0, 1, 64, 2),
+    ("conv", 64, 64, 64, 3, 2, 1, 1, 128, 2),
+    ("conv", 64, 64, 64, 3, 2, 1, 1, 256, 1),
+    ("convT", 256, 256, 256, 3, 2, 1, 1, 32, 4),
+    ("convT", 320, 320, 256, 3, 2, 1, 1, 64, 2),
+    ("convT", 64, 64, 64, 3, 2, 1, 1, 128, 1),
 ]
 
 
-@pytest.mark.parametrize("geom", GEOMS, ids=[f"{g[0]}{g[1]}-{g[3]}k{g[4]}s{g[5]}d{g[7]}" for g in GEOMS])
-def test_wgrad_bf16(gpu, geom):
+@pytest.mark.parametrize("swap", [True, False], ids=["swap", "phases"])
+@pytest.mark.parametrize("geom", GEOMS, ids=[f"{g[0]}{g[1]}-{g[3]}k{g[4]}s{g[5]}d{g[7]}H{g[8]}" for g in GEOMS])
+def test_wgrad_bf16(gpu, geom, swap):
     from zebrapose_amd.engine import Engine, Unit, Act
     from zebrapose_amd.model import layers as LY
     kind, cin, cw, cout, k, s, p, d, H, B = geom
+    if kind == "conv" and not swap:
+        pytest.skip("the exchange applies to ConvTranspose2d only")
     torch.manual_seed(3)
     if kind == "conv":
         conv = LY.Conv2d(cw, cout, k, s, p, d, bias=False)
@@ -53,10 +67,12 @@ def test_wgrad_bf16(gpu, geom):
     want = w.grad
 
     eng = Engine(torch.nn.Module(), torch.bfloat16)
+    eng.convT_wgrad_swap = swap
     convg = conv.to(gpu)
     xa = Act(x.permute(0, 2, 3, 1).contiguous().to(gpu, torch.bfloat16))
     dya = Act(gy.permute(0, 2, 3, 1).contiguous().to(gpu, torch.bfloat16), 0, cout)
     dw = torch.empty_like(convg.weight)
+    assert eng._convT_wgrad_swap(unit, xa, dya) == (kind == "convT" and swap)
     eng._wgrad(unit, xa, unit.fwd_plan(H, H), dya, dw)
     torch.cuda.synchronize()
     got = dw.cpu()

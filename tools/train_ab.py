@@ -6,7 +6,8 @@ bs=32 256x256 bf16 training step (forward + loss + backward + Adam), synthetic c
 
 variant = '+'-joined knobs: side / noside (weight gradients on the engine's second stream or not),
 ymask (BN backward reads the stored activation for the ReLU mask instead of recomputing it from raw),
-r<N> (k_wgrad2 workgroup rounds, zp_conv_tuning key 4), l<N> (k_wgrad_lds rounds, key 5)."""
+r<N> (k_wgrad2 workgroup rounds, zp_conv_tuning key 4), l<N> (k_wgrad_lds rounds, key 5), phases (the
+ConvT weight gradient as four phases instead of the stride-2 conv over dy), nolean (k_wgrad2 off)."""
 import argparse
 import os
 import sys
@@ -47,6 +48,8 @@ def main():
         parts = v.split("+")
         eng.side_wgrad = "noside" not in parts
         eng.bn_mask_from_raw = "ymask" not in parts
+        eng.convT_wgrad_swap = "phases" not in parts  # (round 6) ConvT weight gradient as four phases
+        L.lib.zp_conv_tuning(3, 0 if "nolean" in parts else 1)  # k_wgrad2 off: the general kernel
         r = [int(q[1:]) for q in parts if q.startswith("r") and q[1:].isdigit()]
         L.lib.zp_conv_tuning(4, r[0] if r else 1)
         lr = [int(q[1:]) for q in parts if q.startswith("l") and q[1:].isdigit()]

@@ -2367,6 +2367,12 @@ __global__ void __launch_bounds__(512) k_wgrad_lds(const zp_wgrad_args A, float*
 // 4-7), its column validity a per-lane constant (W 128: one of two).  k_wgrad_lds, profiled on
 // the 256->256 3x3 at 128x128 (bs 32), spent 1.4 VALU + 1.0 SALU per MFMA on per-step pixel
 // arithmetic and ran the MFMA pipe 34% busy.
+// Stride 2 (round 6; the input grid twice the output grid): a lane's x pixel is (S (gy + rh) + ty,
+// S gx + tx) -- per lane (S rh + ty) IW + S gx + tx, per step the image and row (n IH + S gy) IW
+// (+ S 64 for the second half of a W 128 row).  That covers the stride-2 convs and, with x and dy
+// exchanged, the ConvTranspose2d(3, s2, p1, op1) weight gradient: dW[ci][co][ky][kx] = sum_g
+// x[g][ci] dy[2 g + (ky, kx) - 1][co] is the weight gradient of the stride-2 conv over dy whose
+// output gradient is x (geometry.convT_dgrad's plan; the engine's _wgrad).
 // ------------------------------------------------------------------------------------
 template <int NA, int NB, int STAGES, int WN>
 __global__ void __launch_bounds__(512) k_wgrad2(const zp_wgrad_args A, float* __restrict__ ws, int pix_per_split,
@@ -2406,6 +2412,7 @@ __global__ void __launch_bounds__(512) k_wgrad2(const zp_wgrad_args A, float* __
   const int cout8 = (A.Cout + 7) & ~7;
   const int rh = W == 32 ? (wid >> 2) : 0;  // image-row offset of this wave's rows (wave-uniform)
   const int gxl = W == 32 ? (R & 31) : R;   // column (W 128: + 64 * xh)
+  const int SS = A.sy;                      // input stride (1, or 2 with IH = 2 GH, IW = 2 GW)
   // per panel: lane offsets (dy: row + channel; x: row + tap + channel, with column validity folded
   // in as an out-of-range offset), tap row of x panels (wave-uniform)
   unsigned vdy[NA];
@@ -2425,9 +2432,9 @@ __global__ void __launch_bounds__(512) k_wgrad2(const zp_wgrad_args A, float* __
     const int ci = col - t * A.Cin;
     const int ty = S.ty[t], tx = S.tx[t];
     tyP[P] = __builtin_amdgcn_readfirstlane(S.ty[(col0 + 64 * P) / A.Cin < S.ntaps ? (col0 + 64 * P) / A.Cin : 0]);
-    vx[P] = (R + ty * A.IW + tx) * A.ldx * 2 + (A.cx0 + ci) * 2;
-    okx0[P] = ok && (unsigned)(gxl + tx) < (unsigned)W;
-    okx1[P] = ok && (unsigned)(gxl + 64 + tx) < (unsigned)W;
+    vx[P] = ((SS * rh + ty) * A.IW + SS * gxl + tx) * A.ldx * 2 + (A.cx0 + ci) * 2;
+    okx0[P] = ok && (unsigned)(SS * gxl + tx) < (unsigned)A.IW;
+    okx1[P] = ok && (unsigned)(SS * (gxl + 64) + tx) < (unsigned)A.IW;
   }
 #if defined(__HIP_DEVICE_COMPILE__)
   const __amdgpu_buffer_rsrc_t xrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)A.x, (short)0, (int)WB.x_bytes, 0x00020000);
@@ -2435,7 +2442,7 @@ __global__ void __launch_bounds__(512) k_wgrad2(const zp_wgrad_args A, float* __
 #endif
   // scalar walk: pixel p of the next step to issue, its image row gy and (W 128) column half xh
   int p_is = pbeg;
-  int gy_is, xh_is;
+  int gy_is, xh_is, n_is = pbeg / GHW;
   {
     const int r = pbeg % GHW;
     gy_is = r / W;
@@ -2444,7 +2451,8 @@ __global__ void __launch_bounds__(512) k_wgrad2(const zp_wgrad_args A, float* __
   const int ldy2 = S.lddy * 2, ldx2 = A.ldx * 2;
   auto issue = [&](auto slot_c) {
     constexpr int SL = decltype(slot_c)::value;
-    const int sdy = p_is * ldy2, sx = p_is * ldx2;
+    const int sdy = p_is * ldy2;
+    const int sx = ((n_is * A.IH + SS * gy_is) * A.IW + SS * 64 * xh_is) * ldx2;  // (S 1: p_is * ldx2)
 #if defined(__HIP_DEVICE_COMPILE__)
 #pragma unroll
     for (int P = 0; P < NA; ++P) {
@@ -2455,7 +2463,7 @@ __global__ void __launch_bounds__(512) k_wgrad2(const zp_wgrad_args A, float* __
     for (int P = 0; P < NB; ++P) {
       // the full (non-negative when valid) offset in the VGPR: a lane offset below zero is never
       // handed to the buffer unit, whatever its range check does with the scalar part
-      const bool rowok = (unsigned)(gy_is + rh + tyP[P]) < (unsigned)A.IH;  // wave-uniform
+      const bool rowok = (unsigned)(SS * (gy_is + rh) + tyP[P]) < (unsigned)A.IH;  // wave-uniform
       const bool ok = rowok && (xh_is ? okx1[P] : okx0[P]);
       const unsigned v = ok ? (unsigned)(vx[P] + sx) : 0x80000000u;
       auto* d = (__attribute__((address_space(3))) void*)((unsigned char*)lds + SL * SB + (NA + P) * PB + wid * 1024);
@@ -2470,7 +2478,10 @@ __global__ void __launch_bounds__(512) k_wgrad2(const zp_wgrad_args A, float* __
     } else {
       gy_is += KP / W;
     }
-    if (gy_is >= A.GH) gy_is = 0;
+    if (gy_is >= A.GH) {
+      gy_is = 0;
+      ++n_is;
+    }
   };
 
   f32x4 acc[4][4 * WN];
@@ -3104,6 +3115,10 @@ static int wgrad_cfg(const zp_wgrad_args& a) {
   static const int big = getenv("ZP_WGRAD_BIG") ? env_int("ZP_WGRAD_BIG") : 1;
   if (a.Cout <= 64) return 0;
   if (a.Cout < 256 || !big) return 1;
+  // (round 6) a Cout the 256-row tiles would pad by more than the 128-row ones (320: 512 against
+  // 384 rows -- the ConvT weight gradient as the stride-2 conv over dy) takes 128 x 256: measured
+  // 276 -> 261 us for up2's ConvT (tools/wgrad_ab.py, profiles/r06_conv_ablations.md)
+  if (big == 1 && (a.Cout + 255) / 256 * 256 > (a.Cout + 127) / 128 * 128) return 1;
   if (big == 1 && wgrad2_eligible(a)) {
     long M = (long)a.N * a.GH * a.GW;
     int cm = 0;
@@ -3133,8 +3148,8 @@ static int num_cus() {
   return n;
 }
 static bool wgrad2_eligible(const zp_wgrad_args& a) {
-  if (!g_wgrad2 || a.dtype != ZP_BF16 || a.nsub != 1 || a.sy != 1 || a.sx != 1) return false;
-  if (a.IH != a.GH || a.IW != a.GW || (a.GW != 32 && a.GW != 64 && a.GW != 128)) return false;
+  if (!g_wgrad2 || a.dtype != ZP_BF16 || a.nsub != 1 || a.sy != a.sx || (a.sy != 1 && a.sy != 2)) return false;
+  if (a.IH != a.sy * a.GH || a.IW != a.sx * a.GW || (a.GW != 32 && a.GW != 64 && a.GW != 128)) return false;
   if (((long)a.GH * a.GW) % 64 != 0 || a.Cin % 64 != 0) return false;
   const auto& S = a.sub[0];
   return S.oys == 1 && S.oxs == 1 && S.oyo == 0 && S.oxo == 0 && S.OH == a.GH && S.OW == a.GW;

@@ -166,6 +166,7 @@ class Engine:
         # kernel is L2/MFMA-bound, the BN passes HBM-bound; both fill the other's tail).  The
         # streams join at the end of backward().  ZP_SIDE_WGRAD=0 keeps everything on one stream.
         self.side_wgrad = os.environ.get("ZP_SIDE_WGRAD", "1") != "0"
+        self.convT_wgrad_swap = os.environ.get("ZP_CONVT_WGRAD_SWAP", "1") != "0"
         self._side = None
         self._side_used = False
         self.bn_mask_from_raw = True  # BN+ReLU backward without residual: mask from raw (A/B knob)
@@ -660,17 +661,31 @@ class Engine:
             g.zero_()
         return Act(g, act.c0, act.C), True
 
+    def _convT_wgrad_swap(self, unit, x: Act, dy: Act):
+        """True when a ConvTranspose2d(3, s2, p1, op1) weight gradient runs as the stride-2 conv's
+        over dy with x as its output gradient (zp_conv.hip k_wgrad2, stride 2): dW[ci][co][ky][kx] =
+        sum_g x[g][ci] dy[2 g + (ky, kx) - 1][co], the ConvT weight's own [in][out][k][k] layout.
+        16-bit only (the lean kernel's dtype); the four-phase form otherwise (ZP_CONVT_WGRAD_SWAP=0)."""
+        return (self.convT_wgrad_swap and unit.kind == "convT" and self.dt == L.ZP_BF16
+                and (unit.k, unit.s, unit.p, unit.conv.output_padding[0]) == (3, 2, 1, 1)
+                and x.C == unit.cin_w and (dy.H, dy.W) == (2 * x.H, 2 * x.W))
+
     def _wgrad(self, unit, x: Act, plan, dy: Act, dw):
+        # (i, o): the launch's input and output-gradient activations; (x, dy) unless exchanged
+        i_act, o_act, cout, cw, tw = x, dy, unit.cout, unit.cin_w, 1 if unit.kind == "convT" else 0
+        if self._convT_wgrad_swap(unit, x, dy):
+            plan = G.convT_dgrad(x.H, x.W, unit.k, unit.s, unit.p)
+            i_act, o_act, cout, cw, tw = dy, x, unit.cin_w, unit.cout, 0
         a = L.WgradArgs()
         a.dtype = self.dt
-        a.x, a.ldx, a.cx0, a.IH, a.IW, a.Cin = x.ptr, x.ld, x.c0, x.H, x.W, x.C
-        a.N, a.GH, a.GW, a.sy, a.sx = x.B, plan.GH, plan.GW, plan.sy, plan.sy
-        a.Cout, a.Cw, a.kh, a.kw = unit.cout, unit.cin_w, unit.k, unit.k
-        a.transposed_w = 1 if unit.kind == "convT" else 0
+        a.x, a.ldx, a.cx0, a.IH, a.IW, a.Cin = i_act.ptr, i_act.ld, i_act.c0, i_act.H, i_act.W, i_act.C
+        a.N, a.GH, a.GW, a.sy, a.sx = i_act.B, plan.GH, plan.GW, plan.sy, plan.sy
+        a.Cout, a.Cw, a.kh, a.kw = cout, cw, unit.k, unit.k
+        a.transposed_w = tw
         a.nsub = len(plan.subs)
         for i, sb in enumerate(plan.subs):
             s = a.sub[i]
-            s.dy, s.lddy, s.cdy0, s.OH, s.OW = dy.ptr, dy.ld, dy.c0, dy.H, dy.W
+            s.dy, s.lddy, s.cdy0, s.OH, s.OW = o_act.ptr, o_act.ld, o_act.c0, o_act.H, o_act.W
             s.oys, s.oyo, s.oxs, s.oxo = sb.oys, sb.oyo, sb.oxs, sb.oxo
             s.ntaps = len(sb.taps)
             for t, ((ky, kx), (ty, tx)) in enumerate(zip(sb.taps, sb.offs)):
