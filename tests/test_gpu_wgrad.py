@@ -37,14 +37,17 @@ GEOMS = [
 ]
 
 
-@pytest.mark.parametrize("swap", [True, False], ids=["swap", "phases"])
-@pytest.mark.parametrize("geom", GEOMS, ids=[f"{g[0]}{g[1]}-{g[3]}k{g[4]}s{g[5]}d{g[7]}H{g[8]}" for g in GEOMS])
+# (geometry, swap): the ConvTs both ways -- as the stride-2 conv over dy and as four phases
+CASES = [(g, True) for g in GEOMS] + [(g, False) for g in GEOMS if g[0] == "convT"]
+
+
+@pytest.mark.parametrize("geom,swap", CASES, ids=[f"{g[0]}{g[1]}-{g[3]}k{g[4]}s{g[5]}d{g[7]}H{g[8]}"
+                                                  + ("" if g[0] == "conv" else ("-swap" if sw else "-phases"))
+                                                  for g, sw in CASES])
 def test_wgrad_bf16(gpu, geom, swap):
     from zebrapose_amd.engine import Engine, Unit, Act
     from zebrapose_amd.model import layers as LY
     kind, cin, cw, cout, k, s, p, d, H, B = geom
-    if kind == "conv" and not swap:
-        pytest.skip("the exchange applies to ConvTranspose2d only")
     torch.manual_seed(3)
     if kind == "conv":
         conv = LY.Conv2d(cw, cout, k, s, p, d, bias=False)
