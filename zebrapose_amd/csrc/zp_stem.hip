@@ -231,6 +231,22 @@ __global__ void __launch_bounds__(256) k_stem_h2(const float* __restrict__ x, in
 
 using namespace zp;
 
+// zp_conv_tuning key 20: persistent stem workgroups per CU (1 or 2; -1: ZP_STEM_WGS or 1).  Measured
+// (whole fp32 forward, bs 32, hipGraph, tools/bs1_ab.py): 9.392 ms with one, 9.419 with two -- one stays
+static int g_stem_wgs = -1;
+namespace zp {
+int stem_wgs_mode(int v) {
+  const int old = g_stem_wgs;
+  g_stem_wgs = v;
+  return old;
+}
+}  // namespace zp
+static int stem_wgs_per_cu() {
+  static const int env = getenv("ZP_STEM_WGS") ? atoi(getenv("ZP_STEM_WGS")) : 1;
+  const int v = g_stem_wgs >= 0 ? g_stem_wgs : env;
+  return v == 2 ? 2 : 1;
+}
+
 extern "C" int zp_stem_split(const float* x, int B, int H, int W, int ldx, const void* w, int w_rows, int k_pad,
                              const float* scale, const float* shift, int dtype, void* y, int ldy, int cy0, int OH,
                              int OW, void* stream) {
@@ -266,9 +282,11 @@ extern "C" int zp_stem_split(const float* x, int B, int H, int W, int ldx, const
     attr[dev] = true;
   }
   const long tiles = (long)B * OH * OW / 256;
-  // one workgroup per CU (the tile loop holds ~300-400 VGPRs: one wave per SIMD), each walking
-  // ~tiles / CUs tiles with the next tile's region in flight during the current one's MFMAs
-  const unsigned grid = (unsigned)(tiles < (long)cus[dev] ? tiles : (long)cus[dev]);
+  // persistent workgroups, each walking ~tiles / grid tiles with the next tile's region in flight
+  // during the current one's MFMAs: stem_wgs_per_cu() per CU (zp_conv_tuning key 20; 200 VGPRs and
+  // ~69 KB of LDS let two share a CU)
+  const long wgs = (long)cus[dev] * stem_wgs_per_cu();
+  const unsigned grid = (unsigned)(tiles < wgs ? tiles : wgs);
   const long psy = (long)B * OH * OW * ldy;
   if (ldx == 0)
     hipLaunchKernelGGL(k_stem_h2<true>, dim3(grid), dim3(256), lds, (hipStream_t)stream, x, B, H, W, ldx,
