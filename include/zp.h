@@ -187,7 +187,9 @@ long long zp_conv2d_split_ws(const zp_conv_args* a);
  * multi-sub launches (ConvT phases) with a pixel tile's phases adjacent on one XCD (default 0); key 18
  * = the 256 x 256 two-plane tile on 32x32x16 MFMAs (default 0); key 19 = the ring depth (2, 3, 4) of
  * the register-pipelined two-plane 64-channel tile (default 2); key 20 = persistent workgroups per CU
- * of the two-plane stem (1 or 2, default 1).  Returns the previous value, -1 for an unknown key. */
+ * of the two-plane stem (1 or 2, default 1); key 21 = the wide strip tile's next-step pixel fragments
+ * read before the step's barrier (1, default) or after it (0).  Returns the previous value, -1 for an
+ * unknown key. */
 int zp_conv_tuning(int key, int value);
 
 /* Fused 1x1 head (the reference's conv_1x1_4 over torch.cat([x, x_128]) and the mask / code split,

@@ -595,10 +595,13 @@ def test_schedule_flags_are_bit_identical(gpu, geom, B, kernel, tp128):
     old14 = L.lib.zp_conv_tuning(14, tp128)
     try:
         # (round 6) "subint1": zp_conv_tuning key 17 = 1, the ConvT phases interleaved per pixel tile on
-        # one XCD instead of dispatched phase by phase (the default)
-        for extra in [0] + _BITWISE_FLAGS + ["subint1"]:
-            old = L.lib.zp_conv_tuning(1, 478 + (0 if extra == "subint1" else extra))
+        # one XCD instead of dispatched phase by phase (the default); "pfb0": key 21 = 0, the strip
+        # tile's next-step pixel fragments read after the step's barrier instead of before it
+        for extra in [0] + _BITWISE_FLAGS + ["subint1", "pfb0"]:
+            named = extra in ("subint1", "pfb0")
+            old = L.lib.zp_conv_tuning(1, 478 + (0 if named else extra))
             old17 = L.lib.zp_conv_tuning(17, 1 if extra == "subint1" else -1)
+            old21 = L.lib.zp_conv_tuning(21, 0 if extra == "pfb0" else -1)
             try:
                 oa = Act(eng._empty((B, OH, OW, cout), gpu))
                 eng.stage_log = []
@@ -607,13 +610,14 @@ def test_schedule_flags_are_bit_identical(gpu, geom, B, kernel, tp128):
             finally:
                 L.lib.zp_conv_tuning(1, old)
                 L.lib.zp_conv_tuning(17, old17)
+                L.lib.zp_conv_tuning(21, old21)
             outs[extra] = oa.buf._base.clone()
     finally:
         L.lib.zp_conv_tuning(14, old14)
     names = [r[1] for r in eng.stage_log]
     print(geom, names)
     assert names == [kernel], names
-    for extra in _BITWISE_FLAGS + ["subint1"]:
+    for extra in _BITWISE_FLAGS + ["subint1", "pfb0"]:
         assert torch.equal(outs[extra], outs[0]), (geom, extra)
 
 

@@ -43,6 +43,8 @@ def main():
     ap.add_argument("--tp128", default="-1", help="zp_conv_tuning key 14 values to A/B (k_conv3w 256 x 128 tile: 0, 1)")
     ap.add_argument("--subint", default="-1", help="zp_conv_tuning key 16 values to A/B (k_conv3 multi-sub interleave: 0, 1)")
     ap.add_argument("--mf32", default="-1", help="zp_conv_tuning key 18 values to A/B (k_conv3w on 32x32x16 MFMAs: 0, 1)")
+    ap.add_argument("--pfb", default="-1", help="zp_conv_tuning key 21 values to A/B (k_conv3w strip tile: next-step "
+                    "pixel fragments read before the barrier: 0, 1)")
     ap.add_argument("--graph", action="store_true", help="time hipGraph replays of the iters launches (no host "
                     "launch overhead: the bs = 1 launches are shorter than their eager enqueue)")
     ap.add_argument("--wsubint", default="-1", help="zp_conv_tuning key 17 values to A/B (k_conv3w ConvT phases "
@@ -97,11 +99,12 @@ def main():
     sis = [int(m) for m in a.subint.split(",")]
     wsis = [int(m) for m in a.wsubint.split(",")]
     mfs = [int(m) for m in a.mf32.split(",")]
+    pfbs = [int(m) for m in a.pfb.split(",")]
     first = {}
     import itertools
     for r in range(a.rounds):
-        for f0, mb, sm, wd, sk, ac, tq, si, ws, mf in itertools.product(flags, mbs, strips, wides, sks, accs, t128,
-                                                                         sis, wsis, mfs):
+        for f0, mb, sm, wd, sk, ac, tq, si, ws, mf, pb in itertools.product(flags, mbs, strips, wides, sks, accs, t128,
+                                                                             sis, wsis, mfs, pfbs):
             L.lib.zp_conv_tuning(1, f0)
             L.lib.zp_conv_tuning(8, mb)
             L.lib.zp_conv_tuning(7, sm)
@@ -112,7 +115,8 @@ def main():
             L.lib.zp_conv_tuning(16, si)
             L.lib.zp_conv_tuning(17, ws)
             L.lib.zp_conv_tuning(18, mf)
-            f = (f0, mb, sm, wd, sk, ac, tq, si, ws, mf)
+            L.lib.zp_conv_tuning(21, pb)
+            f = (f0, mb, sm, wd, sk, ac, tq, si, ws, mf, pb)
             for name, eng, unit, x, y, fl in setups:
                 def run1():
                     if hasattr(unit, "outs"):
@@ -165,10 +169,11 @@ def main():
     L.lib.zp_conv_tuning(16, -1)
     L.lib.zp_conv_tuning(17, -1)
     L.lib.zp_conv_tuning(18, -1)
+    L.lib.zp_conv_tuning(21, -1)
     for (name, f), v in sorted(res.items()):
         fl = [s[5] for s in setups if s[0] == name][0]
         us = min(v)
-        print(f"{name:8s} flags {f[0]:6d} minblocks {f[1]:4d} strip {f[2]:2d} wide {f[3]:2d} splitk {f[4]} acc {f[5]:2d} tp128 {f[6]:2d} subint {f[7]:2d} wsubint {f[8]:2d} mf32 {f[9]:2d}: {us:9.1f} us  {fl / us * 1e-6:7.1f} TFLOP/s  ({fl / us * 1e-6 / (2516.6 / (6 if a.form == 'x3' else 3)):.3f} of the {a.form} ceiling)")
+        print(f"{name:8s} flags {f[0]:6d} minblocks {f[1]:4d} strip {f[2]:2d} wide {f[3]:2d} splitk {f[4]} acc {f[5]:2d} tp128 {f[6]:2d} subint {f[7]:2d} wsubint {f[8]:2d} mf32 {f[9]:2d} pfb {f[10]:2d}: {us:9.1f} us  {fl / us * 1e-6:7.1f} TFLOP/s  ({fl / us * 1e-6 / (2516.6 / (6 if a.form == 'x3' else 3)):.3f} of the {a.form} ceiling)")
 
 
 if __name__ == "__main__":

@@ -3368,7 +3368,8 @@ extern "C" int zp_conv2d_config(const zp_conv_args* a, int* tc, int* tp, int* st
  * longest first (0, default: measured faster; -1 = ZP_CONV3W_SUBINT); key 18: k_conv3w's 256 x 256 tile
  * on v_mfma_f32_32x32x16_f16 (k_conv3w32; 1) or 16 x 16 x 32 (0, default; -1 = ZP_CONV3W_MF32);
  * key 19: ring depth (2, 3, 4) of k_conv3's register-pipelined two-plane 64-channel tile (-1 =
- * ZP_CONV3_PIPE_ST or 2, the default: measured fastest); key 20: persistent workgroups per CU of the two-plane stem (1 or 2; -1 = ZP_STEM_WGS or 1).
+ * ZP_CONV3_PIPE_ST or 2, the default: measured fastest); key 20: persistent workgroups per CU of the two-plane stem (1 or 2; -1 = ZP_STEM_WGS or 1); key 21: the wide strip tile's next-step pixel
+ * fragments read before the step's barrier (1) or after it (0; -1 = ZP_CONV3W_PFB or 1).
  * Returns the previous value. */
 /* split-fp32 split-K workspace: bytes of f32 slices zp_conv2d uses for these args when a.stats
  * points to that many (0: the launch is not split) */
@@ -3423,6 +3424,7 @@ extern "C" int zp_conv_tuning(int key, int value) {
   if (key == 18) return conv3w_mf32_mode(value);
   if (key == 19) return conv3_pipe_st_mode(value);
   if (key == 20) return stem_wgs_mode(value);
+  if (key == 21) return conv3w_pfb_mode(value);
   if (key == 4) {
     const int old = g_wgrad2_rounds;
     g_wgrad2_rounds = value > 0 ? value : 1;

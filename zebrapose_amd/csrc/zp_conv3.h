@@ -13,6 +13,7 @@ int conv3_nsplit(const zp_conv_args& a);          // split-K slices (1: none)
 int conv3_subint_mode(int v);                     // zp_conv_tuning key 16; returns the previous value
 int conv3_pipe_st_mode(int v);                    // zp_conv_tuning key 19; returns the previous value
 int stem_wgs_mode(int v);                         // zp_conv_tuning key 20; returns the previous value
+int conv3w_pfb_mode(int v);                       // zp_conv_tuning key 21; returns the previous value
 int conv3_launch(const zp_conv_args& a, hipStream_t st, int flags, const zp_head_args* head = nullptr);
 // k_conv3w (zp_conv3w.hip): the 256 x 256 two-plane tile
 struct conv_taps;

@@ -73,8 +73,18 @@ __device__ __forceinline__ void wbarrier() {
 //   strip is issued a step and a half before its first use.
 // SA: one scaled accumulator per block (see the numerics note above); SA = false: k_conv3's
 //   correction accumulator c2, flushed one cout block later (acc = fma(c2, 2^-11, acc))
+#ifdef ZP_STAMP
+// Diagnostic build only (tools/stamp_build.sh -> tools/stamp/libzp_stamp.so, loaded through ZP_LIB; the
+// product libzp.so never defines ZP_STAMP): per wave of the plain wide tile, the shader clock
+// (s_memtime) summed over the K loop's segments -- [0] step start -> first fragments landed,
+// [1] -> end of the step's MFMA blocks, [2] -> the next step's DMA landed (vm_wait), [3] -> past the
+// barrier -- and [4] the whole K loop, written by lane 0 of every wave of the LAST launch.
+constexpr int ZP_STAMP_WAVES = 1 << 17;
+__device__ unsigned long long zp_stamp_buf[ZP_STAMP_WAVES * 8];
+#endif
+
 template <int ABL, int DM, bool HEAD, bool SGB = false, bool PF = false, bool BF = false, bool STR = false,
-          int NUM = ACC_FLUSH, int TPX = 256>
+          int NUM = ACC_FLUSH, int TPX = 256, bool PFB = false>
 __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv_taps TG, const int flags,
                                                 const zp_head_args H, float* __restrict__ ws, const int nsplit) {
   constexpr int NPL = 2;
@@ -84,6 +94,14 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
   constexpr bool SA = NUM == ACC_SA || NUM == ACC_PS || NUM == ACC_FS;  // accumulators on the 2^11 scale
   constexpr bool P2 = NUM == ACC_P2;
   static_assert(!P2 || (TPX == 128 && !HEAD), "the persistent correction accumulator: 256 x 128 tiles");
+  // PFB (round 6, zp_conv_tuning key 21): the next step's pixel fragments read from the strip BEFORE the
+  // barrier that ends a step -- by plain LDS loads the compiler tracks (they are carried across the
+  // barrier and the loop edge) -- instead of after it, where all eight waves' fragment reads hit the
+  // LDS at once (shader-clock stamps: ~16% of the K loop from a step's start to its first fragments,
+  // tools/stamp_conv3w.py).  Legal for 3 x 3 convs (three tap columns): the next step reads the current
+  // strip, or the next group's, issued in the group's first step and complete and visible since the
+  // barrier of its second.  One sub, no split-K (conv3w_launch checks)
+  static_assert(!PFB || (STR && !P2 && NUM == ACC_FLUSH && TPX == 256), "pixel-fragment prefetch: the strip tile");
   constexpr int NTW = TC / 16, NT = (TC + TP) / 16;  // weight tiles / all tiles per plane (16 rows each)
   constexpr int UNITS = NPL * NT;                    // 1 KB DMA units per stage
   constexpr int WC = 8, WP = TP / 64;                // per wave: 8 cout blocks x 4 (TP 128: 2) pixel blocks
@@ -303,6 +321,27 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
   const unsigned sl0 = lds_addr(lds) + (unsigned)(2 * ASTG) * 1024u + (unsigned)(lane >> 4) * 256u;
 
   f32x4 acc[WC][WP];
+#ifdef ZP_STAMP
+  constexpr bool STAMP = !HEAD && NUM == ACC_FLUSH && TPX == 256 && ABL == 0;
+  unsigned long long st_seg[4] = {0, 0, 0, 0}, st_t = 0, st_loop0 = 0;
+  auto stamp = [&](int k) {
+    if constexpr (STAMP) {
+      const unsigned long long now = __builtin_amdgcn_s_memtime();
+      if (k >= 0) st_seg[k] += now - st_t;
+      st_t = now;
+    }
+  };
+#define ZP_STAMP_AT(k)                  \
+  do {                                  \
+    __builtin_amdgcn_sched_barrier(0);  \
+    stamp(k);                           \
+    __builtin_amdgcn_sched_barrier(0);  \
+  } while (0)
+#else
+#define ZP_STAMP_AT(k) \
+  do {                 \
+  } while (0)
+#endif
   // P2 (ACC_P2): the correction products' own running sums, one per block, for the whole K loop --
   // no per-step flush (4 v_fma_f32 per block and step, which with 2 waves per SIMD kept the vector
   // issue port ~95% busy beside the MFMAs: tools/conv3_ab.py ablations)
@@ -347,6 +386,21 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
       asm volatile("" : "+v"(a[j]));
     }
   };
+  uint4 bfo[NPL][WP];  // PFB: the pixel fragments of the step about to run
+  auto load_bf = [&](int gs, int txi) {
+    if constexpr (PFB) {
+      // (the strip fragment addresses of the asm reads below, as uint4 indices into lds)
+      const int base = 2 * ASTG * 64 + (lane >> 4) * 16 + gs * (NPL * SPMAX * 64);
+      const int sh = sh0 + txi * dtx;
+#pragma unroll
+      for (int j = 0; j < WP; ++j) {
+        const int sp = sj[j] + sh;
+        const int ix = base + (sp >> 4) * 64 + (sp & 15);
+#pragma unroll
+        for (int p = 0; p < NPL; ++p) bfo[p][j] = lds[ix + p * SPMAX * 64];
+      }
+    }
+  };
   auto step = [&](auto s_c, const bool more, const bool strip_now) {
     const int s = (int)s_c;  // (a compile-time stage, or -- P2's one-step loop -- a runtime one)
     // the next step's DMA (into the other buffer: every wave has passed the barrier that ended the
@@ -360,9 +414,11 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
       dn.koff = 0;
     }
     const unsigned ab = s ? abase1 : abase0, bb = s ? bbase1 : bbase0;
-    uint4 bf[NPL][WP];
+    uint4 bfl[NPL][WP];
+    uint4(&bf)[NPL][WP] = *(PFB ? &bfo : &bfl);  // PFB: loaded by the previous step / the prologue
     uint4 af[3][NPL];  // weight fragments: a 3-slot ring
-    if constexpr (STR) {  // pixel fragments from the strip: 16 consecutive strip pixels, conflict-free
+    if constexpr (PFB) {
+    } else if constexpr (STR) {  // pixel fragments from the strip: 16 consecutive strip pixels, conflict-free
       const unsigned sb = sl0 + (unsigned)r_gs * (unsigned)(NPL * SPMAX * 1024);
       const int sh = sh0 + r_txi * dtx;
       static_for<WP>([&](auto j_c) {
@@ -403,6 +459,7 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
       constexpr int after = (i + 1 < WC ? NPL : 0) + (i + 2 < WC ? NPL : 0);
       asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(after) : "memory");
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr (i == 0) ZP_STAMP_AT(0);
       // NUM 2 (ACC_PS): the three products of the block, on the 2^11 scale, into a fresh c2 --
       // lo'*hi + hi*lo' + (2^11 hi)*hi, the small terms first -- and acc += c2 (v_add_f32, round to
       // nearest) one cout block later.  NUM 1 (ACC_SA): the same three products straight into acc.
@@ -473,6 +530,17 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
       __builtin_amdgcn_sched_barrier(0);
     });
     if constexpr (NUM == ACC_FLUSH || NUM == ACC_FS) flush(acc[WC - 1], c2p);
+    ZP_STAMP_AT(1);
+    if constexpr (PFB) {  // the next step's pixel fragments (past the last step: harmless reads, unused)
+      int ntxi = r_txi + 1, ngs = r_gs;
+      if (ntxi == nx) {
+        ntxi = 0;
+        ngs ^= 1;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      load_bf(ngs, ntxi);
+      __builtin_amdgcn_sched_barrier(0);
+    }
   };
 
   // prologue: step 0's DMA into buffer 0 (STR: and group 0's strip into strip stage 0)
@@ -481,6 +549,7 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
   vm_wait<0>();
   wbarrier();
   __builtin_amdgcn_sched_barrier(0);
+  if constexpr (PFB) load_bf(r_gs, r_txi);
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
   if (flags & 65536) {  // static priority for the second-dispatched half (MI355X_MICROARCH.md item 4)
@@ -492,8 +561,10 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
     if (STR && sn && nx > 1) vm_wait<4>();  // (one-column groups: the strip is read at the next step)
     else vm_wait<0>();
     asm volatile("" ::"v"(pf_sink));  // the prefetch's (discarded) value: consumed after the wait
+    ZP_STAMP_AT(2);
     if constexpr (!abl_bar) wbarrier();
     __builtin_amdgcn_sched_barrier(0);
+    ZP_STAMP_AT(3);
     if constexpr (STR) {
       if (++r_txi == nx) {
         r_txi = 0;
@@ -509,7 +580,11 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
       step(ks & 1, ks + 1 < nK, sn);
       end_step(sn);
     }
-  } else
+  } else {
+#ifdef ZP_STAMP
+  ZP_STAMP_AT(-1);
+  st_loop0 = st_t;
+#endif
   for (int ks = 0; ks < nK; ks += 2) {
     // step ks on buffer 0, issuing the DMA of step ks + 1 into buffer 1
     const bool sn0 = STR && r_txi == 0 && ks + nx < nK;
@@ -520,6 +595,18 @@ __global__ void __launch_bounds__(512) k_conv3w(const zp_conv_args A, const conv
     step(I1{}, ks + 2 < nK, sn1);
     end_step(sn1);
   }
+#ifdef ZP_STAMP
+  if constexpr (STAMP) {
+    const unsigned long long tot = __builtin_amdgcn_s_memtime() - st_loop0;
+    const long wv = ((long)blockIdx.x + (long)gridDim.x * ((long)blockIdx.y + (long)gridDim.y * blockIdx.z)) * 8 + wid;
+    if (lane == 0 && wv < ZP_STAMP_WAVES) {
+      unsigned long long* o = zp_stamp_buf + wv * 8;
+      o[0] = st_seg[0]; o[1] = st_seg[1]; o[2] = st_seg[2]; o[3] = st_seg[3]; o[4] = tot; o[5] = (unsigned long long)nK;
+    }
+  }
+#endif
+  }
+#undef ZP_STAMP_AT
   if constexpr (P2) {  // the corrections join the main sums once: acc = fma(c2, 2^-11, acc) (one rounding)
 #pragma unroll
     for (int i = 0; i < WC; ++i)
@@ -923,6 +1010,30 @@ static bool conv3w_subint() {
   return (g_conv3w_subint >= 0 ? g_conv3w_subint : env) != 0;
 }
 
+#ifdef ZP_STAMP
+}  // namespace zp
+// diagnostic build only: copy the per-wave segment sums of the last plain wide-tile launch
+extern "C" int zp_stamp_read(unsigned long long* dst, long long n) {
+  if (n > (long long)zp::ZP_STAMP_WAVES * 8) n = (long long)zp::ZP_STAMP_WAVES * 8;
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(zp::zp_stamp_buf), (size_t)n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+namespace zp {
+#endif
+// zp_conv_tuning key 21: the strip tile's next-step pixel fragments read before the step's barrier
+// (PFB; 3 x 3 one-sub launches without split-K).  -1: ZP_CONV3W_PFB or 1.  Measured (tools/conv3_ab.py
+// --pfb 0,1, 5 rounds, bit-identical): layer5 326.5 -> 324.3 us, up1's 3x3 350.3 -> 347.3, up2's
+// 1418.1 -> 1414.7; stamps: the step-start wait 15.8% -> 5.8% of the K loop, most of it moved to the
+// DMA wait the compiler puts before the plain LDS loads (2.1% -> 7.9%), 4741 -> 4660 cycles per step
+static int g_conv3w_pfb = -1;
+int conv3w_pfb_mode(int v) {
+  const int old = g_conv3w_pfb;
+  g_conv3w_pfb = v;
+  return old;
+}
+static bool conv3w_pfb_on() {
+  static const int env = getenv("ZP_CONV3W_PFB") ? atoi(getenv("ZP_CONV3W_PFB")) : 1;
+  return (g_conv3w_pfb >= 0 ? g_conv3w_pfb : env) != 0;
+}
 void conv3w_launch(const zp_conv_args& a0, const conv_taps& tg0, hipStream_t st, int fl, float* ws, int ns) {
   // several sub-problems (the ConvT phases: 1 / 2 / 2 / 4 taps): dispatched longest first (the
   // dispatcher walks blockIdx.z slowest, so the 4-tap phase's workgroups start first and the
@@ -997,7 +1108,9 @@ void conv3w_launch(const zp_conv_args& a0, const conv_taps& tg0, hipStream_t st,
   } else if (acc == ACC_FS) {  // the flushed form on the 2^11 scale
     if (str) hipLaunchKernelGGL((k_conv3w<0, 1, false, false, false, false, true, ACC_FS>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
     else hipLaunchKernelGGL((k_conv3w<0, 1, false, false, false, false, false, ACC_FS>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
-  } else if (str)  // the default: k_conv3's flushed correction accumulator (bit-identical to k_conv3<h2>)
+  } else if (str && ns == 1 && a.nsub == 1 && tg.nx[0] == 3 && conv3w_pfb_on())  // (key 21: pixel-fragment prefetch)
+    hipLaunchKernelGGL((k_conv3w<0, 1, false, false, false, false, true, ACC_FLUSH, 256, true>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
+  else if (str)  // the default: k_conv3's flushed correction accumulator (bit-identical to k_conv3<h2>)
     hipLaunchKernelGGL((k_conv3w<0, 1, false, false, false, false, true>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
   else hipLaunchKernelGGL((k_conv3w<0, 1, false>), grid, dim3(512), 0, st, a, tg, fl, H, ws, ns);
 }
